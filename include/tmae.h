@@ -1,0 +1,143 @@
+/*
+ * tmae.h — C ABI of libtmae.so, the MI355X (gfx950) kernels behind the TextMAE MCM hot path.
+ *
+ * The reference path is pure Python on PyTorch + compressai + timm (no native code of its own).
+ * Each entry point below replaces the reference computation cited next to it; the Python host
+ * (textmae-image-compression_amd/mcm.py) calls these through ctypes exactly where the reference's
+ * nn.Module code runs (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *   - all pointers are device pointers (hipMalloc / torch caching allocator); the library never
+ *     allocates, never synchronises, and enqueues on `stream` (a hipStream_t, NULL = default);
+ *   - `dtype` selects the MFMA operand type: TMAE_F32 (exact f32 MFMA, parity path) or TMAE_BF16
+ *     (bf16 operands, f32 accumulate, throughput path); accumulation, residual stream, entropy
+ *     models and likelihoods are always f32;
+ *   - activations are row-major "token" matrices [rows][channels]; LIC feature maps are NHWC;
+ *     likelihood outputs are NCHW like the reference's tensors;
+ *   - return 0 on success, TMAE_EINVAL for a bad shape/argument, TMAE_EHIP for a launch error;
+ *     tmae_last_error_string() describes the last failure on the calling thread.
+ */
+#ifndef TMAE_H
+#define TMAE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TMAE_ABI_VERSION 1
+
+enum { TMAE_OK = 0, TMAE_EINVAL = 1, TMAE_EHIP = 2 };
+enum { TMAE_F32 = 0, TMAE_BF16 = 1 };
+enum { TMAE_ACT_NONE = 0, TMAE_ACT_GELU = 1 };
+
+const char* tmae_last_error_string(void);
+int tmae_abi_version(void);
+
+/* ---- masking -------------------------------------------------------------------------------
+ * MCM.get_ids_shuffle (models/Compression/MCM.py:364-423) + the argsort / keep-slice of
+ * MCM.random_masking (MCM.py:579-583).  scores [n][L] f32 -> ids_shuffle, ids_restore [n][L] i64.
+ * Bit-exact with the reference.  sum_lanes = torch CPU float-sum vector width (8 on x86 AVX2/512
+ * builds).  Raises TMAE_EINVAL for K > L exactly where MCM.py:374-376 raises. */
+int tmae_ids_shuffle(const float* scores, int64_t* ids_shuffle, int64_t* ids_restore, int n, int L, int K,
+                     int sum_lanes, void* stream);
+
+/* ---- transformer (timm 0.4.5 Block / PatchEmbed, used at MCM.py:300-348, 615-632, 657-686) ---- */
+
+/* LayerNorm(eps) over f32 rows; source row = (r / row_group) * group_stride + row_offset + r % row_group
+ * (drops cls rows without a copy: MCM.py:631-632).  y is f32 or bf16 (out_dtype). */
+int tmae_layernorm_fwd(const float* x, const float* gamma, const float* beta, void* y, int rows, int D,
+                       int row_group, int group_stride, int row_offset, float eps, int out_dtype, void* stream);
+
+/* y[M][N] = act(x[M][K] · w[N][K]^T + bias).  x is f32 (x_f32=1) or dtype; y is f32 (y_f32=1) or dtype.
+ * nn.Linear / 1x1 Conv2d (g_a, MCM.py:77-93) / 1x1 ConvTranspose2d with pre-transposed weight (g_s,
+ * MCM.py:96-112).  Same row remap as tmae_layernorm_fwd. */
+int tmae_linear_fwd(const void* x, int x_f32, int ldx, int row_group, int group_stride, int row_offset,
+                    const void* w, const float* bias, void* y, int y_f32, int ldy, int M, int N, int K, int act,
+                    int dtype, void* stream);
+
+/* resid[M][N] += x[M][K] · w[N][K]^T + bias   (Attention.proj / Mlp.fc2 + the Block residual adds) */
+int tmae_linear_residual_fwd(const void* x, int ldx, const void* w, const float* bias, float* resid, int ldr,
+                             int M, int N, int K, int dtype, void* stream);
+
+/* PatchEmbed conv16/s16 + pos_embed + masking gather, over the KEPT patches only
+ * (MCM.py:615-621 then the gather at 585-586): tokens [n][keep+1][D], rows 1..keep written;
+ * w = proj.weight viewed [D][C*P*P]. */
+int tmae_patch_embed_fwd(const float* imgs, const int64_t* ids_shuffle, const void* w, const float* bias,
+                         const float* pos, float* tokens, int n, int C, int H, int W, int patch, int D, int L,
+                         int keep, int dtype, void* stream);
+
+/* tokens[b][0] = cls_token + pos[0]  (MCM.py:624-626) */
+int tmae_cls_rows(float* tokens, const float* cls, const float* pos, int n, int rows_per_img, int D, void* stream);
+
+/* Fused multi-head attention over qkv [B*T][3*H*dh] (timm layout (3, H, dh)) -> out [B*T][H*dh];
+ * softmax((q k^T) * scale) v, dh in {32, 64}, T <= 512. */
+int tmae_mha_fwd(const void* qkv, void* out, int B, int T, int H, int dh, float scale, int dtype, void* stream);
+
+/* decoder_embed + mask-token unshuffle + decoder_pos_embed (MCM.py:657-675):
+ * x [n*ntok][Din] -> out [n][L+1][D]; token k -> row 0 (k=0) or 1 + ids_shuffle[b][k-1].
+ * ntok = K for MCM (cls already dropped: the reference's off-by-one), K+1 for MAE. */
+int tmae_decoder_embed_fwd(const void* x, int x_f32, const void* w, const float* bias, const float* pos,
+                           const int64_t* ids_shuffle, float* out, int n, int ntok, int L, int Din, int D,
+                           int dtype, void* stream);
+/* the rows the kept tokens do not cover: mask_token + pos (MCM.py:660-664) */
+int tmae_mask_rows(float* out, const float* mask_token, const float* pos, const int64_t* ids_shuffle, int n,
+                   int L, int ntok, int D, void* stream);
+
+/* decoder_pred + drop cls + unpatchify (MCM.py:683-686, 524-546, 795-797): x [n*L][Din] (rows 1..L of
+ * the decoder, cls excluded) -> imgs [n][C][H][W] f32 */
+int tmae_decoder_pred_fwd(const void* x, const void* w, const float* bias, float* imgs, int n, int L, int Din,
+                          int C, int H, int W, int patch, int dtype, void* stream);
+
+/* ---- learned-image-compression stack (MCM.py:729-792), NHWC f32 feature maps ------------------ */
+
+/* 3x3 conv, padding 1 (compressai conv3x3 / nn.Conv2d(k=3, p=1), MCM.py:115-293), input channels
+ * [0,c1) from x1 and [c1,c1+c2) from x2 (torch.cat without a copy).  w = [cout][3][3][c1+c2].
+ * pixel_shuffle=1: subpel_conv3x3 r=2 (conv + PixelShuffle(2)), output [n][2H][2W][cout/4]. */
+int tmae_conv3x3_fwd(const float* x1, int c1, int ld1, const float* x2, int c2, int ld2, int n, int H, int W,
+                     int stride, const void* w, const float* bias, float* y, int ldy, int cout, int act,
+                     int pixel_shuffle, int dtype, void* stream);
+
+/* last cc_transform_scale conv fused with GaussianConditional likelihood and y_hat quantisation
+ * (MCM.py:767-776): sigma = conv + bias; lik[NCHW, channels yoff..] = GC(y~, sigma, mu);
+ * yhat[NHWC] = round(y - mu) + mu.  noise (NCHW [n][Mtot][H][W]) selects training mode. */
+int tmae_conv3x3_gaussian_fwd(const float* x1, int c1, int ld1, const float* x2, int c2, int ld2, int n, int H,
+                              int W, const void* w, const float* bias, int cout, const float* y, int ldy, int yoff,
+                              const float* mu, int ldmu, const float* noise, float* lik, int Mtot, float* yhat,
+                              int ldh, int dtype, void* stream);
+
+/* last lrp_transform conv fused with y_hat += 0.5 * tanh(lrp) (MCM.py:779-784) */
+int tmae_conv3x3_lrp_fwd(const float* x1, int c1, int ld1, const float* x2, int c2, int ld2, int n, int H, int W,
+                         const void* w, const float* bias, int cout, const float* src, int ld_src, float* dst1,
+                         int ld_dst1, float* dst2, int ld_dst2, int dtype, void* stream);
+
+/* compressai EntropyBottleneck parameters (filters = (3, 3, 3, 3)), all f32 device pointers */
+typedef struct tmae_eb_params {
+  const float* matrix[5]; /* _matrix0 [C][3][1], _matrix1..3 [C][3][3], _matrix4 [C][1][3] */
+  const float* bias[5];   /* _bias0..3 [C][3][1], _bias4 [C][1][1] */
+  const float* factor[4]; /* _factor0..3 [C][3][1] */
+  const float* quantiles; /* [C][1][3] */
+} tmae_eb_params;
+
+/* EntropyBottleneck forward likelihood (MCM.py:741) + z_hat = round(z - median) + median
+ * (MCM.py:742-744).  z, zhat NHWC [n*HW][C]; lik, noise NCHW.  table: device scratch C*59 f32. */
+int tmae_eb_likelihood_fwd(const float* z, const tmae_eb_params* params, const float* noise, float* lik,
+                           float* zhat, float* table, int n, int C, int HW, void* stream);
+
+/* CompressionModel.aux_loss (utils/engine.py:79): out[0] = sum |f(quantiles) - target| */
+int tmae_eb_aux_loss(const tmae_eb_params* params, const float* target, float* out, float* table, int C,
+                     void* stream);
+
+/* GaussianConditional.forward, elementwise (same layout for all tensors) */
+int tmae_gc_likelihood_fwd(const float* x, const float* scales, const float* means, const float* noise,
+                           float* x_tilde, float* lik, int total, float scale_bound, void* stream);
+
+/* layout helper: NHWC (channel stride ldx) -> NCHW */
+int tmae_nhwc_to_nchw(const float* x, int ldx, float* y, int n, int C, int HW, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TMAE_H */

@@ -1,0 +1,81 @@
+// Shared definitions for the gfx950 (CDNA4 / MI355X) kernels behind libtmae.so.
+//
+// Everything here is written for one target: 64-lane wavefronts, MFMA matrix cores,
+// 160 KiB LDS per CU.  No CUDA dialect, no dual-platform macros.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tmae.h"
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+// ---------------------------------------------------------------- host-side error plumbing
+void tmae_set_error(int code, const char* fmt, ...);
+
+#define TMAE_REQUIRE(cond, ...)                           \
+  do {                                                    \
+    if (!(cond)) {                                        \
+      tmae_set_error(TMAE_EINVAL, __VA_ARGS__);           \
+      return TMAE_EINVAL;                                 \
+    }                                                     \
+  } while (0)
+
+#define TMAE_LAUNCH_CHECK(name)                                              \
+  do {                                                                       \
+    hipError_t _e = hipGetLastError();                                       \
+    if (_e != hipSuccess) {                                                  \
+      tmae_set_error(TMAE_EHIP, "%s: launch failed: %s", name,               \
+                     hipGetErrorString(_e));                                 \
+      return TMAE_EHIP;                                                      \
+    }                                                                        \
+    return TMAE_OK;                                                          \
+  } while (0)
+
+// ---------------------------------------------------------------- device helpers
+__device__ __forceinline__ float gelu_erf(float x) {
+  // nn.GELU() default (approximate='none'): 0.5 * x * (1 + erf(x / sqrt(2)))
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+template <typename T> __device__ __forceinline__ T to_out(float v);
+template <> __device__ __forceinline__ float to_out<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16 to_out<bf16>(float v) { return (bf16)v; }
+
+__device__ __forceinline__ float bf_to_f(bf16 v) { return (float)v; }
+
+// store 4 consecutive values (16 B for f32, 8 B for bf16)
+__device__ __forceinline__ void store4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ void store4(bf16* p, f32x4 v) {
+  bf16x4 o;
+  o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
+  *reinterpret_cast<bf16x4*>(p) = o;
+}
+__device__ __forceinline__ f32x4 load4f(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+__device__ __forceinline__ f32x4 load4f(const bf16* p) {
+  bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+
+// 16-byte chunk of 8 bf16 from 8 floats (two 16-B loads)
+__device__ __forceinline__ uint4 pack8_bf16(f32x4 a, f32x4 b) {
+  bf16x8 o;
+  o[0] = (bf16)a[0]; o[1] = (bf16)a[1]; o[2] = (bf16)a[2]; o[3] = (bf16)a[3];
+  o[4] = (bf16)b[0]; o[5] = (bf16)b[1]; o[6] = (bf16)b[2]; o[7] = (bf16)b[3];
+  return *reinterpret_cast<uint4*>(&o);
+}
+
+// XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+// blocks b and b+8 land on one XCD; give each XCD a contiguous run of logical tiles.
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }

@@ -1,0 +1,151 @@
+// Entropy-model kernels (compressai 1.2.4 semantics; the package is not vendored in the reference,
+// call sites MCM.py:71-72, 741-744, 771-776, utils/engine.py:79).
+//
+//  * EntropyBottleneck: per-channel monotone density MLP 1-3-3-3-3-1 (_logits_cumulative),
+//    likelihood |sigmoid(s*f(x+1/2)) - sigmoid(s*f(x-1/2))|, s = -sign(f(x+1/2) + f(x-1/2)),
+//    LowerBound(1e-9).  Input x = round(z - median) + median (eval) or z + U(-1/2, 1/2) (train).
+//    The parameter transforms softplus(matrix) / tanh(factor) are computed once per channel into a
+//    packed 59-float table (prep kernel), then one thread per latent element: memory-bound, coalesced
+//    over the NHWC z tensor.
+//  * GaussianConditional likelihood (standalone form; the slice loop uses the fused conv epilogue
+//    in gemm.hip).
+//  * aux_loss = sum |f(quantiles) - target|.
+#include "common.h"
+
+#define EB_PACK 59
+
+__device__ __forceinline__ float softplus_t(float x) {  // F.softplus(beta=1, threshold=20)
+  return x > 20.0f ? x : log1pf(expf(x));
+}
+__device__ __forceinline__ float sigmoid_t(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__global__ void eb_prep_kernel(tmae_eb_params p, float* __restrict__ tab, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float* t = tab + (size_t)c * EB_PACK;
+  for (int j = 0; j < 3; ++j) {
+    t[0 + j] = softplus_t(p.matrix[0][c * 3 + j]);
+    t[3 + j] = p.bias[0][c * 3 + j];
+    t[6 + j] = tanhf(p.factor[0][c * 3 + j]);
+  }
+  for (int l = 1; l <= 3; ++l) {
+    float* q = t + 9 + 15 * (l - 1);
+    for (int e = 0; e < 9; ++e) q[e] = softplus_t(p.matrix[l][c * 9 + e]);
+    for (int j = 0; j < 3; ++j) {
+      q[9 + j] = p.bias[l][c * 3 + j];
+      q[12 + j] = tanhf(p.factor[l][c * 3 + j]);
+    }
+  }
+  for (int k = 0; k < 3; ++k) t[54 + k] = softplus_t(p.matrix[4][c * 3 + k]);
+  t[57] = p.bias[4][c];
+  t[58] = p.quantiles[c * 3 + 1];  // _get_medians(): quantiles[:, :, 1:2]
+}
+
+__device__ __forceinline__ float eb_logits(const float* t, float v) {
+  float h0 = t[0] * v + t[3], h1 = t[1] * v + t[4], h2 = t[2] * v + t[5];
+  h0 += t[6] * tanhf(h0);
+  h1 += t[7] * tanhf(h1);
+  h2 += t[8] * tanhf(h2);
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const float* q = t + 9 + 15 * l;
+    float g0 = (q[0] * h0 + q[1] * h1 + q[2] * h2) + q[9];
+    float g1 = (q[3] * h0 + q[4] * h1 + q[5] * h2) + q[10];
+    float g2 = (q[6] * h0 + q[7] * h1 + q[8] * h2) + q[11];
+    g0 += q[12] * tanhf(g0);
+    g1 += q[13] * tanhf(g1);
+    g2 += q[14] * tanhf(g2);
+    h0 = g0; h1 = g1; h2 = g2;
+  }
+  return (t[54] * h0 + t[55] * h1 + t[56] * h2) + t[57];
+}
+
+// z, zhat: NHWC [n*HW][C]; lik, noise: NCHW [n][C][HW]
+__global__ void __launch_bounds__(256)
+eb_likelihood_kernel(const float* __restrict__ z, const float* __restrict__ tab, const float* __restrict__ noise,
+                     float* __restrict__ lik, float* __restrict__ zhat, int C, int HW, int total) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = i % C, m = i / C;
+  const int b = m / HW, pix = m - b * HW;
+  const float* t = tab + (size_t)c * EB_PACK;
+  const float med = t[58];
+  const float zv = z[i];
+  const float q = rintf(zv - med) + med;
+  const size_t nchw = ((size_t)b * C + c) * HW + pix;
+  const float x = noise ? zv + noise[nchw] : q;
+  const float lower = eb_logits(t, x - 0.5f);
+  const float upper = eb_logits(t, x + 0.5f);
+  const float sum = lower + upper;
+  const float sgn = sum > 0.0f ? -1.0f : (sum < 0.0f ? 1.0f : -0.0f);
+  const float l = fabsf(sigmoid_t(sgn * upper) - sigmoid_t(sgn * lower));
+  lik[nchw] = fmaxf(l, 1e-9f);
+  if (zhat) zhat[i] = q;  // quantize_ste forward value: round(z - med) + med  (MCM.py:742-744)
+}
+
+extern "C" int tmae_eb_likelihood_fwd(const float* z, const tmae_eb_params* params, const float* noise, float* lik,
+                                      float* zhat, float* table, int n, int C, int HW, void* stream) {
+  TMAE_REQUIRE(params != nullptr && table != nullptr, "tmae_eb_likelihood_fwd: params/table required");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, st, *params, table, C);
+  const int total = n * HW * C;
+  if (total > 0)
+    hipLaunchKernelGGL(eb_likelihood_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, z, table, noise, lik,
+                       zhat, C, HW, total);
+  TMAE_LAUNCH_CHECK("tmae_eb_likelihood_fwd");
+}
+
+// aux loss: sum_c sum_j |f_c(quantiles[c][j]) - target[j]|   (compressai EntropyBottleneck.loss)
+__global__ void __launch_bounds__(256)
+eb_aux_loss_kernel(const float* __restrict__ tab, const float* __restrict__ quantiles,
+                   const float* __restrict__ target, float* __restrict__ out, int C) {
+  __shared__ float red[256];
+  float s = 0.0f;
+  for (int i = threadIdx.x; i < C * 3; i += 256) {
+    const int c = i / 3, j = i - 3 * c;
+    s += fabsf(eb_logits(tab + (size_t)c * EB_PACK, quantiles[i]) - target[j]);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+extern "C" int tmae_eb_aux_loss(const tmae_eb_params* params, const float* target, float* out, float* table, int C,
+                                void* stream) {
+  TMAE_REQUIRE(params != nullptr && table != nullptr, "tmae_eb_aux_loss: params/table required");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, st, *params, table, C);
+  hipLaunchKernelGGL(eb_aux_loss_kernel, dim3(1), dim3(256), 0, st, table, params->quantiles, target, out, C);
+  TMAE_LAUNCH_CHECK("tmae_eb_aux_loss");
+}
+
+// GaussianConditional.forward (elementwise, identical layouts): outputs y~ and likelihood
+__global__ void __launch_bounds__(256)
+gc_likelihood_kernel(const float* __restrict__ x, const float* __restrict__ scales, const float* __restrict__ means,
+                     const float* __restrict__ noise, float* __restrict__ xt_out, float* __restrict__ lik, int total,
+                     float scale_bound) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const float mu = means ? means[i] : 0.0f;
+  const float xv = x[i];
+  const float xt = noise ? xv + noise[i] : (means ? rintf(xv - mu) + mu : rintf(xv));
+  const float s = fmaxf(scales[i], scale_bound);
+  const float val = fabsf(means ? xt - mu : xt);
+  const float c = -0.70710678118654752440f;
+  const float up = 0.5f * erfcf(c * ((0.5f - val) / s));
+  const float lo = 0.5f * erfcf(c * ((-0.5f - val) / s));
+  lik[i] = fmaxf(up - lo, 1e-9f);
+  if (xt_out) xt_out[i] = xt;
+}
+
+extern "C" int tmae_gc_likelihood_fwd(const float* x, const float* scales, const float* means, const float* noise,
+                                      float* x_tilde, float* lik, int total, float scale_bound, void* stream) {
+  if (total <= 0) return TMAE_OK;
+  hipLaunchKernelGGL(gc_likelihood_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x, scales,
+                     means, noise, x_tilde, lik, total, scale_bound);
+  TMAE_LAUNCH_CHECK("tmae_gc_likelihood_fwd");
+}

@@ -1,0 +1,81 @@
+// Small data-movement kernels around the GEMMs, plus the library's error plumbing.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.h"
+
+// ------------------------------------------------------------------ error state (thread-local)
+static thread_local char g_err[512] = "";
+
+void tmae_set_error(int code, const char* fmt, ...) {
+  (void)code;
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+extern "C" const char* tmae_last_error_string(void) { return g_err; }
+extern "C" int tmae_abi_version(void) { return TMAE_ABI_VERSION; }
+
+// ------------------------------------------------------------------ cls rows
+// tokens[b][0][:] = cls_token + pos[0]   (MCM.py:624-626 / models_mae.py forward_encoder)
+__global__ void cls_rows_kernel(float* __restrict__ tok, const float* __restrict__ cls, const float* __restrict__ pos,
+                                int n, int rows_per_img, int D) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * D) return;
+  const int b = i / D, d = i - b * D;
+  tok[(size_t)b * rows_per_img * D + d] = cls[d] + pos[d];
+}
+
+extern "C" int tmae_cls_rows(float* tokens, const float* cls, const float* pos, int n, int rows_per_img, int D,
+                             void* stream) {
+  if (n * D == 0) return TMAE_OK;
+  hipLaunchKernelGGL(cls_rows_kernel, dim3(ceil_div(n * D, 256)), dim3(256), 0, (hipStream_t)stream, tokens, cls, pos,
+                     n, rows_per_img, D);
+  TMAE_LAUNCH_CHECK("tmae_cls_rows");
+}
+
+// ------------------------------------------------------------------ decoder mask-token rows
+// For kept ranks m in [ntok-1, L): decoder row 1 + ids_shuffle[b][m] = mask_token + pos[row]
+// (MCM.py:660-675: the mask tokens land wherever ids_restore points past the kept tokens).
+__global__ void mask_rows_kernel(float* __restrict__ out, const float* __restrict__ mask,
+                                 const float* __restrict__ pos, const int64_t* __restrict__ ids, int n, int L,
+                                 int ntok, int D) {
+  const int nm = L - (ntok - 1);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int per_img = nm * (D / 4);
+  if (i >= n * per_img) return;
+  const int b = i / per_img, rem = i - b * per_img;
+  const int mi = rem / (D / 4), d = 4 * (rem - mi * (D / 4));
+  const int row = 1 + (int)ids[(size_t)b * L + (ntok - 1) + mi];
+  const f32x4 v = load4f(mask + d) + load4f(pos + (size_t)row * D + d);
+  store4(out + ((size_t)b * (L + 1) + row) * D + d, v);
+}
+
+extern "C" int tmae_mask_rows(float* out, const float* mask_token, const float* pos, const int64_t* ids_shuffle,
+                              int n, int L, int ntok, int D, void* stream) {
+  TMAE_REQUIRE(D % 4 == 0 && ntok >= 1 && ntok <= L + 1, "tmae_mask_rows: bad shape");
+  const int total = n * (L - (ntok - 1)) * (D / 4);
+  if (total <= 0) return TMAE_OK;
+  hipLaunchKernelGGL(mask_rows_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, out, mask_token,
+                     pos, ids_shuffle, n, L, ntok, D);
+  TMAE_LAUNCH_CHECK("tmae_mask_rows");
+}
+
+// ------------------------------------------------------------------ NHWC -> NCHW (fp32)
+__global__ void nhwc_to_nchw_kernel(const float* __restrict__ x, int ldx, float* __restrict__ y, int n, int C, int HW) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * C * HW) return;
+  const int pix = i % HW, t = i / HW;
+  const int c = t % C, b = t / C;
+  y[i] = x[((size_t)b * HW + pix) * ldx + c];
+}
+
+extern "C" int tmae_nhwc_to_nchw(const float* x, int ldx, float* y, int n, int C, int HW, void* stream) {
+  const int total = n * C * HW;
+  if (total <= 0) return TMAE_OK;
+  hipLaunchKernelGGL(nhwc_to_nchw_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, (hipStream_t)stream, x, ldx, y, n,
+                     C, HW);
+  TMAE_LAUNCH_CHECK("tmae_nhwc_to_nchw");
+}
