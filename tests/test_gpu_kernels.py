@@ -1,0 +1,258 @@
+"""Per-kernel parity: each HIP kernel vs a plain PyTorch fp32 CPU reference of the same op (or the
+oracle, for the masking and entropy models).  Tolerances: f32 MFMA path 1e-4 relative (it is an exact
+f32 fma chain; differences are summation order only), bf16 path 2e-2 relative (operand rounding);
+integer outputs bit-exact."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ids as ids_oracle
+from oracle import mcm_oracle as orc
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def tol(dtype):
+    return 1e-4 if dtype == torch.float32 else 2e-2
+
+
+DTYPES = [torch.float32, torch.bfloat16]
+
+
+# ------------------------------------------------------------------------------------ masking
+def test_ids_kernel_bit_exact_vs_reference_golden(golden_dir, tmae):
+    d = np.load(os.path.join(golden_dir, "ids_shuffle.npz"))
+    for k in sorted(d.files):
+        if not k.endswith("_scores"):
+            continue
+        key = k[: -len("_scores")]
+        K = int(key.split("_")[1][1:])
+        s = torch.from_numpy(d[k]).to(DEV)
+        shuf, rest = tmae.ops.ids_shuffle(s, K)
+        expect = d[key + "_ids"].astype(np.int64)
+        assert np.array_equal(shuf.cpu().numpy(), expect), key
+        assert np.array_equal(rest.cpu().numpy(), np.argsort(expect, axis=1)), key
+
+
+@pytest.mark.parametrize("L,K", [(256, 144), (196, 64), (1024, 400), (1, 1), (100, 0)])
+def test_ids_kernel_vs_oracle_random(tmae, L, K):
+    rng = np.random.default_rng(L + K)
+    s = np.concatenate([rng.random((64, L), dtype=np.float32),
+                        (rng.integers(0, 5, (64, L)) * rng.integers(1, 4, (64, L))).astype(np.float32) / 12.0])
+    shuf, rest = tmae.ops.ids_shuffle(torch.from_numpy(s).to(DEV), K)
+    es, er = ids_oracle.ids_shuffle(s, K)
+    assert np.array_equal(shuf.cpu().numpy(), es)
+    assert np.array_equal(rest.cpu().numpy(), er)
+
+
+def test_ids_kernel_rejects_k_gt_l(tmae):
+    with pytest.raises(ValueError, match="Number of patches"):
+        tmae.ops.ids_shuffle(torch.zeros(2, 16, device=DEV), 17)
+
+
+# ------------------------------------------------------------------------------------ transformer pieces
+@pytest.mark.parametrize("D", [768, 512, 64, 1024])
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_layernorm(tmae, D, dtype):
+    torch.manual_seed(D)
+    x = torch.randn(3, 37, D) * 3 + 1
+    w, b = torch.randn(D), torch.randn(D)
+    # drop row 0 of every group of 37 (the cls-dropping remap)
+    y = tmae.ops.layernorm(x.to(DEV), w.to(DEV), b.to(DEV), 1e-6, dtype, rows=3 * 36, row_group=36,
+                           group_stride=37, row_offset=1)
+    ref = F.layer_norm(x[:, 1:], (D,), w, b, 1e-6).reshape(-1, D)
+    assert rel(y.float(), ref) < tol(dtype)
+
+
+@pytest.mark.parametrize("M,N,K", [(9280, 2304, 768), (300, 64, 32), (129, 704, 640), (77, 32, 96), (1, 4, 8)])
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("act", [0, 1])
+def test_linear(tmae, M, N, K, dtype, act):
+    torch.manual_seed(M + N + K)
+    x, w, b = torch.randn(M, K), torch.randn(N, K) / K ** 0.5, torch.randn(N)
+    y = tmae.ops.linear(x.to(DEV).to(dtype), w.to(DEV).to(dtype), b.to(DEV), dtype, act=act)
+    ref = F.linear(x.to(dtype).float(), w.to(dtype).float(), b)
+    if act:
+        ref = F.gelu(ref)
+    assert rel(y.float(), ref) < tol(dtype)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_linear_f32_source_and_residual(tmae, dtype):
+    torch.manual_seed(3)
+    M, N, K = 500, 384, 512
+    x, w, b = torch.randn(M, K), torch.randn(N, K) / K ** 0.5, torch.randn(N)
+    y = tmae.ops.linear(x.to(DEV), w.to(DEV).to(dtype), b.to(DEV), dtype, out_dtype=torch.float32)
+    assert rel(y, F.linear(x.to(dtype).float(), w.to(dtype).float(), b)) < tol(dtype)
+    r0 = torch.randn(M, N)
+    r = r0.to(DEV).clone()
+    tmae.ops.linear_residual(x.to(DEV).to(dtype), w.to(DEV).to(dtype), b.to(DEV), r, dtype)
+    assert rel(r, r0 + F.linear(x.to(dtype).float(), w.to(dtype).float(), b)) < tol(dtype)
+
+
+def _ref_attn(qkv, B, T, H, dh):
+    q, k, v = qkv.reshape(B, T, 3, H, dh).permute(2, 0, 3, 1, 4)
+    a = ((q @ k.transpose(-2, -1)) * dh ** -0.5).softmax(-1)
+    return (a @ v).transpose(1, 2).reshape(B * T, H * dh)
+
+
+@pytest.mark.parametrize("B,T,H,dh", [(4, 145, 12, 64), (3, 257, 16, 32), (2, 17, 2, 32), (1, 32, 1, 64),
+                                      (2, 33, 4, 64)])
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_mha(tmae, B, T, H, dh, dtype):
+    torch.manual_seed(T)
+    qkv = torch.randn(B * T, 3 * H * dh) * 1.5
+    out = tmae.ops.mha(qkv.to(dtype).to(DEV), B, T, H, dh, dh ** -0.5, dtype)
+    assert rel(out.float(), _ref_attn(qkv.to(dtype).float(), B, T, H, dh)) < (1e-4 if dtype == torch.float32 else 3e-2)
+
+
+# ------------------------------------------------------------------------------------ convs
+@pytest.mark.parametrize("stride", [1, 2])
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_conv3x3_two_segments(tmae, stride, dtype):
+    torch.manual_seed(stride)
+    n, H, c1, c2, cout = 3, 12, 40, 24, 48
+    xa, xb = torch.randn(n, c1, H, H), torch.randn(n, c2, H, H)
+    w, b = torch.randn(cout, c1 + c2, 3, 3) / (9 * (c1 + c2)) ** 0.5, torch.randn(cout)
+    ref = F.gelu(F.conv2d(torch.cat([xa, xb], 1).to(dtype).float(), w.to(dtype).float(), b, stride=stride,
+                          padding=1))
+    Ho = ref.shape[2]
+    # segment 2 lives inside a wider NHWC buffer (channel offset + stride)
+    wide = torch.zeros(n, H, H, c2 + 16)
+    wide[..., 8:8 + c2] = xb.permute(0, 2, 3, 1)
+    wide = wide.to(DEV)
+    x1 = xa.permute(0, 2, 3, 1).contiguous().to(DEV)
+    y = torch.empty(n * Ho * Ho, cout, device=DEV)
+    wk = w.permute(0, 2, 3, 1).contiguous().to(dtype).to(DEV)
+    tmae.ops.conv3x3(x1, c1, c1, n, H, H, wk, b.to(DEV), y, cout, cout, dtype, stride=stride, act=1,
+                     x2=wide.data_ptr() + 8 * 4, c2=c2, ld2=c2 + 16)
+    assert rel(y.view(n, Ho, Ho, cout).permute(0, 3, 1, 2), ref) < tol(dtype)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_subpel_conv(tmae, dtype):
+    torch.manual_seed(5)
+    n, H, cin, c = 2, 6, 48, 16
+    x = torch.randn(n, cin, H, H)
+    w, b = torch.randn(4 * c, cin, 3, 3) / (9 * cin) ** 0.5, torch.randn(4 * c)
+    ref = F.pixel_shuffle(F.conv2d(x.to(dtype).float(), w.to(dtype).float(), b, padding=1), 2)
+    y = torch.empty(n * 4 * H * H, c, device=DEV)
+    tmae.ops.conv3x3(x.permute(0, 2, 3, 1).contiguous().to(DEV), cin, cin, n, H, H,
+                     w.permute(0, 2, 3, 1).contiguous().to(dtype).to(DEV), b.to(DEV), y, c, 4 * c, dtype,
+                     pixel_shuffle=True)
+    assert rel(y.view(n, 2 * H, 2 * H, c).permute(0, 3, 1, 2), ref) < tol(dtype)
+
+
+# ------------------------------------------------------------------------------------ entropy models
+def _eb_module(tmae, C, seed):
+    torch.manual_seed(seed)
+    eb = tmae.EntropyBottleneck(C)
+    with torch.no_grad():
+        for n, p in eb.named_parameters():
+            if "_factor" in n or "_matrix" in n:
+                p.normal_(0, 0.5)
+            if "quantiles" in n:
+                p.add_(torch.rand_like(p) * 0.6 - 0.3)
+    return eb
+
+
+@pytest.mark.parametrize("training", [False, True])
+def test_entropy_bottleneck(tmae, training):
+    C = 192
+    eb = _eb_module(tmae, C, 0)
+    sd = {f"eb.{k}": v for k, v in eb.state_dict().items()}
+    z = torch.randn(4, C, 3, 3) * 4
+    noise = torch.rand(4, C, 3, 3) - 0.5 if training else None
+    lik_ref, zhat_ref = orc.entropy_bottleneck(sd, "eb.", z, noise)
+    eb = eb.to(DEV)
+    out, lik = eb(z.to(DEV), training=training, noise=None if noise is None else noise.to(DEV))
+    assert rel(lik, lik_ref) < 1e-5
+    if not training:
+        assert torch.equal(out.cpu(), zhat_ref)
+    np.testing.assert_allclose(float(eb.loss()), float(orc.eb_aux_loss(sd, "eb.")), rtol=1e-5)
+
+
+@pytest.mark.parametrize("training", [False, True])
+def test_gaussian_conditional(tmae, training):
+    torch.manual_seed(2)
+    y, mu = torch.randn(2, 32, 12, 12) * 5, torch.randn(2, 32, 12, 12)
+    sigma = torch.rand(2, 32, 12, 12) * 3
+    noise = torch.rand(2, 32, 12, 12) - 0.5 if training else None
+    ref = orc.gaussian_conditional(y, sigma, mu, noise)
+    gc = tmae.GaussianConditional(None).to(DEV)
+    _, lik = gc(y.to(DEV), sigma.to(DEV), mu.to(DEV), training=training,
+                noise=None if noise is None else noise.to(DEV))
+    assert rel(lik, ref) < 1e-5
+
+
+# ------------------------------------------------------------------------------------ embed / unembed
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_patch_embed_kept_only(tmae, dtype):
+    torch.manual_seed(9)
+    n, img, P, D, K = 3, 64, 16, 128, 9
+    L = (img // P) ** 2
+    imgs = torch.rand(n, 3, img, img)
+    w, b = torch.randn(D, 3, P, P) / (3 * P * P) ** 0.5, torch.randn(D)
+    pos = torch.randn(1, L + 1, D)
+    shuf = torch.stack([torch.randperm(L) for _ in range(n)])
+    full = F.conv2d(imgs.to(dtype).float(), w.to(dtype).float(), b, stride=P).flatten(2).transpose(1, 2) + pos[:, 1:]
+    ref = torch.gather(full, 1, shuf[:, :K].unsqueeze(-1).repeat(1, 1, D))
+    tok = torch.zeros(n, K + 1, D, device=DEV)
+    tmae.ops.patch_embed(imgs.to(DEV), shuf.to(DEV), w.view(D, -1).to(dtype).to(DEV), b.to(DEV), pos.to(DEV), tok,
+                         K, P, dtype)
+    assert rel(tok[:, 1:], ref) < tol(dtype)
+
+
+@pytest.mark.parametrize("ntok", [16, 17])
+def test_decoder_embed_unshuffle(tmae, ntok):
+    torch.manual_seed(ntok)
+    n, L, Din, D = 2, 64, 96, 32
+    x = torch.randn(n, ntok, Din)
+    w, b = torch.randn(D, Din) / Din ** 0.5, torch.randn(D)
+    pos, mask = torch.randn(1, L + 1, D), torch.randn(1, 1, D)
+    shuf = torch.stack([torch.randperm(L) for _ in range(n)])
+    rest = torch.argsort(shuf, 1)
+    xd = F.linear(x, w, b)
+    x_ = torch.cat([xd[:, 1:], mask.repeat(n, L + 1 - ntok, 1)], 1)
+    x_ = torch.gather(x_, 1, rest.unsqueeze(-1).repeat(1, 1, D))
+    ref = torch.cat([xd[:, :1], x_], 1) + pos
+    out = torch.full((n, L + 1, D), float("nan"), device=DEV)
+    s = shuf.to(DEV)
+    tmae.ops.decoder_embed(x.reshape(-1, Din).to(DEV), w.to(DEV), b.to(DEV), pos.to(DEV), s, out, n, ntok, L,
+                           torch.float32)
+    tmae.ops.mask_rows(out, mask.to(DEV), pos.to(DEV), s, n, L, ntok, D)
+    assert rel(out, ref) < 1e-5
+
+
+def test_decoder_pred_unpatchify(tmae):
+    torch.manual_seed(4)
+    n, L, Din, P = 2, 16, 64, 16
+    x = torch.randn(n * L, Din)
+    w, b = torch.randn(P * P * 3, Din) / 8, torch.randn(P * P * 3)
+    ref = orc.unpatchify(F.linear(x, w, b).view(n, L, -1), P)
+    imgs = torch.empty(n, 3, 64, 64, device=DEV)
+    tmae.ops.decoder_pred(x.to(DEV), w.to(DEV), b.to(DEV), imgs, n, L, P, torch.float32)
+    assert rel(imgs, ref) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_block_module(tmae, dtype):
+    torch.manual_seed(0)
+    blk = tmae.Block(128, 4, qkv_bias=True, norm_layer=lambda d: torch.nn.LayerNorm(d, eps=1e-6))
+    x = torch.randn(3, 41, 128)
+    sd = {f"b.{k}": v for k, v in blk.state_dict().items()}
+    if dtype == torch.bfloat16:
+        sd = {k: (v.to(dtype).float() if v.dim() == 2 else v) for k, v in sd.items()}
+    ref = orc.block(x, sd, "b.", 4, 1e-6)
+    blk = blk.to(DEV)
+    blk.compute_dtype = dtype
+    assert rel(blk(x.to(DEV)), ref) < (1e-4 if dtype == torch.float32 else 3e-2)

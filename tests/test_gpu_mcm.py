@@ -1,0 +1,128 @@
+"""End-to-end parity of the drop-in MCM on the GPU.
+
+* against the reference's golden outputs (tests/golden/mcm_*.npz, produced by the REAL reference
+  glue) at two small configurations, eval and train (injected quantisation noise);
+* against the oracle at the north-star configuration (ViT-B, 256x256, K=144), batch 2.
+
+Tolerance (north_star: 1e-3 f32 rel-tol): max|a-b| / max|b| <= 1e-3 for x_hat, likelihoods and bpp.
+Eval/train quantisation rounds y - mu: an f32 summation-order difference can flip round() for an
+element sitting within ~1e-6 of a .5 boundary; such a flip changes that one latent by 1, so the
+likelihood check allows <= 0.1 % of elements outside tolerance while the aggregate (bpp) and the
+reconstruction must still meet 1e-3.  ids are bit-exact.
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.mcm_oracle import MCMConfig, make_state_dict, mcm_forward
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+TINY = dict(img_size=128, patch_size=16, encoder_embed_dim=64, encoder_depth=2, encoder_num_heads=2,
+            decoder_embed_dim=32, decoder_depth=2, decoder_num_heads=1, latent_depth=64, hyperprior_depth=32,
+            num_slices=4, num_keep_patches=16)
+SMALL12 = dict(img_size=128, patch_size=16, encoder_embed_dim=128, encoder_depth=1, encoder_num_heads=2,
+               decoder_embed_dim=64, decoder_depth=1, decoder_num_heads=2, latent_depth=192, hyperprior_depth=96,
+               num_slices=12, num_keep_patches=16)
+
+
+def build(tmae, cfgd, seed, dtype=torch.float32):
+    cfg = MCMConfig(**cfgd)
+    m = tmae.MCM(**cfg.kwargs())
+    full = m.state_dict()
+    full.update(make_state_dict(cfg, seed))
+    m.load_state_dict(full)
+    m.compute_dtype = dtype
+    return m.to(DEV), cfg
+
+
+def maxrel(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return float((a - b).abs().max() / b.abs().max())
+
+
+def frac_bad(a, b, rtol):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return float(((a - b).abs() > rtol * b.abs() + 1e-7).double().mean())
+
+
+def bpp(y, z, px):
+    return sum(float(torch.log(torch.as_tensor(l).double()).sum()) for l in (y, z)) / (-math.log(2) * px)
+
+
+@pytest.mark.parametrize("name,cfgd,seed", [("tiny", TINY, 7), ("small12", SMALL12, 11)])
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_mcm_vs_reference_golden(golden_dir, tmae, name, cfgd, seed, mode):
+    f = np.load(os.path.join(golden_dir, f"mcm_{name}.npz"))
+    m, cfg = build(tmae, cfgd, seed)
+    m.train(mode == "train")
+    imgs = torch.from_numpy(f["imgs"]).to(DEV)
+    noise = (torch.from_numpy(f["z_noise"]).to(DEV), torch.from_numpy(f["y_noise"]).to(DEV))
+    with torch.no_grad():
+        out = m(imgs, torch.from_numpy(f["scores"]).to(DEV), noise=noise if mode == "train" else None)
+    px = imgs.shape[0] * imgs.shape[2] * imgs.shape[3]
+    assert maxrel(out["x_hat"], f[f"{mode}_x_hat"]) < 1e-3
+    assert frac_bad(out["likelihoods"]["y"], f[f"{mode}_y_lik"], 1e-3) <= 1e-3
+    assert maxrel(out["likelihoods"]["z"], f[f"{mode}_z_lik"]) < 1e-3
+    got_bpp = bpp(out["likelihoods"]["y"], out["likelihoods"]["z"], px)
+    assert abs(got_bpp - float(f[f"{mode}_bpp_loss"])) <= 1e-3 * abs(float(f[f"{mode}_bpp_loss"]))
+    np.testing.assert_allclose(float(out["loss"][0]), f[f"{mode}_ssim_loss"], rtol=1e-3)
+    np.testing.assert_allclose(float(out["loss"][1]), f[f"{mode}_l1_loss"], rtol=1e-3)
+    np.testing.assert_allclose(float(m.aux_loss()), f["aux_loss"], rtol=1e-4)
+
+
+@pytest.fixture(scope="module")
+def vitb(tmae):
+    cfgd = dict(img_size=256, num_keep_patches=144)
+    m, cfg = build(tmae, cfgd, 3)
+    sd = make_state_dict(cfg, 3)
+    rng = np.random.default_rng(0)
+    imgs = torch.from_numpy(((rng.random((2, 3, 256, 256), dtype=np.float32) - 0.45) / 0.225).astype(np.float32))
+    scores = torch.from_numpy(rng.random((2, 256), dtype=np.float32))
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    ref = mcm_forward(sd, cfg, imgs, scores)
+    return m, cfg, imgs, scores, ref
+
+
+def test_mcm_vitb_f32_vs_oracle(vitb):
+    m, cfg, imgs, scores, ref = vitb
+    m.eval()
+    m.compute_dtype = torch.float32
+    with torch.no_grad():
+        out = m(imgs.to(DEV), scores.to(DEV))
+    px = 2 * 256 * 256
+    assert maxrel(out["x_hat"], ref.x_hat) < 1e-3
+    assert frac_bad(out["likelihoods"]["y"], ref.y_likelihood, 1e-3) <= 1e-3
+    assert maxrel(out["likelihoods"]["z"], ref.z_likelihood) < 1e-3
+    b_ref = bpp(ref.y_likelihood, ref.z_likelihood, px)
+    assert abs(bpp(out["likelihoods"]["y"], out["likelihoods"]["z"], px) - b_ref) <= 1e-3 * abs(b_ref)
+
+
+def test_mcm_vitb_bf16_close_to_oracle(vitb):
+    """bf16 operands cannot meet 1e-3; this bounds the throughput path's deviation (relative L2)."""
+    m, cfg, imgs, scores, ref = vitb
+    m.eval()
+    m.compute_dtype = torch.bfloat16
+    with torch.no_grad():
+        out = m(imgs.to(DEV), scores.to(DEV))
+    m.compute_dtype = torch.float32
+    xh = out["x_hat"].cpu().double()
+    l2 = float((xh - ref.x_hat.double()).norm() / ref.x_hat.double().norm())
+    assert l2 < 3e-2, l2
+    px = 2 * 256 * 256
+    b_ref = bpp(ref.y_likelihood, ref.z_likelihood, px)
+    assert abs(bpp(out["likelihoods"]["y"], out["likelihoods"]["z"], px) - b_ref) <= 3e-2 * abs(b_ref)
+
+
+def test_mcm_batch_independence(vitb):
+    """images are independent: image 0 of a batch of 2 == the same image alone (DP sharding premise)"""
+    m, cfg, imgs, scores, ref = vitb
+    m.eval()
+    with torch.no_grad():
+        a = m(imgs.to(DEV), scores.to(DEV))["x_hat"][:1]
+        b = m(imgs[:1].to(DEV), scores[:1].to(DEV))["x_hat"]
+    assert maxrel(a, b) < 1e-5

@@ -1,0 +1,88 @@
+"""The oracle pinned against the reference's own outputs (tests/golden/, made by tools/gen_golden.py
+from the real reference code).  CPU only."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ids as ids_oracle
+from oracle.mcm_oracle import MCMConfig, eb_aux_loss, forward_loss, make_state_dict, mcm_forward, pos_embed_2d, rate_bpp
+
+TINY = dict(img_size=128, patch_size=16, encoder_embed_dim=64, encoder_depth=2, encoder_num_heads=2,
+            decoder_embed_dim=32, decoder_depth=2, decoder_num_heads=1, latent_depth=64, hyperprior_depth=32,
+            num_slices=4, num_keep_patches=16)
+SMALL12 = dict(img_size=128, patch_size=16, encoder_embed_dim=128, encoder_depth=1, encoder_num_heads=2,
+               decoder_embed_dim=64, decoder_depth=1, decoder_num_heads=2, latent_depth=192, hyperprior_depth=96,
+               num_slices=12, num_keep_patches=16)
+FIXTURES = {"tiny": (TINY, 7), "small12": (SMALL12, 11)}
+
+
+def _ids_groups(golden_dir):
+    d = np.load(os.path.join(golden_dir, "ids_shuffle.npz"))
+    for k in sorted(d.files):
+        if k.endswith("_scores"):
+            key = k[: -len("_scores")]
+            L, K = int(key.split("_")[0][1:]), int(key.split("_")[1][1:])
+            yield key, L, K, d[k], d[key + "_ids"].astype(np.int64)
+
+
+def test_ids_oracle_bit_exact_vs_reference(golden_dir):
+    n = 0
+    for key, L, K, scores, expect in _ids_groups(golden_dir):
+        got, rest = ids_oracle.ids_shuffle(scores, K, lanes=8)
+        assert np.array_equal(got, expect), key
+        assert np.array_equal(np.take_along_axis(got, rest, 1), np.tile(np.arange(L), (len(got), 1)))
+        n += len(scores)
+    assert n >= 900
+
+
+def test_ids_oracle_raises_like_reference():
+    with pytest.raises(ValueError, match="Number of patches"):
+        ids_oracle.ids_shuffle(np.zeros((1, 16), np.float32), 17)
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 8, 9, 31, 64, 65, 200, 1000, 5000])
+def test_torch_sum_order_emulation(n):
+    """the oracle's float32 group sums follow torch's CPU cascade order bit for bit"""
+    rng = np.random.default_rng(n)
+    for scale in (1.0, 1e3, 1e-3):
+        x = (rng.random(n) * scale).astype(np.float32)
+        assert np.float32(torch.from_numpy(x).sum().item()) == np.float32(ids_oracle.torch_sum_f32(x))
+
+
+@pytest.mark.parametrize("name", ["tiny", "small12"])
+@pytest.mark.parametrize("mode", ["eval", "train"])
+def test_oracle_forward_vs_reference(golden_dir, name, mode):
+    cfgd, seed = FIXTURES[name]
+    f = np.load(os.path.join(golden_dir, f"mcm_{name}.npz"))
+    cfg = MCMConfig(**cfgd)
+    sd = make_state_dict(cfg, seed)
+    sha = hashlib.sha256(np.concatenate([v.numpy().ravel() for v in sd.values()]).tobytes()).hexdigest()[:16]
+    assert sha == str(f["weights_sha"]), "deterministic weight generator drifted"
+    kw = {}
+    if mode == "train":
+        kw = dict(z_noise=torch.from_numpy(f["z_noise"]), y_noise=torch.from_numpy(f["y_noise"]))
+    o = mcm_forward(sd, cfg, torch.from_numpy(f["imgs"]), torch.from_numpy(f["scores"]), **kw)
+    assert np.array_equal(o.ids_restore.numpy(), f[f"{mode}_ids_restore"])
+    for got, key in ((o.x_hat, "x_hat"), (o.y_likelihood, "y_lik"), (o.z_likelihood, "z_lik")):
+        np.testing.assert_allclose(got.numpy(), f[f"{mode}_{key}"], rtol=1e-6, atol=1e-7)
+    imgs = torch.from_numpy(f["imgs"])
+    ssim_l, l1 = forward_loss(o.x_hat, imgs)
+    np.testing.assert_allclose(float(ssim_l), f[f"{mode}_ssim_loss"], rtol=1e-6)
+    np.testing.assert_allclose(float(l1), f[f"{mode}_l1_loss"], rtol=1e-6)
+    bpp = rate_bpp(o.y_likelihood, o.z_likelihood, imgs.shape[0] * imgs.shape[2] * imgs.shape[3])
+    np.testing.assert_allclose(float(bpp), f[f"{mode}_bpp_loss"], rtol=1e-6)
+    np.testing.assert_allclose(float(eb_aux_loss(sd, "entropy_bottleneck.")), f["aux_loss"], rtol=1e-6)
+
+
+def test_pos_embed_vs_reference(golden_dir, tmae):
+    d = np.load(os.path.join(golden_dir, "pos_embed.npz"))
+    from textmae_amd.pos_embed import get_2d_sincos_pos_embed
+
+    for dim, g in [(768, 16), (512, 16), (768, 14), (1024, 16), (64, 8), (32, 8)]:
+        for pe in (pos_embed_2d(dim, g), get_2d_sincos_pos_embed(dim, g, cls_token=True)):
+            pe = pe.astype(np.float32)
+            assert hashlib.sha256(pe.tobytes()).hexdigest()[:16] == str(d[f"d{dim}_g{g}_sha"])
+            np.testing.assert_array_equal(pe[[0, 1, g + 3, g * g]], d[f"d{dim}_g{g}_rows"])

@@ -1,0 +1,14 @@
+"""MI355X-native (gfx950) TextMAE MCM hot path: MAE-ViT encode/decode + entropy-bottleneck and
+Gaussian-conditional rate estimation, behind the reference's nn.Module surface.
+
+Import name: ``textmae_amd`` (see textmae_amd.py at the repo root; the directory name contains
+dashes, as the build layout requires).
+"""
+from . import ops  # noqa: F401
+from ._lib import LIB_PATH, load as load_library  # noqa: F401
+from .entropy import CompressionModel, EntropyBottleneck, GaussianConditional, get_scale_table  # noqa: F401
+from .layers import Block, PatchEmbed  # noqa: F401
+from .mcm import MCM  # noqa: F401
+
+__all__ = ["MCM", "Block", "PatchEmbed", "EntropyBottleneck", "GaussianConditional", "CompressionModel", "ops",
+           "load_library", "LIB_PATH", "get_scale_table"]

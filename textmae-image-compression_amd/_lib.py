@@ -1,0 +1,79 @@
+"""ctypes binding of libtmae.so (include/tmae.h).
+
+The library is the product: if it is missing or fails to load, every op raises — there is no
+PyTorch or CPU fallback anywhere on the hot path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libtmae.so")
+
+TMAE_F32, TMAE_BF16 = 0, 1
+ACT_NONE, ACT_GELU = 0, 1
+
+P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+
+
+class EBParams(ctypes.Structure):
+    _fields_ = [("matrix", ctypes.c_void_p * 5), ("bias", ctypes.c_void_p * 5), ("factor", ctypes.c_void_p * 4),
+                ("quantiles", ctypes.c_void_p)]
+
+
+# name -> argtypes (all return int status except where noted)
+SIGNATURES = {
+    "tmae_abi_version": [],
+    "tmae_ids_shuffle": [P, P, P, I, I, I, I, P],
+    "tmae_layernorm_fwd": [P, P, P, P, I, I, I, I, I, F, I, P],
+    "tmae_linear_fwd": [P, I, I, I, I, I, P, P, P, I, I, I, I, I, I, I, P],
+    "tmae_linear_residual_fwd": [P, I, P, P, P, I, I, I, I, I, P],
+    "tmae_patch_embed_fwd": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "tmae_cls_rows": [P, P, P, I, I, I, P],
+    "tmae_mha_fwd": [P, P, I, I, I, I, F, I, P],
+    "tmae_decoder_embed_fwd": [P, I, P, P, P, P, P, I, I, I, I, I, I, P],
+    "tmae_mask_rows": [P, P, P, P, I, I, I, I, P],
+    "tmae_decoder_pred_fwd": [P, P, P, P, I, I, I, I, I, I, I, I, P],
+    "tmae_conv3x3_fwd": [P, I, I, P, I, I, I, I, I, I, P, P, P, I, I, I, I, I, P],
+    "tmae_conv3x3_gaussian_fwd": [P, I, I, P, I, I, I, I, I, P, P, I, P, I, I, P, I, P, P, I, P, I, I, P],
+    "tmae_conv3x3_lrp_fwd": [P, I, I, P, I, I, I, I, I, P, P, I, P, I, P, I, P, I, I, P],
+    "tmae_eb_likelihood_fwd": [P, ctypes.POINTER(EBParams), P, P, P, P, I, I, I, P],
+    "tmae_eb_aux_loss": [ctypes.POINTER(EBParams), P, P, P, I, P],
+    "tmae_gc_likelihood_fwd": [P, P, P, P, P, P, I, F, P],
+    "tmae_nhwc_to_nchw": [P, I, P, I, I, I, P],
+}
+
+_lib = None
+
+
+class TmaeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libtmae.so (raises if it has not been built — run __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise TmaeError(f"{LIB_PATH} is missing: build it with `python __graft_entry__.py` or build.build()")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, args in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = ctypes.c_int
+        lib.tmae_last_error_string.argtypes = []
+        lib.tmae_last_error_string.restype = ctypes.c_char_p
+        _lib = lib
+    return _lib
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.tmae_last_error_string().decode(errors="replace")
+        if rc == 1:
+            raise ValueError(f"{name}: {msg}")
+        raise TmaeError(f"{name} failed (status {rc}): {msg}")
+    return rc

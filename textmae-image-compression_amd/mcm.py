@@ -1,0 +1,466 @@
+"""MCM — drop-in for reference models/Compression/MCM.py:25 (``class MCM(CompressionModel)``).
+
+Same constructor arguments and defaults (MCM.py:34-52), same submodule names, so
+``state_dict()`` keys, ``named_parameters()`` (``*.quantiles`` split, model_utils.py:67-90) and
+``load_state_dict`` behave as in the reference; same call surface (``forward(imgs, total_scores)``
+-> ``{"loss", "likelihoods", "x_hat"}``, ``aux_loss()``, ``from_state_dict``, ``patchify`` /
+``unpatchify``).
+
+Underneath, ``forward`` never calls a PyTorch compute op on the hot path: it enqueues the gfx950
+kernels of libtmae.so on the current stream through a persistent workspace (``_Executor``), with
+the LIC feature maps kept NHWC end to end.  ``compute_dtype`` selects the MFMA
+operand type: torch.float32 (exact f32 MFMA; the parity path, default) or torch.bfloat16
+(throughput path; f32 accumulate, f32 residual stream / entropy models / likelihoods).
+"""
+from __future__ import annotations
+
+from functools import partial
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from .entropy import CompressionModel, EntropyBottleneck, GaussianConditional
+from .layers import Block, BlockScratch, BlockWeights, PatchEmbed, conv3x3, run_block, subpel_conv3x3
+from .pos_embed import get_2d_sincos_pos_embed
+
+
+class MCM(CompressionModel):
+    """Masked-compression model: MAE-ViT encoder -> hyperprior LIC with channel-conditional slices ->
+    MAE-ViT decoder (reference MCM.py:25-968)."""
+
+    def __init__(self, img_size=224, patch_size=16, in_chans=3, encoder_embed_dim=768, encoder_depth=12,
+                 encoder_num_heads=12, decoder_embed_dim=512, decoder_depth=8, decoder_num_heads=16, mlp_ratio=4.0,
+                 norm_layer=partial(nn.LayerNorm, eps=1e-6), norm_pix_loss=False, latent_depth=384,
+                 hyperprior_depth=192, num_slices=12, num_keep_patches=144):
+        super().__init__()
+        self.frozen_stages = -1
+        self.encoder_embed_dim = E = encoder_embed_dim
+        self.encoder_depth = encoder_depth
+        self.encoder_num_heads = encoder_num_heads
+        self.decoder_embed_dim = Dd = decoder_embed_dim
+        self.decoder_depth = decoder_depth
+        self.decoder_num_heads = decoder_num_heads
+        self.latent_depth = M = latent_depth
+        self.hyperprior_depth = N = hyperprior_depth
+        self.num_slices = S = num_slices
+        self.num_keep_patches = num_keep_patches
+
+        # entropy models (MCM.py:71-73)
+        self.entropy_bottleneck = EntropyBottleneck(N)
+        self.gaussian_conditional = GaussianConditional(None)
+        self.max_support_slices = S // 2
+
+        # g_a / g_s: 1x1 convs E -> .. -> M and back (MCM.py:77-112)
+        ga = [E, int(Dd + (E - Dd) * 3 / 4), int(Dd + (E - Dd) * 2 / 4), Dd, M]
+        self.g_a = nn.Sequential(*_interleave([nn.Conv2d(ga[j], ga[j + 1], 1, 1, 0) for j in range(4)]))
+        gs = ga[::-1]
+        self.g_s = nn.Sequential(*_interleave([nn.ConvTranspose2d(gs[j], gs[j + 1], 1, 1, 0) for j in range(4)]))
+
+        # h_a / h_s (MCM.py:115-162)
+        ha = [M, M, int(N + (M - N) * 3 / 4), int(N + (M - N) * 2 / 4), int(N + (M - N) / 4), N]
+        self.h_a = nn.Sequential(*_interleave([conv3x3(ha[j], ha[j + 1], stride=(2 if j in (2, 4) else 1))
+                                               for j in range(5)]))
+        hs = [N, int(N + (M - N) / 4), int(N + (M - N) * 2 / 4), int(N + (M - N) * 3 / 4), M, M]
+
+        def h_s():
+            return nn.Sequential(*_interleave([
+                conv3x3(hs[0], hs[1]), subpel_conv3x3(hs[1], hs[2], r=2), conv3x3(hs[2], hs[3]),
+                subpel_conv3x3(hs[3], hs[4], r=2), conv3x3(hs[4], hs[5])]))
+
+        self.h_s_mean = h_s()
+        self.h_s_scale = h_s()
+
+        # channel-conditional slice transforms (MCM.py:165-293)
+        sw = M // S
+        mid = [int(sw * (S // 2 + 1)), int(sw * (S // 2 * 3 / 4 + 1)), int(sw * (S // 2 * 2 / 4 + 1)),
+               int(sw * (S // 2 * 1 / 4 + 1)), sw]
+
+        def stack(cin):
+            ch = [cin] + mid
+            return nn.Sequential(*_interleave([nn.Conv2d(ch[j], ch[j + 1], 3, 1, 1) for j in range(5)]))
+
+        self.cc_transform_mean = nn.ModuleList([stack(int(M + sw * min(i, S // 2))) for i in range(S)])
+        self.cc_transform_scale = nn.ModuleList([stack(int(M + sw * min(i, S // 2))) for i in range(S)])
+        self.lrp_transform = nn.ModuleList([stack(int(M + sw * min(i + 1, S // 2 + 1))) for i in range(S)])
+
+        # MAE encoder / decoder (MCM.py:300-354)
+        self.encoder_embed = PatchEmbed(img_size, patch_size, in_chans, E)
+        num_patches = self.encoder_embed.num_patches
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, E))
+        self.encoder_pos_embed = nn.Parameter(torch.zeros(1, num_patches + 1, E), requires_grad=False)
+        self.encoder_blocks = nn.ModuleList([Block(dim=E, num_heads=encoder_num_heads, mlp_ratio=mlp_ratio,
+                                                   qkv_bias=True, norm_layer=norm_layer)
+                                             for _ in range(encoder_depth)])
+        self.encoder_norm = norm_layer(E)
+        self.decoder_embed = nn.Linear(E, Dd, bias=True)
+        self.mask_token = nn.Parameter(torch.zeros(1, 1, Dd))
+        self.decoder_pos_embed = nn.Parameter(torch.zeros(1, num_patches + 1, Dd), requires_grad=False)
+        self.decoder_blocks = nn.ModuleList([Block(dim=Dd, num_heads=decoder_num_heads, mlp_ratio=mlp_ratio,
+                                                   qkv_bias=True, norm_layer=norm_layer)
+                                             for _ in range(decoder_depth)])
+        self.decoder_norm = norm_layer(Dd)
+        self.decoder_pred = nn.Linear(Dd, patch_size ** 2 * in_chans, bias=True)
+        self.norm_pix_loss = norm_pix_loss
+        self.initialize_weights()
+
+        # MI355X execution settings (not part of the reference surface)
+        self.compute_dtype = torch.float32
+        self.sum_lanes = 8          # torch CPU float-sum vector width the reference ran with
+        self.distortion = "ssim+l1"  # forward_loss terms; "none" skips them (encode/decode/rate only)
+        self._exec = None
+
+    # ---------------------------------------------------------------------------------- init
+    def initialize_weights(self):
+        """MCM.initialize_weights / _init_weights (MCM.py:454-495)."""
+        g = int(self.encoder_embed.num_patches ** 0.5)
+        self.encoder_pos_embed.data.copy_(
+            torch.from_numpy(get_2d_sincos_pos_embed(self.encoder_pos_embed.shape[-1], g, True)).float().unsqueeze(0))
+        self.decoder_pos_embed.data.copy_(
+            torch.from_numpy(get_2d_sincos_pos_embed(self.decoder_pos_embed.shape[-1], g, True)).float().unsqueeze(0))
+        w = self.encoder_embed.proj.weight.data
+        torch.nn.init.xavier_uniform_(w.view([w.shape[0], -1]))
+        torch.nn.init.normal_(self.cls_token, std=0.02)
+        torch.nn.init.normal_(self.mask_token, std=0.02)
+        self.apply(self._init_weights)
+
+    @staticmethod
+    def _init_weights(m):
+        if isinstance(m, nn.Linear):
+            torch.nn.init.xavier_uniform_(m.weight)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, nn.LayerNorm):
+            nn.init.constant_(m.bias, 0)
+            nn.init.constant_(m.weight, 1.0)
+
+    def load_state_dict(self, state_dict, strict=True):
+        # the reference override drops `strict` (MCM.py:445-446); keep the compressai buffer resizing
+        r = super().load_state_dict(state_dict, strict=strict)
+        self._exec = None
+        return r
+
+    @classmethod
+    def from_state_dict(cls, num_keep_patches, state_dict):
+        net = cls(num_keep_patches=num_keep_patches)
+        net.load_state_dict(state_dict)
+        return net
+
+    # ---------------------------------------------------------------------------------- layout helpers
+    def patchify(self, imgs):
+        p = self.encoder_embed.patch_size[0]
+        assert imgs.shape[2] == imgs.shape[3] and imgs.shape[2] % p == 0
+        h = w = imgs.shape[2] // p
+        x = imgs.reshape(imgs.shape[0], 3, h, p, w, p)
+        return torch.einsum("nchpwq->nhwpqc", x).reshape(imgs.shape[0], h * w, p ** 2 * 3)
+
+    def unpatchify(self, x):
+        p = self.encoder_embed.patch_size[0]
+        h = w = int(x.shape[1] ** 0.5)
+        assert h * w == x.shape[1]
+        x = torch.einsum("nhwpqc->nchpwq", x.reshape(x.shape[0], h, w, p, p, 3))
+        return x.reshape(x.shape[0], 3, h * p, w * p)
+
+    # ---------------------------------------------------------------------------------- masking
+    def get_ids_shuffle(self, total_scores):
+        """MCM.get_ids_shuffle (MCM.py:364-423) — one GPU launch for the whole batch."""
+        if self.num_keep_patches > total_scores.shape[1]:
+            raise ValueError("Number of patches should not be greater than the length of scores")
+        return ops.ids_shuffle(total_scores, self.num_keep_patches, self.sum_lanes)[0]
+
+    def random_masking(self, x, total_scores):
+        """MCM.random_masking (MCM.py:548-588): (x_remain, ids_restore)."""
+        shuf, rest = ops.ids_shuffle(total_scores, self.num_keep_patches, self.sum_lanes)
+        D = x.shape[-1]
+        x_remain = torch.gather(x, 1, shuf[:, : self.num_keep_patches].unsqueeze(-1).repeat(1, 1, D))
+        return x_remain, rest
+
+    # ---------------------------------------------------------------------------------- forward
+    def _executor(self, batch, device):
+        dt = self.compute_dtype
+        if torch.is_autocast_enabled() and dt == torch.float32:
+            dt = torch.bfloat16  # val_one_epoch runs under autocast (utils/engine.py:189)
+        ex = self._exec
+        if ex is None or ex.batch != batch or ex.dtype != dt or ex.device != device:
+            ex = self._exec = _Executor(self, batch, dt, device)
+        ex.refresh_weights()
+        return ex
+
+    def forward(self, imgs, total_scores, noise=None):
+        """MCM.forward (MCM.py:714-803).  `noise=(z_noise, y_noise)` (NCHW, U(-1/2, 1/2)) replaces the
+        training-mode quantisation noise — used by parity tests; otherwise drawn on the device."""
+        if not imgs.is_cuda:
+            raise ValueError("MCM.forward runs on the MI355X kernels: move the model and inputs to the GPU")
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError(
+                "training-mode autograd is not available in this build: run forward under torch.no_grad()")
+        with torch.no_grad():
+            ex = self._executor(imgs.shape[0], imgs.device)
+            out = ex.run(imgs, total_scores, self.training, noise)
+            x_hat = out["x_hat"]
+            loss = self.forward_loss(imgs, x_hat) if self.distortion != "none" else (
+                torch.zeros((), device=imgs.device),) * 3
+        return {"loss": loss, "likelihoods": {"y": out["y"], "z": out["z"]}, "x_hat": x_hat}
+
+    def forward_loss(self, imgs, x_hat):
+        """MCM.forward_loss (MCM.py:690-712): (1 - SSIM, L1, VGG feature loss).  The VGG term needs
+        torchvision's pretrained VGG16 (a network download in the reference, vgg.py:14) and is 0 here."""
+        from .distortion import l1_loss, ssim_loss
+
+        return ssim_loss(x_hat, imgs), l1_loss(x_hat, imgs), torch.zeros((), device=imgs.device)
+
+    def aux_loss(self):
+        return self.entropy_bottleneck.loss()
+
+    def compress(self, imgs, total_scores):
+        raise NotImplementedError("MCM.compress: entropy coding (rANS) is the next §8f row, not in this build")
+
+    def decompress(self, strings, shape, ids_restore=None):
+        raise NotImplementedError("MCM.decompress: entropy coding (rANS) is the next §8f row, not in this build")
+
+
+def _interleave(layers):
+    out = []
+    for j, l in enumerate(layers):
+        out.append(l)
+        if j < len(layers) - 1:
+            out.append(nn.GELU())
+    return out
+
+
+# ====================================================================================== executor
+class _Executor:
+    """Prepared weights + persistent workspaces for one (batch, dtype, device); `run` enqueues the
+    whole forward (about 270 launches at the default config) on the current stream."""
+
+    def __init__(self, m: MCM, batch, dtype, device):
+        self.m, self.batch, self.dtype, self.device = m, batch, dtype, device
+        self._sig = None
+        B = batch
+        E, Dd, M, N, S = m.encoder_embed_dim, m.decoder_embed_dim, m.latent_depth, m.hyperprior_depth, m.num_slices
+        K = m.num_keep_patches
+        P = m.encoder_embed.patch_size[0]
+        self.img = m.encoder_embed.img_size[0]
+        self.P, self.L = P, m.encoder_embed.num_patches
+        self.g = g = int(round(K ** 0.5))
+        if g * g != K:
+            raise ValueError(f"num_keep_patches={K} must be a perfect square (MCM.py:729-732 views it as sqrt x sqrt)")
+        self.hz = ((g + 1) // 2 + 1) // 2  # two stride-2 convs
+        if self.hz * 4 != g:
+            raise ValueError(f"sqrt(num_keep_patches)={g} must be a multiple of 4 so h_s returns to the y grid")
+        self.sw = M // S
+        self.maxsup = S // 2
+        f32, dt = torch.float32, dtype
+        dev = device
+
+        def z(*shape, dtype=f32):
+            return torch.empty(shape, dtype=dtype, device=dev)
+
+        Te, Td = K + 1, self.L + 1
+        hid_e = m.encoder_blocks[0].mlp.fc1.out_features if m.encoder_depth else 4 * E
+        hid_d = m.decoder_blocks[0].mlp.fc1.out_features if m.decoder_depth else 4 * Dd
+        self.tok = z(B * Te, E)
+        self.enc_s = BlockScratch(B * Te, E, hid_e, dt, dev)
+        self.enc_out = z(B * K, E, dtype=dt)
+        ga = [l.out_channels for l in m.g_a if isinstance(l, nn.Conv2d)]
+        self.ga_buf = [z(B * K, c, dtype=dt) for c in ga[:-1]]
+        self.Y = z(B * K, M)
+        ha = [l.out_channels for l in m.h_a if isinstance(l, nn.Conv2d)]
+        res = [g, g, (g + 1) // 2, (g + 1) // 2, self.hz]
+        self.ha_buf = [z(B * r * r, c) for c, r in zip(ha[:-1], res[:-1])]
+        self.Z = z(B * self.hz * self.hz, N)
+        self.ZLIK = z(B, N, self.hz, self.hz)
+        self.ZHAT = z(B * self.hz * self.hz, N)
+        self.eb_table = z(N, 59)
+        hs_out = [m.h_s_mean[0].out_channels, m.h_s_mean[2][0].out_channels // 4, m.h_s_mean[4].out_channels,
+                  m.h_s_mean[6][0].out_channels // 4]
+        hs_res = [self.hz, 2 * self.hz, 2 * self.hz, g]
+        self.hs_buf = [z(B * r * r, c) for c, r in zip(hs_out, hs_res)]
+        self.SUPW = M + self.sw * (self.maxsup + 1)
+        self.SUP = z(B * g * g, self.SUPW)  # [latent_means | y_hat slots 0..maxsup-1 | current slice]
+        self.LS = z(B * g * g, M)
+        mid = [l.out_channels for l in m.cc_transform_mean[0] if isinstance(l, nn.Conv2d)]
+        self.cc_buf = [z(B * g * g, c) for c in mid[:-1]]
+        self.MU = z(B * g * g, self.sw)
+        self.YLIK = z(B, M, g, g)
+        self.YH = z(B * g * g, M)
+        gs = [l.out_channels for l in m.g_s if isinstance(l, nn.ConvTranspose2d)]
+        self.gs_buf = [z(B * K, c, dtype=dt) for c in gs]
+        self.dec = z(B * Td, Dd)
+        self.dec_s = BlockScratch(B * Td, Dd, hid_d, dt, dev)
+        self.dn = z(B * self.L, Dd, dtype=dt)
+
+    # ------------------------------------------------------------------ weights
+    def refresh_weights(self):
+        sig = tuple((p.data_ptr(), p._version) for p in self.m.parameters())
+        if sig == self._sig:
+            return
+        self._sig = sig
+        m, dt = self.m, self.dtype
+        cast = (lambda t: t.detach().contiguous()) if dt == torch.float32 else (
+            lambda t: t.detach().to(dt).contiguous())
+
+        def conv_w(conv):  # [Cout][Cin][3][3] -> [Cout][3][3][Cin]
+            return cast(conv.weight.detach().permute(0, 2, 3, 1))
+
+        self.w_pe = cast(m.encoder_embed.proj.weight.view(m.encoder_embed.proj.weight.shape[0], -1))
+        self.enc_w = [BlockWeights.from_block(b, dt) for b in m.encoder_blocks]
+        self.dec_w = [BlockWeights.from_block(b, dt) for b in m.decoder_blocks]
+        self.ga_w = [(cast(l.weight.view(l.weight.shape[0], -1)), l.bias.detach())
+                     for l in m.g_a if isinstance(l, nn.Conv2d)]
+        self.gs_w = [(cast(l.weight.view(l.weight.shape[0], -1).t()), l.bias.detach())
+                     for l in m.g_s if isinstance(l, nn.ConvTranspose2d)]
+        self.ha_w = [(conv_w(l), l.bias.detach(), l.stride[0]) for l in m.h_a if isinstance(l, nn.Conv2d)]
+
+        def hs_w(seq):
+            out = []
+            for l in seq:
+                if isinstance(l, nn.Conv2d):
+                    out.append((conv_w(l), l.bias.detach(), False))
+                elif isinstance(l, nn.Sequential):
+                    out.append((conv_w(l[0]), l[0].bias.detach(), True))
+            return out
+
+        self.hsm_w, self.hss_w = hs_w(m.h_s_mean), hs_w(m.h_s_scale)
+
+        def stack_w(seq):
+            return [(conv_w(l), l.bias.detach()) for l in seq if isinstance(l, nn.Conv2d)]
+
+        self.ccm_w = [stack_w(s) for s in m.cc_transform_mean]
+        self.ccs_w = [stack_w(s) for s in m.cc_transform_scale]
+        self.lrp_w = [stack_w(s) for s in m.lrp_transform]
+        self.w_de = cast(m.decoder_embed.weight)
+        self.w_dp = cast(m.decoder_pred.weight)
+
+    # ------------------------------------------------------------------ forward
+    def run(self, imgs, scores, training, noise):
+        m, dt, B = self.m, self.dtype, self.batch
+        E, Dd, M, N, S = m.encoder_embed_dim, m.decoder_embed_dim, m.latent_depth, m.hyperprior_depth, m.num_slices
+        K, L, P, g, hz, sw = m.num_keep_patches, self.L, self.P, self.g, self.hz, self.sw
+        Te, Td = K + 1, L + 1
+        imgs = imgs.float().contiguous()
+        if imgs.shape[1:] != (m.encoder_embed.proj.in_channels, self.img, self.img):
+            raise ValueError(f"Input image size {tuple(imgs.shape[2:])} doesn't match model ({self.img})")
+        if training:
+            if noise is not None:
+                z_noise, y_noise = (t.float().contiguous() for t in noise)
+            else:
+                z_noise = torch.empty((B, N, hz, hz), device=self.device).uniform_(-0.5, 0.5)
+                y_noise = torch.empty((B, M, g, g), device=self.device).uniform_(-0.5, 0.5)
+        else:
+            z_noise = y_noise = None
+
+        # ---- encoder (MCM.py:590-634): ids on device, embed only the kept patches
+        shuf, rest = ops.ids_shuffle(scores, K, m.sum_lanes)
+        pos_e = m.encoder_pos_embed.detach()
+        ops.patch_embed(imgs, shuf, self.w_pe, m.encoder_embed.proj.bias.detach(), pos_e, self.tok, K, P, dt)
+        ops.cls_rows(self.tok, m.cls_token.detach(), pos_e, B, Te, E)
+        for w in self.enc_w:
+            run_block(self.tok, w, B, Te, dt, self.enc_s)
+        ops.layernorm(self.tok, m.encoder_norm.weight, m.encoder_norm.bias, m.encoder_norm.eps, dt, rows=B * K,
+                      row_group=K, group_stride=Te, row_offset=1, out=self.enc_out)
+
+        # ---- g_a: 1x1 convs on the token matrix (tokens in ids_keep order = the g x g grid, MCM.py:729-735)
+        x = self.enc_out
+        for j, (w, b) in enumerate(self.ga_w):
+            last = j == len(self.ga_w) - 1
+            out = self.Y if last else self.ga_buf[j]
+            ops.linear(x, w, b, dt, act=ops.ACT_NONE if last else ops.ACT_GELU, out=out)
+            x = out
+
+        # ---- h_a (MCM.py:739)
+        H = g
+        x, cin = self.Y, M
+        for j, (w, b, stride) in enumerate(self.ha_w):
+            last = j == len(self.ha_w) - 1
+            out = self.Z if last else self.ha_buf[j]
+            cout = w.shape[0]
+            ops.conv3x3(x, cin, cin, B, H, H, w, b, out, cout, cout, dt, stride=stride,
+                        act=ops.ACT_NONE if last else ops.ACT_GELU)
+            H = (H + 2 - 3) // stride + 1
+            x, cin = out, cout
+
+        # ---- entropy bottleneck + z_hat (MCM.py:741-744)
+        ops.eb_likelihood(m.entropy_bottleneck, self.Z, B, N, hz * hz, noise=z_noise, lik=self.ZLIK, zhat=self.ZHAT,
+                          table=self.eb_table)
+
+        # ---- h_s_scale -> LS, h_s_mean -> SUP[:, :M]  (MCM.py:747-748)
+        self._h_s(self.hss_w, self.LS, M)
+        self._h_s(self.hsm_w, self.SUP, self.SUPW)
+
+        # ---- slice loop (MCM.py:751-787)
+        SUP, W4 = self.SUP, self.SUP.element_size()
+        sup_base = SUP.data_ptr()
+        for i in range(S):
+            nsup = min(i, self.maxsup)
+            cur = M + nsup * sw  # channel offset of this slice's y_hat in SUP
+            # mu = cc_transform_mean[i](cat(latent_means, y_hat[:nsup]))
+            self._stack(self.ccm_w[i], SUP, cur, self.SUPW, None, 0, 0)
+            mu_w, mu_b = self.ccm_w[i][-1]
+            ops.conv3x3(self.cc_buf[-1], self.cc_buf[-1].shape[1], self.cc_buf[-1].shape[1], B, g, g, mu_w, mu_b,
+                        self.MU, sw, sw, dt)
+            # sigma = cc_transform_scale[i](cat(latent_scales, y_hat[:nsup])) fused with the GC likelihood
+            self._stack(self.ccs_w[i], self.LS, M, M, sup_base + M * W4, nsup * sw, self.SUPW)
+            sg_w, sg_b = self.ccs_w[i][-1]
+            c4 = self.cc_buf[-1].shape[1]
+            ops.conv3x3_gaussian(self.cc_buf[-1], c4, c4, B, g, g, sg_w, sg_b, sw, self.Y, M, i * sw, self.MU, sw,
+                                 y_noise, self.YLIK, M, sup_base + cur * W4, self.SUPW, dt)
+            # lrp = lrp_transform[i](cat(mean_support, y_hat_slice)); y_hat += 0.5 tanh(lrp)
+            self._stack(self.lrp_w[i], SUP, cur + sw, self.SUPW, None, 0, 0)
+            lw, lb = self.lrp_w[i][-1]
+            dst2 = sup_base + cur * W4 if i < self.maxsup else None
+            ops.conv3x3_lrp(self.cc_buf[-1], c4, c4, B, g, g, lw, lb, sw, sup_base + cur * W4, self.SUPW,
+                            self.YH.data_ptr() + i * sw * W4, M, dst2, self.SUPW, dt)
+
+        # ---- g_s (MCM.py:790-792): transposed 1x1 convs back to E-dim tokens
+        x = self.YH
+        for j, (w, b) in enumerate(self.gs_w):
+            last = j == len(self.gs_w) - 1
+            ops.linear(x, w, b, dt, act=ops.ACT_NONE if last else ops.ACT_GELU, out=self.gs_buf[j])
+            x = self.gs_buf[j]
+
+        # ---- decoder (MCM.py:636-688): embed + unshuffle (+ off-by-one cls), blocks, norm, pred+unpatchify
+        pos_d = m.decoder_pos_embed.detach()
+        ops.decoder_embed(x, self.w_de, m.decoder_embed.bias.detach(), pos_d, shuf, self.dec, B, K, L, dt)
+        ops.mask_rows(self.dec, m.mask_token.detach(), pos_d, shuf, B, L, K, Dd)
+        for w in self.dec_w:
+            run_block(self.dec, w, B, Td, dt, self.dec_s)
+        ops.layernorm(self.dec, m.decoder_norm.weight, m.decoder_norm.bias, m.decoder_norm.eps, dt, rows=B * L,
+                      row_group=L, group_stride=Td, row_offset=1, out=self.dn)
+        x_hat = torch.empty((B, imgs.shape[1], self.img, self.img), dtype=torch.float32, device=self.device)
+        ops.decoder_pred(self.dn, self.w_dp, m.decoder_pred.bias.detach(), x_hat, B, L, P, dt)
+        return {"x_hat": x_hat, "y": self.YLIK.clone(), "z": self.ZLIK.clone(), "ids_restore": rest,
+                "ids_shuffle": shuf}
+
+    def _h_s(self, layers, out_final, ld_final):
+        B, dt = self.batch, self.dtype
+        x, cin, H = self.ZHAT, self.m.hyperprior_depth, self.hz
+        for j, (w, b, pshuf) in enumerate(layers):
+            last = j == len(layers) - 1
+            cout = w.shape[0]
+            if last:
+                out, ldo = out_final, ld_final
+            else:
+                out = self.hs_buf[j]
+                ldo = out.shape[1]
+            ops.conv3x3(x, cin, cin, B, H, H, w, b, out, ldo, cout, dt, act=ops.ACT_NONE if last else ops.ACT_GELU,
+                        pixel_shuffle=pshuf)
+            if pshuf:
+                H *= 2
+                cin = cout // 4
+            else:
+                cin = cout
+            x = out
+
+    def _stack(self, layers, x1, c1, ld1, x2, c2, ld2):
+        """first four convs (+GELU) of a 5-conv slice transform into cc_buf[0..3]."""
+        B, g, dt = self.batch, self.g, self.dtype
+        for j in range(4):
+            w, b = layers[j]
+            cout = w.shape[0]
+            out = self.cc_buf[j]
+            if j == 0:
+                ops.conv3x3(x1, c1, ld1, B, g, g, w, b, out, cout, cout, dt, act=ops.ACT_GELU, x2=x2, c2=c2, ld2=ld2)
+            else:
+                cin = self.cc_buf[j - 1].shape[1]
+                ops.conv3x3(self.cc_buf[j - 1], cin, cin, B, g, g, w, b, out, cout, cout, dt, act=ops.ACT_GELU)

@@ -1,0 +1,211 @@
+"""Tensor-level wrappers over the C ABI (include/tmae.h).
+
+Each wrapper checks device / dtype / contiguity on the host, then enqueues the HIP kernel on
+torch's current stream.  They allocate outputs with torch (the caching allocator owns all memory,
+the library never allocates) unless an `out=` buffer is passed.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+from ._lib import ACT_GELU, ACT_NONE, TMAE_BF16, TMAE_F32, EBParams
+
+__all__ = [
+    "ids_shuffle", "layernorm", "linear", "linear_residual", "patch_embed", "cls_rows", "mha", "decoder_embed",
+    "mask_rows", "decoder_pred", "conv3x3", "conv3x3_gaussian", "conv3x3_lrp", "eb_likelihood", "eb_aux_loss",
+    "gc_likelihood", "nhwc_to_nchw", "dtype_code", "TMAE_F32", "TMAE_BF16", "ACT_NONE", "ACT_GELU",
+]
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t):
+    """device address of a tensor, a raw int address (offset views into a workspace), or None"""
+    if t is None or isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+def _need(t: torch.Tensor, dtype=None, name="tensor"):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device (HIP) tensor")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return TMAE_F32
+    if dt == torch.bfloat16:
+        return TMAE_BF16
+    raise ValueError(f"unsupported compute dtype {dt}")
+
+
+# --------------------------------------------------------------------------------------- masking
+def ids_shuffle(scores: torch.Tensor, keep: int, sum_lanes: int = 8):
+    """MCM.get_ids_shuffle + argsort (MCM.py:364-423, 579-580) -> (ids_shuffle, ids_restore) int64."""
+    s = _need(scores.float().contiguous(), name="total_scores")
+    n, L = s.shape
+    shuf = torch.empty((n, L), dtype=torch.int64, device=s.device)
+    rest = torch.empty_like(shuf)
+    _lib.call("tmae_ids_shuffle", s.data_ptr(), shuf.data_ptr(), rest.data_ptr(), n, L, keep, sum_lanes, _stream())
+    return shuf, rest
+
+
+# --------------------------------------------------------------------------------------- transformer
+def layernorm(x, weight, bias, eps, out_dtype, rows=None, row_group=None, group_stride=0, row_offset=0, out=None):
+    _need(x, torch.float32, "x")
+    D = x.shape[-1]
+    rows = x.numel() // D if rows is None else rows
+    row_group = rows if row_group is None else row_group
+    if out is None:
+        out = torch.empty((rows, D), dtype=out_dtype, device=x.device)
+    _lib.call("tmae_layernorm_fwd", x.data_ptr(), weight.data_ptr(), bias.data_ptr(), out.data_ptr(), rows, D,
+              max(row_group, 1), group_stride, row_offset, float(eps), dtype_code(out.dtype), _stream())
+    return out
+
+
+def linear(x, w, b, dtype, act=ACT_NONE, out=None, out_dtype=None, M=None, ldx=None, row_group=None, group_stride=0,
+           row_offset=0):
+    """y = act(x W^T + b); x f32 or `dtype`; W [N][K] in `dtype`."""
+    N, K = w.shape
+    M = x.numel() // x.shape[-1] if M is None else M
+    ldx = x.shape[-1] if ldx is None else ldx
+    out_dtype = out_dtype or dtype
+    if out is None:
+        out = torch.empty((M, N), dtype=out_dtype, device=x.device)
+    code = dtype_code(dtype)
+    x_f32 = int(x.dtype == torch.float32)
+    if code == TMAE_BF16 and not x_f32 and x.dtype != torch.bfloat16:
+        raise ValueError("x must be f32 or bf16")
+    if code == TMAE_F32 and (x.dtype != torch.float32 or out.dtype != torch.float32):
+        raise ValueError("f32 path needs f32 tensors")
+    _lib.call("tmae_linear_fwd", x.data_ptr(), x_f32, ldx, row_group or M, group_stride, row_offset, w.data_ptr(),
+              _p(b), out.data_ptr(), int(out.dtype == torch.float32), out.shape[-1], M, N, K, act, code, _stream())
+    return out
+
+
+def linear_residual(x, w, b, resid, dtype):
+    N, K = w.shape
+    M = x.numel() // K
+    _lib.call("tmae_linear_residual_fwd", x.data_ptr(), K, w.data_ptr(), _p(b), resid.data_ptr(), resid.shape[-1], M,
+              N, K, dtype_code(dtype), _stream())
+    return resid
+
+
+def patch_embed(imgs, ids_shuffle, w, b, pos, tokens, keep, patch, dtype):
+    n, C, H, W = imgs.shape
+    D = w.shape[0]
+    L = ids_shuffle.shape[1]
+    _lib.call("tmae_patch_embed_fwd", _need(imgs, torch.float32, "imgs").data_ptr(), ids_shuffle.data_ptr(),
+              w.data_ptr(), b.data_ptr(), pos.data_ptr(), tokens.data_ptr(), n, C, H, W, patch, D, L, keep,
+              dtype_code(dtype), _stream())
+    return tokens
+
+
+def cls_rows(tokens, cls, pos, n, rows_per_img, D):
+    _lib.call("tmae_cls_rows", tokens.data_ptr(), cls.data_ptr(), pos.data_ptr(), n, rows_per_img, D, _stream())
+
+
+def mha(qkv, B, T, H, dh, scale, dtype, out=None):
+    if out is None:
+        out = torch.empty((B * T, H * dh), dtype=dtype, device=qkv.device)
+    _lib.call("tmae_mha_fwd", qkv.data_ptr(), out.data_ptr(), B, T, H, dh, float(scale), dtype_code(dtype), _stream())
+    return out
+
+
+def decoder_embed(x, w, b, pos, ids_shuffle, out, n, ntok, L, dtype):
+    D, Din = w.shape
+    _lib.call("tmae_decoder_embed_fwd", x.data_ptr(), int(x.dtype == torch.float32), w.data_ptr(), b.data_ptr(),
+              pos.data_ptr(), ids_shuffle.data_ptr(), out.data_ptr(), n, ntok, L, Din, D, dtype_code(dtype),
+              _stream())
+
+
+def mask_rows(out, mask_token, pos, ids_shuffle, n, L, ntok, D):
+    _lib.call("tmae_mask_rows", out.data_ptr(), mask_token.data_ptr(), pos.data_ptr(), ids_shuffle.data_ptr(), n, L,
+              ntok, D, _stream())
+
+
+def decoder_pred(x, w, b, imgs, n, L, patch, dtype):
+    N, Din = w.shape
+    C, H, W = imgs.shape[1:]
+    _lib.call("tmae_decoder_pred_fwd", x.data_ptr(), w.data_ptr(), b.data_ptr(), imgs.data_ptr(), n, L, Din, C, H, W,
+              patch, dtype_code(dtype), _stream())
+
+
+# --------------------------------------------------------------------------------------- LIC
+def conv3x3(x1, c1, ld1, n, H, W, w, b, y, ldy, cout, dtype, stride=1, act=ACT_NONE, pixel_shuffle=False, x2=None,
+            c2=0, ld2=0):
+    _lib.call("tmae_conv3x3_fwd", _p(x1), c1, ld1, _p(x2), c2, ld2, n, H, W, stride, _p(w), _p(b),
+              _p(y), ldy, cout, act, int(pixel_shuffle), dtype_code(dtype), _stream())
+
+
+def conv3x3_gaussian(x1, c1, ld1, n, H, W, w, b, cout, y, ldy, yoff, mu, ldmu, noise, lik, Mtot, yhat, ldh, dtype,
+                     x2=None, c2=0, ld2=0):
+    _lib.call("tmae_conv3x3_gaussian_fwd", _p(x1), c1, ld1, _p(x2), c2, ld2, n, H, W, _p(w),
+              _p(b), cout, _p(y), ldy, yoff, _p(mu), ldmu, _p(noise), _p(lik), Mtot,
+              _p(yhat), ldh, dtype_code(dtype), _stream())
+
+
+def conv3x3_lrp(x1, c1, ld1, n, H, W, w, b, cout, src, ld_src, dst1, ld_dst1, dst2, ld_dst2, dtype, x2=None,
+                c2=0, ld2=0):
+    _lib.call("tmae_conv3x3_lrp_fwd", _p(x1), c1, ld1, _p(x2), c2, ld2, n, H, W, _p(w), _p(b),
+              cout, _p(src), ld_src, _p(dst1), ld_dst1, _p(dst2), ld_dst2, dtype_code(dtype), _stream())
+
+
+def _eb_params(eb) -> EBParams:
+    p = EBParams()
+    for i in range(5):
+        p.matrix[i] = getattr(eb, f"_matrix{i}").data_ptr()
+        p.bias[i] = getattr(eb, f"_bias{i}").data_ptr()
+        if i < 4:
+            p.factor[i] = getattr(eb, f"_factor{i}").data_ptr()
+    p.quantiles = eb.quantiles.data_ptr()
+    return p
+
+
+def eb_likelihood(eb, z_nhwc, n, C, HW, noise=None, lik=None, zhat=None, table=None):
+    """EntropyBottleneck forward on NHWC z: returns (lik NCHW, z_hat NHWC)."""
+    dev = z_nhwc.device
+    if lik is None:
+        lik = torch.empty((n, C, HW), dtype=torch.float32, device=dev)
+    if zhat is None:
+        zhat = torch.empty((n * HW, C), dtype=torch.float32, device=dev)
+    if table is None:
+        table = torch.empty((C, 59), dtype=torch.float32, device=dev)
+    params = _eb_params(eb)
+    _lib.call("tmae_eb_likelihood_fwd", z_nhwc.data_ptr(), params, _p(noise), lik.data_ptr(), _p(zhat),
+              table.data_ptr(), n, C, HW, _stream())
+    return lik, zhat
+
+
+def eb_aux_loss(eb, out=None, table=None):
+    C = eb.channels
+    dev = eb.quantiles.device
+    out = torch.empty((), dtype=torch.float32, device=dev) if out is None else out
+    table = torch.empty((C, 59), dtype=torch.float32, device=dev) if table is None else table
+    params = _eb_params(eb)
+    _lib.call("tmae_eb_aux_loss", params, eb.target.data_ptr(), out.data_ptr(), table.data_ptr(), C, _stream())
+    return out
+
+
+def gc_likelihood(x, scales, means=None, noise=None, scale_bound=0.11):
+    x = _need(x.contiguous(), torch.float32, "inputs")
+    lik = torch.empty_like(x)
+    xt = torch.empty_like(x)
+    _lib.call("tmae_gc_likelihood_fwd", x.data_ptr(), _need(scales.contiguous(), torch.float32, "scales").data_ptr(),
+              _p(None if means is None else means.contiguous()), _p(noise), xt.data_ptr(), lik.data_ptr(), x.numel(),
+              float(scale_bound), _stream())
+    return xt, lik
+
+
+def nhwc_to_nchw(x, ldx, n, C, H, W, out=None):
+    out = torch.empty((n, C, H, W), dtype=torch.float32, device=x.device) if out is None else out
+    _lib.call("tmae_nhwc_to_nchw", x.data_ptr(), ldx, out.data_ptr(), n, C, H * W, _stream())
+    return out

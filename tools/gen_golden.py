@@ -195,6 +195,19 @@ def gen_mae_masking():
     print("mae_masking.npz")
 
 
+def gen_state_keys(MCM):
+    """ordered state_dict keys + shapes of the default reference MCM (checkpoint compatibility)"""
+    import json
+
+    torch.manual_seed(0)
+    ref = MCM(num_keep_patches=144)
+    sd = ref.state_dict()
+    init_sha = sha16(np.concatenate([v.float().numpy().ravel() for v in sd.values() if v.numel()]))
+    with open(os.path.join(OUT, "mcm_state_keys.json"), "w") as f:
+        json.dump({"keys": {k: list(v.shape) for k, v in sd.items()}, "init_sha_seed0": init_sha}, f)
+    print("mcm_state_keys.json")
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     install_stubs()
@@ -207,6 +220,7 @@ def main():
     gen_forward(MCM, "tiny", TINY, batch=2, seed=7)
     gen_forward(MCM, "small12", SMALL12, batch=2, seed=11)
     gen_mae_masking()
+    gen_state_keys(MCM)
 
 
 if __name__ == "__main__":
