@@ -52,10 +52,11 @@ int tmae_layernorm_fwd(const float* x, const float* gamma, const float* beta, vo
 
 /* y[M][N] = act(x[M][K] · w[N][K]^T + bias).  x is f32 (x_f32=1) or dtype; y is f32 (y_f32=1) or dtype.
  * nn.Linear / 1x1 Conv2d (g_a, MCM.py:77-93) / 1x1 ConvTranspose2d with pre-transposed weight (g_s,
- * MCM.py:96-112).  Same row remap as tmae_layernorm_fwd. */
+ * MCM.py:96-112).  Same row remap as tmae_layernorm_fwd.  y32 (optional): second f32 copy of the output
+ * (g_a's last layer feeds the f32 Gaussian likelihood and the bf16 h_a convs). */
 int tmae_linear_fwd(const void* x, int x_f32, int ldx, int row_group, int group_stride, int row_offset,
-                    const void* w, const float* bias, void* y, int y_f32, int ldy, int M, int N, int K, int act,
-                    int dtype, void* stream);
+                    const void* w, const float* bias, void* y, int y_f32, int ldy, float* y32, int ld32, int M, int N,
+                    int K, int act, int dtype, void* stream);
 
 /* resid[M][N] += x[M][K] · w[N][K]^T + bias   (Attention.proj / Mlp.fc2 + the Block residual adds) */
 int tmae_linear_residual_fwd(const void* x, int ldx, const void* w, const float* bias, float* resid, int ldr,
@@ -92,25 +93,36 @@ int tmae_decoder_pred_fwd(const void* x, const void* w, const float* bias, float
 
 /* ---- learned-image-compression stack (MCM.py:729-792), NHWC f32 feature maps ------------------ */
 
-/* 3x3 conv, padding 1 (compressai conv3x3 / nn.Conv2d(k=3, p=1), MCM.py:115-293), input channels
- * [0,c1) from x1 and [c1,c1+c2) from x2 (torch.cat without a copy).  w = [cout][3][3][c1+c2].
- * pixel_shuffle=1: subpel_conv3x3 r=2 (conv + PixelShuffle(2)), output [n][2H][2W][cout/4]. */
-int tmae_conv3x3_fwd(const float* x1, int c1, int ld1, const float* x2, int c2, int ld2, int n, int H, int W,
-                     int stride, const void* w, const float* bias, float* y, int ldy, int cout, int act,
-                     int pixel_shuffle, int dtype, void* stream);
+/* Batched 3x3 conv, padding 1 (compressai conv3x3 / nn.Conv2d(k=3, p=1), MCM.py:115-293) as an implicit
+ * GEMM.  Inputs are NHWC in the operand dtype; channels [0,c1) come from x1 and [c1,c1+c2) from x2
+ * (torch.cat without a copy).  w = [cout][3][3][c1+c2].  nb1*nb2 independent problems run in one
+ * launch: problem b = b1*nb2 + b2 offsets every pointer by b1*s1 + b2*s2 elements.
+ * Epilogue: y = act(acc + bias + addend) (addend optional: precomputed partial sums), optional f32 copy
+ * y32; pixel_shuffle=1 -> subpel_conv3x3 r=2 (output [n][2H][2W][cout/4]); lrp_src set -> the last
+ * lrp_transform conv: y (and y2) = lrp_src + 0.5*tanh(acc + bias)  (MCM.py:779-784). */
+typedef struct tmae_conv_args {
+  const void* x1; int c1, ld1; long long x1_s1, x1_s2;
+  const void* x2; int c2, ld2; long long x2_s1, x2_s2;
+  int n, H, W, stride;
+  const void* w; long long w_s1, w_s2;
+  const float* bias; long long b_s1, b_s2;
+  int cout, act, pixel_shuffle;
+  void* y; int y_f32, ldy; long long y_s1, y_s2;
+  float* y32; int ld32; long long y32_s1, y32_s2;
+  const float* addend; int ld_add; long long a_s1, a_s2;
+  const float* lrp_src; int ld_src; long long src_s1, src_s2;
+  void* y2; int ldy2; long long y2_s1, y2_s2;
+  int nb1, nb2;
+} tmae_conv_args;
+int tmae_conv3x3(const tmae_conv_args* args, int dtype, void* stream);
 
-/* last cc_transform_scale conv fused with GaussianConditional likelihood and y_hat quantisation
- * (MCM.py:767-776): sigma = conv + bias; lik[NCHW, channels yoff..] = GC(y~, sigma, mu);
- * yhat[NHWC] = round(y - mu) + mu.  noise (NCHW [n][Mtot][H][W]) selects training mode. */
-int tmae_conv3x3_gaussian_fwd(const float* x1, int c1, int ld1, const float* x2, int c2, int ld2, int n, int H,
-                              int W, const void* w, const float* bias, int cout, const float* y, int ldy, int yoff,
-                              const float* mu, int ldmu, const float* noise, float* lik, int Mtot, float* yhat,
-                              int ldh, int dtype, void* stream);
-
-/* last lrp_transform conv fused with y_hat += 0.5 * tanh(lrp) (MCM.py:779-784) */
-int tmae_conv3x3_lrp_fwd(const float* x1, int c1, int ld1, const float* x2, int c2, int ld2, int n, int H, int W,
-                         const void* w, const float* bias, int cout, const float* src, int ld_src, float* dst1,
-                         int ld_dst1, float* dst2, int ld_dst2, int dtype, void* stream);
+/* GaussianConditional likelihood + y_hat quantisation for `nslices` consecutive slices of width sw
+ * (MCM.py:767-776): lik[NCHW channel yoff + j*sw + c] = GC(y~, max(sigma, .11), mu), LowerBound 1e-9;
+ * yhat (dtype yhat_dtype) and yhat32 (f32, optional) [pixel][channel] = round(y - mu) + mu.
+ * noise (NCHW like lik) selects the training-mode y~ = y + noise. */
+int tmae_gc_slices_fwd(const float* y, int ldy, int yoff, const float* mu, const float* sigma, long long ms_stride,
+                       int ld_ms, const float* noise, float* lik, int Mtot, void* yhat, int yhat_dtype, int ld_yhat,
+                       float* yhat32, int ld32, int n, int HW, int nslices, int sw, void* stream);
 
 /* compressai EntropyBottleneck parameters (filters = (3, 3, 3, 3)), all f32 device pointers */
 typedef struct tmae_eb_params {
@@ -121,9 +133,10 @@ typedef struct tmae_eb_params {
 } tmae_eb_params;
 
 /* EntropyBottleneck forward likelihood (MCM.py:741) + z_hat = round(z - median) + median
- * (MCM.py:742-744).  z, zhat NHWC [n*HW][C]; lik, noise NCHW.  table: device scratch C*59 f32. */
+ * (MCM.py:742-744).  z, zhat NHWC [n*HW][C] (zhat in zhat_dtype); lik, noise NCHW.
+ * table: device scratch C*59 f32. */
 int tmae_eb_likelihood_fwd(const float* z, const tmae_eb_params* params, const float* noise, float* lik,
-                           float* zhat, float* table, int n, int C, int HW, void* stream);
+                           void* zhat, int zhat_dtype, float* table, int n, int C, int HW, void* stream);
 
 /* CompressionModel.aux_loss (utils/engine.py:79): out[0] = sum |f(quantiles) - target| */
 int tmae_eb_aux_loss(const tmae_eb_params* params, const float* target, float* out, float* table, int C,

@@ -43,10 +43,12 @@ def test_host_side_validation(tmae):
         _lib.call("tmae_ids_shuffle", None, None, None, 2, 16, 17, 8, None)
     with pytest.raises(ValueError, match="head dim"):
         _lib.call("tmae_mha_fwd", None, None, 1, 10, 2, 48, ctypes.c_float(1.0), 0, None)
+    a = _lib.ConvArgs()
+    a.c1, a.ld1, a.n, a.H, a.W, a.stride, a.cout, a.nb1, a.nb2, a.y_f32 = 20, 20, 1, 4, 4, 1, 8, 1, 1, 1
     with pytest.raises(ValueError, match="multiples of"):
-        _lib.call("tmae_conv3x3_fwd", None, 20, 20, None, 0, 0, 1, 4, 4, 1, None, None, None, 8, 8, 0, 0, 1, None)
+        _lib.call("tmae_conv3x3", ctypes.byref(a), 1, None)
     with pytest.raises(ValueError, match="K=30"):
-        _lib.call("tmae_linear_fwd", None, 0, 30, 1, 0, 0, None, None, None, 0, 8, 4, 8, 30, 0, 1, None)
+        _lib.call("tmae_linear_fwd", None, 0, 30, 1, 0, 0, None, None, None, 0, 8, None, 0, 4, 8, 30, 0, 1, None)
 
 
 def test_missing_library_fails_loudly(tmae, monkeypatch):

@@ -116,11 +116,20 @@ def test_mha(tmae, B, T, H, dh, dtype):
 
 
 # ------------------------------------------------------------------------------------ convs
+def _nhwc(x, dtype):
+    return x.permute(0, 2, 3, 1).contiguous().to(dtype).to(DEV)
+
+
+def _wk(w, dtype):
+    return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1).contiguous().to(dtype).to(DEV)
+
+
 @pytest.mark.parametrize("stride", [1, 2])
 @pytest.mark.parametrize("dtype", DTYPES)
-def test_conv3x3_two_segments(tmae, stride, dtype):
-    torch.manual_seed(stride)
-    n, H, c1, c2, cout = 3, 12, 40, 24, 48
+@pytest.mark.parametrize("H", [12, 3, 7])
+def test_conv3x3_two_segments(tmae, stride, dtype, H):
+    torch.manual_seed(stride + H)
+    n, c1, c2, cout = 3, 40, 24, 48
     xa, xb = torch.randn(n, c1, H, H), torch.randn(n, c2, H, H)
     w, b = torch.randn(cout, c1 + c2, 3, 3) / (9 * (c1 + c2)) ** 0.5, torch.randn(cout)
     ref = F.gelu(F.conv2d(torch.cat([xa, xb], 1).to(dtype).float(), w.to(dtype).float(), b, stride=stride,
@@ -129,13 +138,55 @@ def test_conv3x3_two_segments(tmae, stride, dtype):
     # segment 2 lives inside a wider NHWC buffer (channel offset + stride)
     wide = torch.zeros(n, H, H, c2 + 16)
     wide[..., 8:8 + c2] = xb.permute(0, 2, 3, 1)
-    wide = wide.to(DEV)
-    x1 = xa.permute(0, 2, 3, 1).contiguous().to(DEV)
+    wide = wide.to(dtype).to(DEV)
     y = torch.empty(n * Ho * Ho, cout, device=DEV)
-    wk = w.permute(0, 2, 3, 1).contiguous().to(dtype).to(DEV)
-    tmae.ops.conv3x3(x1, c1, c1, n, H, H, wk, b.to(DEV), y, cout, cout, dtype, stride=stride, act=1,
-                     x2=wide.data_ptr() + 8 * 4, c2=c2, ld2=c2 + 16)
+    tmae.ops.conv3x3(_nhwc(xa, dtype), c1, c1, n, H, H, _wk(w, dtype), b.to(DEV), y, cout, cout, dtype,
+                     stride=stride, act=1, x2=wide.data_ptr() + 8 * wide.element_size(), c2=c2, ld2=c2 + 16)
     assert rel(y.view(n, Ho, Ho, cout).permute(0, 3, 1, 2), ref) < tol(dtype)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_conv3x3_batched_addend(tmae, dtype):
+    """nb1 x nb2 problems in one launch, per-problem weights/bias/addend/outputs, shared input"""
+    torch.manual_seed(11)
+    n, H, cin, cout, nb1, nb2 = 2, 12, 64, 32, 2, 3
+    x = torch.randn(n, cin, H, H)
+    w = torch.randn(nb1, nb2, cout, cin, 3, 3) / (9 * cin) ** 0.5
+    b = torch.randn(nb1, nb2, cout)
+    add = torch.randn(n * H * H, 7 * cout)  # problem (b1, b2) reads columns (3*b1 + b2)*cout
+    y = torch.empty(nb1, nb2, n * H * H, cout, device=DEV)
+    wk = torch.stack([torch.stack([w[i, j].permute(0, 2, 3, 1).reshape(cout, -1) for j in range(nb2)])
+                      for i in range(nb1)]).to(dtype).contiguous().to(DEV)
+    tmae.ops.conv3x3(_nhwc(x, dtype), cin, cin, n, H, H, wk, b.to(DEV), y, cout, cout, dtype, act=1,
+                     addend=add.to(DEV), ld_add=7 * cout, nb=(nb1, nb2),
+                     strides={"w": (nb2 * cout * 9 * cin, cout * 9 * cin), "b": (nb2 * cout, cout),
+                              "a": (3 * cout, cout), "y": (nb2 * n * H * H * cout, n * H * H * cout)})
+    for i in range(nb1):
+        for j in range(nb2):
+            ref = F.conv2d(x.to(dtype).float(), w[i, j].to(dtype).float(), b[i, j], padding=1)
+            ref = F.gelu(ref.permute(0, 2, 3, 1).reshape(-1, cout) + add[:, (3 * i + j) * cout:(3 * i + j + 1) * cout])
+            assert rel(y[i, j], ref) < tol(dtype), (i, j)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_conv3x3_lrp_epilogue(tmae, dtype):
+    torch.manual_seed(12)
+    n, H, cin, cout = 2, 12, 80, 32
+    x = torch.randn(n, cin, H, H)
+    w, b = torch.randn(cout, cin, 3, 3) / (9 * cin) ** 0.5, torch.randn(cout)
+    src = torch.randn(n * H * H, 96) * 4
+    ref = src[:, 40:72] + 0.5 * torch.tanh(
+        F.conv2d(x.to(dtype).float(), w.to(dtype).float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, cout))
+    y = torch.zeros(n * H * H, 96, dtype=dtype, device=DEV)
+    y2 = torch.zeros(n * H * H, 64, dtype=dtype, device=DEV)
+    s = src.to(DEV)
+    es = y.element_size()
+    tmae.ops.conv3x3(_nhwc(x, dtype), cin, cin, n, H, H, _wk(w, dtype), b.to(DEV), y.data_ptr() + 40 * es, 96, cout,
+                     dtype, y_f32=(dtype == torch.float32), lrp_src=s.data_ptr() + 40 * 4, ld_src=96,
+                     y2=y2.data_ptr() + 16 * es, ldy2=64)
+    assert rel(y[:, 40:72].float(), ref) < tol(dtype)
+    assert rel(y2[:, 16:48].float(), ref) < tol(dtype)
+    assert float(y[:, :40].abs().max()) == 0.0 and float(y[:, 72:].abs().max()) == 0.0
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
@@ -144,12 +195,40 @@ def test_subpel_conv(tmae, dtype):
     n, H, cin, c = 2, 6, 48, 16
     x = torch.randn(n, cin, H, H)
     w, b = torch.randn(4 * c, cin, 3, 3) / (9 * cin) ** 0.5, torch.randn(4 * c)
-    ref = F.pixel_shuffle(F.conv2d(x.to(dtype).float(), w.to(dtype).float(), b, padding=1), 2)
+    ref = F.gelu(F.pixel_shuffle(F.conv2d(x.to(dtype).float(), w.to(dtype).float(), b, padding=1), 2))
     y = torch.empty(n * 4 * H * H, c, device=DEV)
-    tmae.ops.conv3x3(x.permute(0, 2, 3, 1).contiguous().to(DEV), cin, cin, n, H, H,
-                     w.permute(0, 2, 3, 1).contiguous().to(dtype).to(DEV), b.to(DEV), y, c, 4 * c, dtype,
-                     pixel_shuffle=True)
+    tmae.ops.conv3x3(_nhwc(x, dtype), cin, cin, n, H, H, _wk(w, dtype), b.to(DEV), y, c, 4 * c, dtype,
+                     act=1, pixel_shuffle=True)
     assert rel(y.view(n, 2 * H, 2 * H, c).permute(0, 3, 1, 2), ref) < tol(dtype)
+
+
+@pytest.mark.parametrize("training", [False, True])
+@pytest.mark.parametrize("yt", DTYPES)
+def test_gc_slices(tmae, training, yt):
+    torch.manual_seed(21)
+    n, HW, M, sw, nsl, yoff = 2, 16, 96, 16, 3, 32
+    y = torch.randn(n * HW, M) * 5
+    mu = torch.randn(2, nsl, n * HW, sw)
+    sigma = torch.rand(nsl, n * HW, sw) * 3
+    musig = torch.stack([mu[0], sigma])  # [mu | sigma] blocks like the executor's MUSIG
+    noise = torch.rand(n, M, HW) - 0.5 if training else None
+    lik = torch.zeros(n, M, HW, device=DEV)
+    yh = torch.zeros(n * HW, M, dtype=yt, device=DEV)
+    yh32 = torch.zeros(n * HW, M, device=DEV)
+    ms = musig.to(DEV)
+    tmae.ops.gc_slices(y.to(DEV), M, yoff, ms, ms.data_ptr() + nsl * n * HW * sw * 4, n * HW * sw, sw,
+                       None if noise is None else noise.to(DEV), lik, M, yh, yt, M, yh32, M, n, HW, nsl, sw)
+    for j in range(nsl):
+        ch = slice(yoff + j * sw, yoff + (j + 1) * sw)
+        ys = y[:, ch].reshape(n, HW, sw).permute(0, 2, 1)
+        mj = mu[0, j].reshape(n, HW, sw).permute(0, 2, 1)
+        sj = sigma[j].reshape(n, HW, sw).permute(0, 2, 1)
+        nz = None if noise is None else noise[:, ch]
+        ref = orc.gaussian_conditional(ys, sj, mj, nz)
+        assert rel(lik[:, ch].cpu(), ref) < 1e-5
+        q = (torch.round(ys - mj) + mj).permute(0, 2, 1).reshape(-1, sw)
+        assert torch.equal(yh32[:, ch].cpu(), q)
+        assert rel(yh[:, ch].float(), q) <= (0 if yt == torch.float32 else 1e-2)
 
 
 # ------------------------------------------------------------------------------------ entropy models

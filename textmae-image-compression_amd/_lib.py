@@ -17,6 +17,27 @@ ACT_NONE, ACT_GELU = 0, 1
 P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 
 
+LL = ctypes.c_longlong
+
+
+class ConvArgs(ctypes.Structure):
+    """mirror of tmae_conv_args (include/tmae.h)"""
+    _fields_ = [
+        ("x1", P), ("c1", I), ("ld1", I), ("x1_s1", LL), ("x1_s2", LL),
+        ("x2", P), ("c2", I), ("ld2", I), ("x2_s1", LL), ("x2_s2", LL),
+        ("n", I), ("H", I), ("W", I), ("stride", I),
+        ("w", P), ("w_s1", LL), ("w_s2", LL),
+        ("bias", P), ("b_s1", LL), ("b_s2", LL),
+        ("cout", I), ("act", I), ("pixel_shuffle", I),
+        ("y", P), ("y_f32", I), ("ldy", I), ("y_s1", LL), ("y_s2", LL),
+        ("y32", P), ("ld32", I), ("y32_s1", LL), ("y32_s2", LL),
+        ("addend", P), ("ld_add", I), ("a_s1", LL), ("a_s2", LL),
+        ("lrp_src", P), ("ld_src", I), ("src_s1", LL), ("src_s2", LL),
+        ("y2", P), ("ldy2", I), ("y2_s1", LL), ("y2_s2", LL),
+        ("nb1", I), ("nb2", I),
+    ]
+
+
 class EBParams(ctypes.Structure):
     _fields_ = [("matrix", ctypes.c_void_p * 5), ("bias", ctypes.c_void_p * 5), ("factor", ctypes.c_void_p * 4),
                 ("quantiles", ctypes.c_void_p)]
@@ -27,7 +48,7 @@ SIGNATURES = {
     "tmae_abi_version": [],
     "tmae_ids_shuffle": [P, P, P, I, I, I, I, P],
     "tmae_layernorm_fwd": [P, P, P, P, I, I, I, I, I, F, I, P],
-    "tmae_linear_fwd": [P, I, I, I, I, I, P, P, P, I, I, I, I, I, I, I, P],
+    "tmae_linear_fwd": [P, I, I, I, I, I, P, P, P, I, I, P, I, I, I, I, I, I, P],
     "tmae_linear_residual_fwd": [P, I, P, P, P, I, I, I, I, I, P],
     "tmae_patch_embed_fwd": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "tmae_cls_rows": [P, P, P, I, I, I, P],
@@ -35,10 +56,9 @@ SIGNATURES = {
     "tmae_decoder_embed_fwd": [P, I, P, P, P, P, P, I, I, I, I, I, I, P],
     "tmae_mask_rows": [P, P, P, P, I, I, I, I, P],
     "tmae_decoder_pred_fwd": [P, P, P, P, I, I, I, I, I, I, I, I, P],
-    "tmae_conv3x3_fwd": [P, I, I, P, I, I, I, I, I, I, P, P, P, I, I, I, I, I, P],
-    "tmae_conv3x3_gaussian_fwd": [P, I, I, P, I, I, I, I, I, P, P, I, P, I, I, P, I, P, P, I, P, I, I, P],
-    "tmae_conv3x3_lrp_fwd": [P, I, I, P, I, I, I, I, I, P, P, I, P, I, P, I, P, I, I, P],
-    "tmae_eb_likelihood_fwd": [P, ctypes.POINTER(EBParams), P, P, P, P, I, I, I, P],
+    "tmae_conv3x3": [ctypes.POINTER(ConvArgs), I, P],
+    "tmae_gc_slices_fwd": [P, I, I, P, P, LL, I, P, P, I, P, I, I, P, I, I, I, I, I, P],
+    "tmae_eb_likelihood_fwd": [P, ctypes.POINTER(EBParams), P, P, P, I, P, I, I, I, P],
     "tmae_eb_aux_loss": [ctypes.POINTER(EBParams), P, P, P, I, P],
     "tmae_gc_likelihood_fwd": [P, P, P, P, P, P, I, F, P],
     "tmae_nhwc_to_nchw": [P, I, P, I, I, I, P],

@@ -1,0 +1,174 @@
+// LIC 3x3 convolutions (h_a, h_s, cc_transform_mean/scale, lrp_transform; MCM.py:115-293) as
+// implicit GEMMs on the MFMA core, batched over independent problems (mean/scale chains of one
+// slice; slices 6..11 whose support is fixed), plus the Gaussian-conditional slice kernel.
+#include "gemm_core.h"
+
+// conv + PixelShuffle(2) (compressai subpel_conv3x3, r=2): conv channel co = c*4 + i*2 + j goes to
+// pixel (2y+i, 2x+j), channel c of the NHWC output.
+template <typename OT, int ACT> struct EpiPixelShuffle2 {
+  OT* out;
+  const float* bias;
+  int H, W, ldo;
+  BStride so, sb;
+  __device__ void batch(int b1, int b2) { out += so.at(b1, b2); bias += sb.at(b1, b2); }
+  __device__ void operator()(int m, int n, f32x4 v) const {
+    const int hw = H * W;
+    const int b = m / hw, rem = m - b * hw;
+    const int y = rem / W, x = rem - y * W;
+    v += load4f(bias + n);
+    const int c = n >> 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float o = v[j];
+      if (ACT == TMAE_ACT_GELU) o = gelu_erf(o);
+      const int oy = 2 * y + (j >> 1), ox = 2 * x + (j & 1);
+      out[(((size_t)b * 2 * H + oy) * 2 * W + ox) * ldo + c] = to_out<OT>(o);
+    }
+  }
+};
+
+// last lrp_transform conv: y_hat = y_hat_pre + 0.5 * tanh(acc + bias)  (MCM.py:779-784)
+template <typename OT> struct EpiLRP {
+  const float* src;
+  int lds;
+  OT* out;
+  int ldo;
+  OT* out2;  // optional
+  int ldo2;
+  const float* bias;
+  BStride ssrc, so, so2, sb;
+  __device__ void batch(int b1, int b2) {
+    src += ssrc.at(b1, b2);
+    out += so.at(b1, b2);
+    if (out2) out2 += so2.at(b1, b2);
+    bias += sb.at(b1, b2);
+  }
+  __device__ void operator()(int m, int n, f32x4 v) const {
+    v += load4f(bias + n);
+    f32x4 o = load4f(src + (size_t)m * lds + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = o[j] + 0.5f * tanhf(v[j]);
+    store4(out + (size_t)m * ldo + n, o);
+    if (out2) store4(out2 + (size_t)m * ldo2 + n, o);
+  }
+};
+
+template <typename T>
+static int conv_t(const tmae_conv_args& a, hipStream_t st) {
+  const int e = Elt<T>::EPC;
+  TMAE_REQUIRE(a.c1 % e == 0 && a.c2 % e == 0 && a.ld1 % e == 0 && (a.c2 == 0 || a.ld2 % e == 0) && a.cout % 4 == 0,
+               "tmae_conv3x3: channel counts (%d + %d -> %d) must be multiples of %d", a.c1, a.c2, a.cout, e);
+  TMAE_REQUIRE(a.stride == 1 || a.stride == 2, "tmae_conv3x3: stride %d", a.stride);
+  TMAE_REQUIRE(!(a.pixel_shuffle && a.lrp_src), "tmae_conv3x3: pixel_shuffle and lrp are exclusive");
+  TMAE_REQUIRE(a.nb1 >= 1 && a.nb2 >= 1, "tmae_conv3x3: batch %d x %d", a.nb1, a.nb2);
+  ConvSrc<T> xs;
+  xs.x1 = (const T*)a.x1; xs.x2 = (const T*)a.x2; xs.c1 = a.c1; xs.ld1 = a.ld1; xs.ld2 = a.ld2;
+  xs.Cin = a.c1 + a.c2; xs.H = a.H; xs.W = a.W;
+  xs.Ho = (a.H + 2 - 3) / a.stride + 1; xs.Wo = (a.W + 2 - 3) / a.stride + 1; xs.stride = a.stride;
+  xs.rows = a.n * xs.Ho * xs.Wo; xs.K = 9 * xs.Cin; xs.inv_cin = xs.Cin ? 1.0f / (float)xs.Cin : 0.0f;
+  xs.bs1 = BStride{a.x1_s1, a.x1_s2}; xs.bs2 = BStride{a.x2_s1, a.x2_s2};
+  const int M = xs.rows, K = xs.K, N = a.cout;
+  const T* W = (const T*)a.w;
+  const char* nm = "tmae_conv3x3";
+#define TMAE_GO(EPI) return launch_gemm<true, T>(nm, W, a.w_s1, a.w_s2, N, K, xs, EPI, M, a.nb1, a.nb2, st)
+  if (a.pixel_shuffle) {
+    TMAE_REQUIRE(a.stride == 1, "tmae_conv3x3: pixel shuffle needs stride 1");
+    if (a.y_f32) {
+      EpiPixelShuffle2<float, 1> g{(float*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2}};
+      EpiPixelShuffle2<float, 0> l{(float*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2}};
+      if (a.act == TMAE_ACT_GELU) TMAE_GO(g);
+      TMAE_GO(l);
+    }
+    EpiPixelShuffle2<T, 1> g{(T*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2}};
+    EpiPixelShuffle2<T, 0> l{(T*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2}};
+    if (a.act == TMAE_ACT_GELU) TMAE_GO(g);
+    TMAE_GO(l);
+  }
+  if (a.lrp_src) {
+    TMAE_REQUIRE(!a.y_f32 || sizeof(T) == 4, "tmae_conv3x3: lrp output must be in the operand dtype");
+    EpiLRP<T> r{a.lrp_src, a.ld_src, (T*)a.y, a.ldy, (T*)a.y2, a.ldy2, a.bias, {a.src_s1, a.src_s2},
+                {a.y_s1, a.y_s2}, {a.y2_s1, a.y2_s2}, {a.b_s1, a.b_s2}};
+    TMAE_GO(r);
+  }
+  if (a.y_f32) {
+    auto g = make_store<float, 1>((float*)a.y, a.ldy, a.bias);
+    auto l = make_store<float, 0>((float*)a.y, a.ldy, a.bias);
+    g.so = l.so = BStride{a.y_s1, a.y_s2};
+    g.sb = l.sb = BStride{a.b_s1, a.b_s2};
+    g.addend = l.addend = a.addend;
+    g.ld_add = l.ld_add = a.ld_add;
+    g.sa = l.sa = BStride{a.a_s1, a.a_s2};
+    if (a.act == TMAE_ACT_GELU) TMAE_GO(g);
+    TMAE_GO(l);
+  }
+  auto g = make_store<T, 1>((T*)a.y, a.ldy, a.bias);
+  auto l = make_store<T, 0>((T*)a.y, a.ldy, a.bias);
+  g.so = l.so = BStride{a.y_s1, a.y_s2};
+  g.sb = l.sb = BStride{a.b_s1, a.b_s2};
+  g.addend = l.addend = a.addend;
+  g.ld_add = l.ld_add = a.ld_add;
+  g.sa = l.sa = BStride{a.a_s1, a.a_s2};
+  g.out32 = l.out32 = a.y32;
+  g.ld32 = l.ld32 = a.ld32;
+  g.s32 = l.s32 = BStride{a.y32_s1, a.y32_s2};
+  if (a.act == TMAE_ACT_GELU) TMAE_GO(g);
+  TMAE_GO(l);
+#undef TMAE_GO
+}
+
+extern "C" int tmae_conv3x3(const tmae_conv_args* args, int dtype, void* stream) {
+  TMAE_REQUIRE(args != nullptr, "tmae_conv3x3: args is NULL");
+  if (dtype == TMAE_BF16) return conv_t<bf16>(*args, (hipStream_t)stream);
+  TMAE_REQUIRE(args->y_f32 || args->lrp_src, "tmae_conv3x3: the f32 path writes f32 outputs");
+  return conv_t<float>(*args, (hipStream_t)stream);
+}
+
+// ------------------------------------------------------------------ Gaussian conditional, per slice
+// compressai GaussianConditional forward (LowerBound(0.11) on scales, erfc CDF, LowerBound(1e-9))
+// for `nslices` consecutive slices of width sw, and y_hat = round(y - mu) + mu (quantize_ste forward
+// value, MCM.py:767-776).  Element (pixel m, slice j, channel c) of the latent channel
+// ch = yoff + j*sw + c; mu/sigma of slice j at mu[j*ms_stride + m*ld_ms + c].
+template <typename YT>
+__global__ void __launch_bounds__(256)
+gc_slices_kernel(const float* __restrict__ y, int ldy, int yoff, const float* __restrict__ mu,
+                 const float* __restrict__ sigma, long long ms_stride, int ld_ms, const float* __restrict__ noise,
+                 float* __restrict__ lik, int Mtot, YT* __restrict__ yhat, int ld_yhat, float* __restrict__ yhat32,
+                 int ld32, int HW, int nslices, int sw, int total) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int per_pix = nslices * sw;
+  const int m = i / per_pix, r = i - m * per_pix;
+  const int j = r / sw, c = r - j * sw;
+  const int ch = yoff + j * sw + c;
+  const int b = m / HW, pix = m - b * HW;
+  const float yv = y[(size_t)m * ldy + ch];
+  const float mv = mu[j * ms_stride + (size_t)m * ld_ms + c];
+  const float sv = sigma[j * ms_stride + (size_t)m * ld_ms + c];
+  const size_t nchw = ((size_t)b * Mtot + ch) * HW + pix;
+  const float q = rintf(yv - mv) + mv;
+  const float xt = noise ? yv + noise[nchw] : q;
+  const float s = fmaxf(sv, 0.11f);
+  const float val = fabsf(xt - mv);
+  const float k = -0.70710678118654752440f;
+  const float up = 0.5f * erfcf(k * ((0.5f - val) / s));
+  const float lo = 0.5f * erfcf(k * ((-0.5f - val) / s));
+  lik[nchw] = fmaxf(up - lo, 1e-9f);
+  yhat[(size_t)m * ld_yhat + ch] = to_out<YT>(q);
+  if (yhat32) yhat32[(size_t)m * ld32 + ch] = q;
+}
+
+extern "C" int tmae_gc_slices_fwd(const float* y, int ldy, int yoff, const float* mu, const float* sigma,
+                                  long long ms_stride, int ld_ms, const float* noise, float* lik, int Mtot,
+                                  void* yhat, int yhat_dtype, int ld_yhat, float* yhat32, int ld32, int n, int HW,
+                                  int nslices, int sw, void* stream) {
+  const int total = n * HW * nslices * sw;
+  if (total <= 0) return TMAE_OK;
+  const dim3 grid(ceil_div(total, 256));
+  if (yhat_dtype == TMAE_BF16)
+    hipLaunchKernelGGL(gc_slices_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, y, ldy, yoff, mu, sigma,
+                       ms_stride, ld_ms, noise, lik, Mtot, (bf16*)yhat, ld_yhat, yhat32, ld32, HW, nslices, sw, total);
+  else
+    hipLaunchKernelGGL(gc_slices_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, y, ldy, yoff, mu, sigma,
+                       ms_stride, ld_ms, noise, lik, Mtot, (float*)yhat, ld_yhat, yhat32, ld32, HW, nslices, sw, total);
+  TMAE_LAUNCH_CHECK("tmae_gc_slices_fwd");
+}

@@ -63,7 +63,7 @@ __device__ __forceinline__ float eb_logits(const float* t, float v) {
 // z, zhat: NHWC [n*HW][C]; lik, noise: NCHW [n][C][HW]
 __global__ void __launch_bounds__(256)
 eb_likelihood_kernel(const float* __restrict__ z, const float* __restrict__ tab, const float* __restrict__ noise,
-                     float* __restrict__ lik, float* __restrict__ zhat, int C, int HW, int total) {
+                     float* __restrict__ lik, void* __restrict__ zhat, int zhat_bf16, int C, int HW, int total) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int c = i % C, m = i / C;
@@ -80,18 +80,22 @@ eb_likelihood_kernel(const float* __restrict__ z, const float* __restrict__ tab,
   const float sgn = sum > 0.0f ? -1.0f : (sum < 0.0f ? 1.0f : -0.0f);
   const float l = fabsf(sigmoid_t(sgn * upper) - sigmoid_t(sgn * lower));
   lik[nchw] = fmaxf(l, 1e-9f);
-  if (zhat) zhat[i] = q;  // quantize_ste forward value: round(z - med) + med  (MCM.py:742-744)
+  // quantize_ste forward value: round(z - med) + med  (MCM.py:742-744)
+  if (zhat) {
+    if (zhat_bf16) ((bf16*)zhat)[i] = (bf16)q;
+    else ((float*)zhat)[i] = q;
+  }
 }
 
 extern "C" int tmae_eb_likelihood_fwd(const float* z, const tmae_eb_params* params, const float* noise, float* lik,
-                                      float* zhat, float* table, int n, int C, int HW, void* stream) {
+                                      void* zhat, int zhat_dtype, float* table, int n, int C, int HW, void* stream) {
   TMAE_REQUIRE(params != nullptr && table != nullptr, "tmae_eb_likelihood_fwd: params/table required");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, st, *params, table, C);
   const int total = n * HW * C;
   if (total > 0)
     hipLaunchKernelGGL(eb_likelihood_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, z, table, noise, lik,
-                       zhat, C, HW, total);
+                       zhat, zhat_dtype == TMAE_BF16, C, HW, total);
   TMAE_LAUNCH_CHECK("tmae_eb_likelihood_fwd");
 }
 

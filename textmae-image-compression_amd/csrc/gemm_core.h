@@ -1,0 +1,445 @@
+// MFMA GEMM core for gfx950 shared by gemm.hip (token GEMMs) and conv.hip (LIC convs).
+//
+//   out[m][n] = epilogue( sum_k X[m][k] * W[n][k] + bias[n] )     for every problem of a batch
+//
+// W is a [N][K] row-major weight in the operand type T (nn.Linear layout; conv weights re-laid out
+// to [Cout][ky][kx][Cin] at weight-prep time).  X rows come from a row source: dense token rows,
+// an implicit-GEMM 3x3 conv gather over NHWC maps, or the patch-embed gather over the image.
+//
+// Two staging variants of the same tile/LDS/MFMA design:
+//   gemm_glds_kernel: global -> LDS with global_load_lds_dwordx4 (no VGPR round trip, 16 B/lane),
+//                     the per-lane SOURCE address carries the LDS swizzle, masked lanes read a zero
+//                     page; 2-stage LDS ring, next tile in flight under the current tile's MFMAs.
+//   gemm_reg_kernel:  global -> VGPR -> LDS, for sources that must be converted on the way (the
+//                     f32 image into bf16 patch-embed operands).
+// LDS rows are 128 B (64 bf16 / 32 f32 of K); 16-B chunk c of row r sits at c ^ ((r >> 1) & 7), which
+// makes the ds_read_b128 fragment reads of 16 consecutive rows conflict-free.  The MFMA is issued
+// swapped (A = weight rows, B = activation rows) so every lane owns 4 consecutive output columns.
+//   bf16: v_mfma_f32_16x16x32_bf16 (f32 accumulate)       f32: v_mfma_f32_16x16x4_f32 (exact f32)
+#pragma once
+
+#include "common.h"
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+// zero page for masked glds lanes (one copy per translation unit; no relocatable device code)
+static __device__ __attribute__((aligned(64))) uint4 g_tmae_zero_page[4] = {};
+
+// One LDS-DMA piece: 64 lanes x 16 B -> LDS [lds_addr, lds_addr + 1 KiB), lane-linear.  Issued from
+// inline asm so hipcc does not count it: with the builtin, hipcc cannot prove that the stage being
+// filled does not alias the stage being read and puts an s_waitcnt vmcnt(0) in front of the next
+// ds_read, serialising every K-step behind its own prefetch.  The caller waits (vmcnt) itself.
+// M0 is saved/restored inside the statement (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_addr)
+               : "memory");
+}
+
+template <typename T> struct Elt;
+template <> struct Elt<bf16> { static constexpr int EPC = 8; };
+template <> struct Elt<float> { static constexpr int EPC = 4; };
+
+// batch decomposition: problem b = b1 * n2 + b2 -> element offset b1 * s1 + b2 * s2
+struct BStride {
+  long long s1, s2;
+  __device__ __forceinline__ long long at(int b1, int b2) const { return (long long)b1 * s1 + (long long)b2 * s2; }
+};
+
+template <typename T> __device__ __forceinline__ uint4 load_chunk_from_f32(const float* p);
+template <> __device__ __forceinline__ uint4 load_chunk_from_f32<float>(const float* p) {
+  return *reinterpret_cast<const uint4*>(p);
+}
+template <> __device__ __forceinline__ uint4 load_chunk_from_f32<bf16>(const float* p) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  const f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+  return pack8_bf16(a, b);
+}
+
+// ------------------------------------------------------------------ row sources
+// Dense rows of T.  source row = (m / G) * Gs + off + (m % G)   (strided views: drop cls rows)
+template <typename T> struct DenseSrc {
+  const T* p;
+  int ld, rows, K, G, Gs, off;
+  BStride bs;
+  struct Row { const T* ptr; };
+  __device__ void batch(int b1, int b2) { p += bs.at(b1, b2); }
+  __device__ Row row(int m) const {
+    if (m >= rows) return {nullptr};
+    const int sm = (m / G) * Gs + off + (m % G);
+    return {p + (size_t)sm * ld};
+  }
+  __device__ const void* addr(const Row& r, int kt, int c) const {
+    const int k = kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC;
+    return (r.ptr && k < K) ? (const void*)(r.ptr + k) : (const void*)g_tmae_zero_page;
+  }
+  __device__ uint4 load(const Row& r, int kt, int c) const { return *reinterpret_cast<const uint4*>(addr(r, kt, c)); }
+};
+
+// Implicit-GEMM 3x3 conv (padding 1, stride s) over NHWC maps of T; input channels [0,c1) from x1,
+// [c1, c1+c2) from x2 (torch.cat without a copy, MCM.py:761,766,780).  K = (ky*3 + kx) * Cin + c.
+template <typename T> struct ConvSrc {
+  const T* x1;
+  const T* x2;
+  int c1, ld1, ld2, Cin, H, W, Ho, Wo, stride, rows, K;
+  float inv_cin;
+  BStride bs1, bs2;
+  struct Row { int pix; int iy0; int ix0; bool ok; };
+  __device__ void batch(int b1, int b2) { x1 += bs1.at(b1, b2); x2 += bs2.at(b1, b2); }
+  __device__ Row row(int m) const {
+    if (m >= rows) return {0, 0, 0, false};
+    const int hw = Ho * Wo;
+    const int b = m / hw, rem = m - b * hw;
+    const int oy = rem / Wo, ox = rem - oy * Wo;
+    return {b * H * W, oy * stride - 1, ox * stride - 1, true};
+  }
+  __device__ const void* addr(const Row& r, int kt, int c) const {
+    const int k = kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC;
+    if (!r.ok || k >= K) return g_tmae_zero_page;
+    int tap = (int)((float)k * inv_cin);
+    if (tap * Cin > k) --tap;
+    if ((tap + 1) * Cin <= k) ++tap;
+    const int ci = k - tap * Cin;
+    const int ky = (tap * 11) >> 5;  // tap / 3 for tap < 9
+    const int iy = r.iy0 + ky, ix = r.ix0 + (tap - 3 * ky);
+    if (iy < 0 || iy >= H || ix < 0 || ix >= W) return g_tmae_zero_page;
+    const int pix = r.pix + iy * W + ix;
+    return (ci < c1) ? (const void*)(x1 + (size_t)pix * ld1 + ci) : (const void*)(x2 + (size_t)pix * ld2 + (ci - c1));
+  }
+  __device__ uint4 load(const Row& r, int kt, int c) const { return *reinterpret_cast<const uint4*>(addr(r, kt, c)); }
+};
+
+// Patch-embed gather over the KEPT patches (timm PatchEmbed conv16/s16 as a GEMM, MCM.py:615):
+// row m = (image b, kept rank k) reads patch ids_shuffle[b][k] of the f32 NCHW image; converts.
+template <typename T> struct PatchSrc {
+  const float* img;
+  const int64_t* ids;
+  int L, keep, C, H, W, P, G, rows, K;
+  struct Row { const float* base; };
+  __device__ void batch(int, int) {}
+  __device__ Row row(int m) const {
+    if (m >= rows) return {nullptr};
+    const int b = m / keep, k = m - b * keep;
+    const int p = (int)ids[(size_t)b * L + k];
+    const int hy = p / G, hx = p - hy * G;
+    return {img + (size_t)b * C * H * W + (size_t)(hy * P) * W + hx * P};
+  }
+  __device__ uint4 load(const Row& r, int kt, int c) const {
+    const int k = kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC;
+    if (!r.base || k >= K) return uint4{0, 0, 0, 0};
+    const int pp = P * P;
+    const int ch = k / pp, rem = k - ch * pp;
+    const int py = rem / P, px = rem - py * P;
+    return load_chunk_from_f32<T>(r.base + (ch * H + py) * W + px);
+  }
+};
+
+// ------------------------------------------------------------------ tile order
+// blockIdx.x -> (n tile, m tile).  xcd_remap gives each XCD a contiguous run of logical tiles (blocks
+// b and b+8 share an XCD); inside that run tiles go in groups of 8 M-tiles x all N-tiles, M fastest,
+// so the ~64 workgroups co-resident on one XCD touch ~8 activation panels and ~8 weight panels —
+// a working set that fits the XCD's 4 MiB L2 instead of streaming the whole weight per M panel.
+__device__ __forceinline__ void tile_order(int ntn, int ntm, int& tn, int& tm) {
+  constexpr int GM = 8;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int group = GM * ntn;
+  const int first_m = (t / group) * GM;
+  const int gm = min(ntm - first_m, GM);
+  const int r = t - (t / group) * group;
+  tm = first_m + r % gm;
+  tn = r / gm;
+}
+
+// ------------------------------------------------------------------ shared compute step
+template <typename T, int BN, int WN, int WM, int TN, int TM>
+__device__ __forceinline__ void mfma_tile(const uint4* base, int wn, int wm, int lane, f32x4 (&acc)[TN][TM]) {
+  const int fr = lane & 15, fq = lane >> 4;
+  if constexpr (sizeof(T) == 2) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 a[TN], b[TM];
+      const int c = 4 * s + fq;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int r = wn * WN + 16 * i + fr;
+        uint4 u = base[r * 8 + (c ^ ((r >> 1) & 7))];
+        a[i] = *reinterpret_cast<bf16x8*>(&u);
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int r = wm * WM + 16 * j + fr;
+        uint4 u = base[(BN + r) * 8 + (c ^ ((r >> 1) & 7))];
+        b[j] = *reinterpret_cast<bf16x8*>(&u);
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  } else {
+    const float* fb = reinterpret_cast<const float*>(base);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float a[TN], b[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int r = wn * WN + 16 * i + fr;
+        a[i] = fb[(r * 8 + (q ^ ((r >> 1) & 7))) * 4 + fq];
+      }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int r = wm * WM + 16 * j + fr;
+        b[j] = fb[((BN + r) * 8 + (q ^ ((r >> 1) & 7))) * 4 + fq];
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+}
+
+template <int TN, int TM, int WN, int WM, class EPI>
+__device__ __forceinline__ void epilogue(const EPI& epi, const f32x4 (&acc)[TN][TM], int n0, int m0, int wn, int wm,
+                                         int lane, int M, int N) {
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = n0 + wn * WN + 16 * i + 4 * fq;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = m0 + wm * WM + 16 * j + fr;
+      if (m < M && n < N) epi(m, n, acc[i][j]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ glds kernel
+template <typename T, int BN, int BM, int WGN, class WS, class XS, class EPI>
+__global__ void __launch_bounds__(256, 2)
+gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
+  constexpr int BKE = 8 * Elt<T>::EPC;
+  constexpr int WGM = 4 / WGN;
+  constexpr int WN = BN / WGN, WM = BM / WGM;
+  constexpr int TN = WN / 16, TM = WM / 16;
+  constexpr int WJ = BN / 32, XJ = BM / 32;  // glds instructions per wave per stage
+  constexpr int ROWS = BN + BM;
+  static_assert(TN >= 1 && TM >= 1 && WJ >= 1 && XJ >= 1, "bad tile");
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * ROWS * 8];
+
+  const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
+  ws.batch(b1, b2);
+  xs.batch(b1, b2);
+  epi.batch(b1, b2);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave % WGN, wm = wave / WGN;
+  int tn, tm;
+  tile_order((N + BN - 1) / BN, (M + BM - 1) / BM, tn, tm);
+  const int n0 = tn * BN, m0 = tm * BM;
+
+  // this lane's rows / logical chunks for every glds it issues (constant over K)
+  const int lr = 8 * wave + (lane >> 3);
+  const int pch = lane & 7;
+  typename WS::Row wrow[WJ];
+  typename XS::Row xrow[XJ];
+  int wc[WJ], xc[XJ];
+#pragma unroll
+  for (int j = 0; j < WJ; ++j) {
+    const int r = 32 * j + lr;
+    wrow[j] = ws.row(n0 + r);
+    wc[j] = pch ^ ((r >> 1) & 7);
+  }
+#pragma unroll
+  for (int j = 0; j < XJ; ++j) {
+    const int r = 32 * j + lr;
+    xrow[j] = xs.row(m0 + r);
+    xc[j] = pch ^ ((r >> 1) & 7);
+  }
+  const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
+  auto issue = [&](int stage, int kt) {
+    const unsigned sb = lds_base + (unsigned)stage * ROWS * 128u;
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) glds16(ws.addr(wrow[j], kt, wc[j]), sb + (32u * j + 8u * wave_u) * 128u);
+#pragma unroll
+    for (int j = 0; j < XJ; ++j) glds16(xs.addr(xrow[j], kt, xc[j]), sb + (BN + 32u * j + 8u * wave_u) * 128u);
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K + BKE - 1) / BKE;
+  if (nk > 0) issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) issue((kt + 1) & 1, kt + 1);
+    mfma_tile<T, BN, WN, WM, TN, TM>(lds + (kt & 1) * ROWS * 8, wn, wm, lane, acc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  epilogue<TN, TM, WN, WM>(epi, acc, n0, m0, wn, wm, lane, M, N);
+}
+
+// ------------------------------------------------------------------ register-staged kernel
+template <typename T, int BN, int BM, int WGN, class WS, class XS, class EPI>
+__global__ void __launch_bounds__(256, 2)
+gemm_reg_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
+  constexpr int BKE = 8 * Elt<T>::EPC;
+  constexpr int WGM = 4 / WGN;
+  constexpr int WN = BN / WGN, WM = BM / WGM;
+  constexpr int TN = WN / 16, TM = WM / 16;
+  constexpr int WCH = BN / 32, XCH = BM / 32;
+  constexpr int ROWS = BN + BM;
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * ROWS * 8];
+
+  const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
+  ws.batch(b1, b2);
+  xs.batch(b1, b2);
+  epi.batch(b1, b2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave % WGN, wm = wave / WGN;
+  int tn, tm;
+  tile_order((N + BN - 1) / BN, (M + BM - 1) / BM, tn, tm);
+  const int n0 = tn * BN, m0 = tm * BM;
+  const int ch = tid & 7, r0 = tid >> 3;
+
+  typename WS::Row wrow[WCH];
+  typename XS::Row xrow[XCH];
+#pragma unroll
+  for (int p = 0; p < WCH; ++p) wrow[p] = ws.row(n0 + r0 + 32 * p);
+#pragma unroll
+  for (int p = 0; p < XCH; ++p) xrow[p] = xs.row(m0 + r0 + 32 * p);
+  uint4 wreg[WCH], xreg[XCH];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int p = 0; p < WCH; ++p) wreg[p] = ws.load(wrow[p], kt, ch);
+#pragma unroll
+    for (int p = 0; p < XCH; ++p) xreg[p] = xs.load(xrow[p], kt, ch);
+  };
+  auto swrite = [&](int buf) {
+    uint4* base = lds + buf * ROWS * 8;
+#pragma unroll
+    for (int p = 0; p < WCH; ++p) {
+      const int r = r0 + 32 * p;
+      base[r * 8 + (ch ^ ((r >> 1) & 7))] = wreg[p];
+    }
+#pragma unroll
+    for (int p = 0; p < XCH; ++p) {
+      const int r = r0 + 32 * p;
+      base[(BN + r) * 8 + (ch ^ ((r >> 1) & 7))] = xreg[p];
+    }
+  };
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (K + BKE - 1) / BKE;
+  if (nk > 0) {
+    gload(0);
+    swrite(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload(kt + 1);
+    mfma_tile<T, BN, WN, WM, TN, TM>(lds + (kt & 1) * ROWS * 8, wn, wm, lane, acc);
+    if (kt + 1 < nk) swrite((kt + 1) & 1);
+    __syncthreads();
+  }
+  epilogue<TN, TM, WN, WM>(epi, acc, n0, m0, wn, wm, lane, M, N);
+}
+
+// ------------------------------------------------------------------ launch with tile selection
+struct TileChoice { int bn, bm; };
+
+// pick the tile that maximises (useful fraction of padded MFMA work) x (fill of 2 WGs/CU) x (tile
+// efficiency of larger tiles); ties go to the larger tile
+static inline TileChoice choose_tile(int M, int N, int batch) {
+  const int cand[5][2] = {{128, 128}, {64, 128}, {32, 128}, {64, 64}, {32, 64}};
+  const double eff[5] = {1.0, 0.86, 0.70, 0.72, 0.55};
+  double best = -1.0;
+  TileChoice tc{128, 128};
+  for (int i = 0; i < 5; ++i) {
+    const int bn = cand[i][0], bm = cand[i][1];
+    const double tn = ceil_div(N, bn), tm = ceil_div(M, bm);
+    const double useful = ((double)N / (tn * bn)) * ((double)M / (tm * bm));
+    const double wgs = tn * tm * batch;
+    const double fill = wgs >= 512.0 ? 1.0 : wgs / 512.0;
+    const double score = useful * fill * eff[i];
+    if (score > best + 1e-9) { best = score; tc = TileChoice{bn, bm}; }
+  }
+  return tc;
+}
+
+template <bool GLDS, typename T, int BN, int BM, int WGN, class WS, class XS, class EPI>
+static int launch_one(const char* name, const WS& ws, const XS& xs, const EPI& epi, int M, int N, int K, int n1,
+                      int n2, hipStream_t st) {
+  const int grid = ceil_div(N, BN) * ceil_div(M, BM);
+  if (grid == 0 || n1 * n2 == 0) return TMAE_OK;
+  if constexpr (GLDS)
+    hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, WS, XS, EPI>), dim3(grid, n1 * n2), dim3(256), 0, st, ws, xs,
+                       epi, M, N, K, n2);
+  else
+    hipLaunchKernelGGL((gemm_reg_kernel<T, BN, BM, WGN, WS, XS, EPI>), dim3(grid, n1 * n2), dim3(256), 0, st, ws, xs,
+                       epi, M, N, K, n2);
+  TMAE_LAUNCH_CHECK(name);
+}
+
+template <bool GLDS, typename T, class XS, class EPI>
+static int launch_gemm(const char* name, const T* w, long long ws1, long long ws2, int N, int K, const XS& xs,
+                       const EPI& epi, int M, int n1 = 1, int n2 = 1, hipStream_t st = 0) {
+  DenseSrc<T> ws{w, K, N, K, 1 << 30, 0, 0, BStride{ws1, ws2}};
+  const TileChoice tc = choose_tile(M, N, n1 * n2);
+  if (tc.bn == 128) return launch_one<GLDS, T, 128, 128, 2>(name, ws, xs, epi, M, N, K, n1, n2, st);
+  if (tc.bn == 64 && tc.bm == 128) return launch_one<GLDS, T, 64, 128, 1>(name, ws, xs, epi, M, N, K, n1, n2, st);
+  if (tc.bn == 32 && tc.bm == 128) return launch_one<GLDS, T, 32, 128, 1>(name, ws, xs, epi, M, N, K, n1, n2, st);
+  if (tc.bn == 64) return launch_one<GLDS, T, 64, 64, 2>(name, ws, xs, epi, M, N, K, n1, n2, st);
+  return launch_one<GLDS, T, 32, 64, 1>(name, ws, xs, epi, M, N, K, n1, n2, st);
+}
+
+// ------------------------------------------------------------------ shared epilogues
+// out[m][n..n+3] = act(acc + bias (+ addend[m][n])) in OT; optional second f32 copy (out32).
+template <typename OT, int ACT> struct EpiStore {
+  OT* out;
+  int ldo;
+  const float* bias;
+  const float* addend;  // optional pre-activation addend (precomputed partial sums)
+  int ld_add;
+  float* out32;         // optional f32 copy
+  int ld32;
+  BStride so, sb, sa, s32;
+  __device__ void batch(int b1, int b2) {
+    out += so.at(b1, b2);
+    if (bias) bias += sb.at(b1, b2);
+    if (addend) addend += sa.at(b1, b2);
+    if (out32) out32 += s32.at(b1, b2);
+  }
+  __device__ void operator()(int m, int n, f32x4 v) const {
+    if (bias) v += load4f(bias + n);
+    if (addend) v += load4f(addend + (size_t)m * ld_add + n);
+    if (ACT == TMAE_ACT_GELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = gelu_erf(v[j]);
+    }
+    store4(out + (size_t)m * ldo + n, v);
+    if (out32) store4(out32 + (size_t)m * ld32 + n, v);
+  }
+};
+
+template <typename OT, int ACT>
+static inline EpiStore<OT, ACT> make_store(OT* out, int ldo, const float* bias) {
+  EpiStore<OT, ACT> e;
+  e.out = out; e.ldo = ldo; e.bias = bias; e.addend = nullptr; e.ld_add = 0; e.out32 = nullptr; e.ld32 = 0;
+  e.so = e.sb = e.sa = e.s32 = BStride{0, 0};
+  return e;
+}

@@ -231,7 +231,19 @@ def _interleave(layers):
 # ====================================================================================== executor
 class _Executor:
     """Prepared weights + persistent workspaces for one (batch, dtype, device); `run` enqueues the
-    whole forward (about 270 launches at the default config) on the current stream."""
+    whole forward on the current stream (graph-capturable: no host sync, no allocation-dependent
+    control flow).
+
+    LIC slice loop restructure (exact up to f32 summation order):
+      * the first conv of every cc_transform_mean/scale and lrp_transform stack sees
+        cat(latent_{means,scales}, y_hat slices): its latent-channel part is the same input for all 12
+        slices, so it is computed for all slices up front as two big convs (N = 3 * 12 * 224) into the
+        partial-sum buffer P; each slice's first conv then only contracts the y_hat channels and adds
+        its P block in the epilogue;
+      * the mean and scale stacks of a slice run as one batched launch per layer;
+      * slices 6..11 all condition on y_hat slices 0..5 (max_support_slices = 6, MCM.py:73, 756-758),
+        so their mean/scale stacks, Gaussian likelihoods and lrp stacks run batched (12 / 6 problems).
+    """
 
     def __init__(self, m: MCM, batch, dtype, device):
         self.m, self.batch, self.dtype, self.device = m, batch, dtype, device
@@ -250,6 +262,7 @@ class _Executor:
             raise ValueError(f"sqrt(num_keep_patches)={g} must be a multiple of 4 so h_s returns to the y grid")
         self.sw = M // S
         self.maxsup = S // 2
+        self.nb = S - self.maxsup  # slices sharing the full support (batched)
         f32, dt = torch.float32, dtype
         dev = device
 
@@ -257,6 +270,8 @@ class _Executor:
             return torch.empty(shape, dtype=dtype, device=dev)
 
         Te, Td = K + 1, self.L + 1
+        Mp = B * g * g
+        self.Mp = Mp
         hid_e = m.encoder_blocks[0].mlp.fc1.out_features if m.encoder_depth else 4 * E
         hid_d = m.decoder_blocks[0].mlp.fc1.out_features if m.decoder_depth else 4 * Dd
         self.tok = z(B * Te, E)
@@ -264,26 +279,33 @@ class _Executor:
         self.enc_out = z(B * K, E, dtype=dt)
         ga = [l.out_channels for l in m.g_a if isinstance(l, nn.Conv2d)]
         self.ga_buf = [z(B * K, c, dtype=dt) for c in ga[:-1]]
-        self.Y = z(B * K, M)
+        self.Y32 = z(Mp, M)
+        self.YT = self.Y32 if dt == f32 else z(Mp, M, dtype=dt)
         ha = [l.out_channels for l in m.h_a if isinstance(l, nn.Conv2d)]
         res = [g, g, (g + 1) // 2, (g + 1) // 2, self.hz]
-        self.ha_buf = [z(B * r * r, c) for c, r in zip(ha[:-1], res[:-1])]
+        self.ha_buf = [z(B * r * r, c, dtype=dt) for c, r in zip(ha[:-1], res[:-1])]
         self.Z = z(B * self.hz * self.hz, N)
         self.ZLIK = z(B, N, self.hz, self.hz)
-        self.ZHAT = z(B * self.hz * self.hz, N)
+        self.ZHAT = z(B * self.hz * self.hz, N, dtype=dt)
         self.eb_table = z(N, 59)
         hs_out = [m.h_s_mean[0].out_channels, m.h_s_mean[2][0].out_channels // 4, m.h_s_mean[4].out_channels,
                   m.h_s_mean[6][0].out_channels // 4]
         hs_res = [self.hz, 2 * self.hz, 2 * self.hz, g]
-        self.hs_buf = [z(B * r * r, c) for c, r in zip(hs_out, hs_res)]
-        self.SUPW = M + self.sw * (self.maxsup + 1)
-        self.SUP = z(B * g * g, self.SUPW)  # [latent_means | y_hat slots 0..maxsup-1 | current slice]
-        self.LS = z(B * g * g, M)
-        mid = [l.out_channels for l in m.cc_transform_mean[0] if isinstance(l, nn.Conv2d)]
-        self.cc_buf = [z(B * g * g, c) for c in mid[:-1]]
-        self.MU = z(B * g * g, self.sw)
+        self.hs_buf = [z(B * r * r, c, dtype=dt) for c, r in zip(hs_out, hs_res)]
+        self.LS = z(Mp, M, dtype=dt)
+        self.LM = z(Mp, M, dtype=dt)
+        self.mid = [l.out_channels for l in m.cc_transform_mean[0] if isinstance(l, nn.Conv2d)]
+        c0 = self.mid[0]
+        self.PW = 3 * S * c0  # partial sums: [mean (S*c0) | lrp (S*c0) | scale (S*c0)]
+        self.Pbuf = z(Mp, self.PW)
+        self.SUPY = z(Mp, M, dtype=dt)    # y_hat slices (post-LRP for i < maxsup; pre-LRP for the batched ones)
+        self.YPRE = z(Mp, M)              # f32 pre-LRP y_hat = round(y - mu) + mu
+        self.YH = z(Mp, M, dtype=dt)      # final y_hat (g_s input)
+        nb = self.nb
+        self.CM = [z(2, nb, Mp, c, dtype=dt) for c in self.mid[:-1]]
+        self.MUSIG = z(2, nb, Mp, self.sw)
+        self.CL = [z(nb, Mp, c, dtype=dt) for c in self.mid[:-1]]
         self.YLIK = z(B, M, g, g)
-        self.YH = z(B * g * g, M)
         gs = [l.out_channels for l in m.g_s if isinstance(l, nn.ConvTranspose2d)]
         self.gs_buf = [z(B * K, c, dtype=dt) for c in gs]
         self.dec = z(B * Td, Dd)
@@ -297,11 +319,17 @@ class _Executor:
             return
         self._sig = sig
         m, dt = self.m, self.dtype
-        cast = (lambda t: t.detach().contiguous()) if dt == torch.float32 else (
-            lambda t: t.detach().to(dt).contiguous())
+        M, S, sw, ms = m.latent_depth, m.num_slices, self.sw, self.maxsup
 
-        def conv_w(conv):  # [Cout][Cin][3][3] -> [Cout][3][3][Cin]
-            return cast(conv.weight.detach().permute(0, 2, 3, 1))
+        def cast(t):
+            t = t.detach()
+            return (t if dt == torch.float32 else t.to(dt)).contiguous()
+
+        def cw(w, lo=None, hi=None):  # conv weight [Cout][Cin][3][3] -> [Cout][3][3][Cin slice]
+            w = w.detach()
+            if lo is not None:
+                w = w[:, lo:hi]
+            return w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
 
         self.w_pe = cast(m.encoder_embed.proj.weight.view(m.encoder_embed.proj.weight.shape[0], -1))
         self.enc_w = [BlockWeights.from_block(b, dt) for b in m.encoder_blocks]
@@ -310,25 +338,53 @@ class _Executor:
                      for l in m.g_a if isinstance(l, nn.Conv2d)]
         self.gs_w = [(cast(l.weight.view(l.weight.shape[0], -1).t()), l.bias.detach())
                      for l in m.g_s if isinstance(l, nn.ConvTranspose2d)]
-        self.ha_w = [(conv_w(l), l.bias.detach(), l.stride[0]) for l in m.h_a if isinstance(l, nn.Conv2d)]
+        self.ha_w = [(cast(cw(l.weight)), l.bias.detach(), l.stride[0]) for l in m.h_a if isinstance(l, nn.Conv2d)]
 
         def hs_w(seq):
             out = []
             for l in seq:
                 if isinstance(l, nn.Conv2d):
-                    out.append((conv_w(l), l.bias.detach(), False))
+                    out.append((cast(cw(l.weight)), l.bias.detach(), False))
                 elif isinstance(l, nn.Sequential):
-                    out.append((conv_w(l[0]), l[0].bias.detach(), True))
+                    out.append((cast(cw(l[0].weight)), l[0].bias.detach(), True))
             return out
 
         self.hsm_w, self.hss_w = hs_w(m.h_s_mean), hs_w(m.h_s_scale)
 
-        def stack_w(seq):
-            return [(conv_w(l), l.bias.detach()) for l in seq if isinstance(l, nn.Conv2d)]
+        def convs(seq):
+            return [l for l in seq if isinstance(l, nn.Conv2d)]
 
-        self.ccm_w = [stack_w(s) for s in m.cc_transform_mean]
-        self.ccs_w = [stack_w(s) for s in m.cc_transform_scale]
-        self.lrp_w = [stack_w(s) for s in m.lrp_transform]
+        mean = [convs(s) for s in m.cc_transform_mean]
+        scale = [convs(s) for s in m.cc_transform_scale]
+        lrp = [convs(s) for s in m.lrp_transform]
+        # latent-channel parts of every first conv: [mean | lrp] from latent_means, scale from latent_scales
+        self.w_pre_ml = cast(torch.cat([cw(mean[i][0].weight, 0, M) for i in range(S)]
+                                       + [cw(lrp[i][0].weight, 0, M) for i in range(S)]))
+        self.w_pre_s = cast(torch.cat([cw(scale[i][0].weight, 0, M) for i in range(S)]))
+        # per-slice y_hat-channel parts + the remaining layers, packed for batched launches
+        self.ms_first, self.ms_layers, self.lrp_first, self.lrp_layers = [], [], [], []
+        for i in range(ms):
+            ny = sw * i
+            self.ms_first.append((cast(torch.stack([cw(mean[i][0].weight, M, M + ny), cw(scale[i][0].weight, M, M + ny)])),
+                                  torch.stack([mean[i][0].bias, scale[i][0].bias]).detach().contiguous()))
+            self.ms_layers.append([(cast(torch.stack([cw(mean[i][j].weight), cw(scale[i][j].weight)])),
+                                    torch.stack([mean[i][j].bias, scale[i][j].bias]).detach().contiguous())
+                                   for j in range(1, 5)])
+            self.lrp_first.append((cast(cw(lrp[i][0].weight, M, M + ny + sw)), lrp[i][0].bias.detach()))
+            self.lrp_layers.append([(cast(cw(lrp[i][j].weight)), lrp[i][j].bias.detach()) for j in range(1, 5)])
+        bs = range(ms, S)
+        ny = sw * ms
+        self.b_ms_first = (cast(torch.stack([torch.stack([cw(t[i][0].weight, M, M + ny) for i in bs])
+                                             for t in (mean, scale)])),
+                           torch.stack([torch.stack([t[i][0].bias for i in bs]) for t in (mean, scale)]).detach()
+                           .contiguous())
+        self.b_ms_layers = [(cast(torch.stack([torch.stack([cw(t[i][j].weight) for i in bs]) for t in (mean, scale)])),
+                             torch.stack([torch.stack([t[i][j].bias for i in bs]) for t in (mean, scale)]).detach()
+                             .contiguous()) for j in range(1, 5)]
+        self.b_lrp_first = (cast(torch.stack([cw(lrp[i][0].weight, M, M + ny + sw) for i in bs])),
+                            torch.stack([lrp[i][0].bias for i in bs]).detach().contiguous())
+        self.b_lrp_layers = [(cast(torch.stack([cw(lrp[i][j].weight) for i in bs])),
+                              torch.stack([lrp[i][j].bias for i in bs]).detach().contiguous()) for j in range(1, 5)]
         self.w_de = cast(m.decoder_embed.weight)
         self.w_dp = cast(m.decoder_pred.weight)
 
@@ -336,7 +392,7 @@ class _Executor:
     def run(self, imgs, scores, training, noise):
         m, dt, B = self.m, self.dtype, self.batch
         E, Dd, M, N, S = m.encoder_embed_dim, m.decoder_embed_dim, m.latent_depth, m.hyperprior_depth, m.num_slices
-        K, L, P, g, hz, sw = m.num_keep_patches, self.L, self.P, self.g, self.hz, self.sw
+        K, L, P, g, hz = m.num_keep_patches, self.L, self.P, self.g, self.hz
         Te, Td = K + 1, L + 1
         imgs = imgs.float().contiguous()
         if imgs.shape[1:] != (m.encoder_embed.proj.in_channels, self.img, self.img):
@@ -364,13 +420,15 @@ class _Executor:
         x = self.enc_out
         for j, (w, b) in enumerate(self.ga_w):
             last = j == len(self.ga_w) - 1
-            out = self.Y if last else self.ga_buf[j]
-            ops.linear(x, w, b, dt, act=ops.ACT_NONE if last else ops.ACT_GELU, out=out)
-            x = out
+            if last:
+                ops.linear(x, w, b, dt, out=self.YT, out32=None if self.YT is self.Y32 else self.Y32)
+            else:
+                ops.linear(x, w, b, dt, act=ops.ACT_GELU, out=self.ga_buf[j])
+                x = self.ga_buf[j]
 
         # ---- h_a (MCM.py:739)
         H = g
-        x, cin = self.Y, M
+        x, cin = self.YT, M
         for j, (w, b, stride) in enumerate(self.ha_w):
             last = j == len(self.ha_w) - 1
             out = self.Z if last else self.ha_buf[j]
@@ -384,33 +442,12 @@ class _Executor:
         ops.eb_likelihood(m.entropy_bottleneck, self.Z, B, N, hz * hz, noise=z_noise, lik=self.ZLIK, zhat=self.ZHAT,
                           table=self.eb_table)
 
-        # ---- h_s_scale -> LS, h_s_mean -> SUP[:, :M]  (MCM.py:747-748)
-        self._h_s(self.hss_w, self.LS, M)
-        self._h_s(self.hsm_w, self.SUP, self.SUPW)
+        # ---- h_s (MCM.py:747-748)
+        self._h_s(self.hss_w, self.LS)
+        self._h_s(self.hsm_w, self.LM)
 
         # ---- slice loop (MCM.py:751-787)
-        SUP, W4 = self.SUP, self.SUP.element_size()
-        sup_base = SUP.data_ptr()
-        for i in range(S):
-            nsup = min(i, self.maxsup)
-            cur = M + nsup * sw  # channel offset of this slice's y_hat in SUP
-            # mu = cc_transform_mean[i](cat(latent_means, y_hat[:nsup]))
-            self._stack(self.ccm_w[i], SUP, cur, self.SUPW, None, 0, 0)
-            mu_w, mu_b = self.ccm_w[i][-1]
-            ops.conv3x3(self.cc_buf[-1], self.cc_buf[-1].shape[1], self.cc_buf[-1].shape[1], B, g, g, mu_w, mu_b,
-                        self.MU, sw, sw, dt)
-            # sigma = cc_transform_scale[i](cat(latent_scales, y_hat[:nsup])) fused with the GC likelihood
-            self._stack(self.ccs_w[i], self.LS, M, M, sup_base + M * W4, nsup * sw, self.SUPW)
-            sg_w, sg_b = self.ccs_w[i][-1]
-            c4 = self.cc_buf[-1].shape[1]
-            ops.conv3x3_gaussian(self.cc_buf[-1], c4, c4, B, g, g, sg_w, sg_b, sw, self.Y, M, i * sw, self.MU, sw,
-                                 y_noise, self.YLIK, M, sup_base + cur * W4, self.SUPW, dt)
-            # lrp = lrp_transform[i](cat(mean_support, y_hat_slice)); y_hat += 0.5 tanh(lrp)
-            self._stack(self.lrp_w[i], SUP, cur + sw, self.SUPW, None, 0, 0)
-            lw, lb = self.lrp_w[i][-1]
-            dst2 = sup_base + cur * W4 if i < self.maxsup else None
-            ops.conv3x3_lrp(self.cc_buf[-1], c4, c4, B, g, g, lw, lb, sw, sup_base + cur * W4, self.SUPW,
-                            self.YH.data_ptr() + i * sw * W4, M, dst2, self.SUPW, dt)
+        self._slices(y_noise)
 
         # ---- g_s (MCM.py:790-792): transposed 1x1 convs back to E-dim tokens
         x = self.YH
@@ -432,19 +469,15 @@ class _Executor:
         return {"x_hat": x_hat, "y": self.YLIK.clone(), "z": self.ZLIK.clone(), "ids_restore": rest,
                 "ids_shuffle": shuf}
 
-    def _h_s(self, layers, out_final, ld_final):
+    def _h_s(self, layers, out_final):
         B, dt = self.batch, self.dtype
         x, cin, H = self.ZHAT, self.m.hyperprior_depth, self.hz
         for j, (w, b, pshuf) in enumerate(layers):
             last = j == len(layers) - 1
             cout = w.shape[0]
-            if last:
-                out, ldo = out_final, ld_final
-            else:
-                out = self.hs_buf[j]
-                ldo = out.shape[1]
-            ops.conv3x3(x, cin, cin, B, H, H, w, b, out, ldo, cout, dt, act=ops.ACT_NONE if last else ops.ACT_GELU,
-                        pixel_shuffle=pshuf)
+            out = out_final if last else self.hs_buf[j]
+            ops.conv3x3(x, cin, cin, B, H, H, w, b, out, out.shape[1], cout, self.dtype,
+                        act=ops.ACT_NONE if last else ops.ACT_GELU, pixel_shuffle=pshuf)
             if pshuf:
                 H *= 2
                 cin = cout // 4
@@ -452,15 +485,81 @@ class _Executor:
                 cin = cout
             x = out
 
-    def _stack(self, layers, x1, c1, ld1, x2, c2, ld2):
-        """first four convs (+GELU) of a 5-conv slice transform into cc_buf[0..3]."""
-        B, g, dt = self.batch, self.g, self.dtype
-        for j in range(4):
-            w, b = layers[j]
-            cout = w.shape[0]
-            out = self.cc_buf[j]
-            if j == 0:
-                ops.conv3x3(x1, c1, ld1, B, g, g, w, b, out, cout, cout, dt, act=ops.ACT_GELU, x2=x2, c2=c2, ld2=ld2)
-            else:
-                cin = self.cc_buf[j - 1].shape[1]
-                ops.conv3x3(self.cc_buf[j - 1], cin, cin, B, g, g, w, b, out, cout, cout, dt, act=ops.ACT_GELU)
+    def _slices(self, y_noise):
+        m, dt, B, g = self.m, self.dtype, self.batch, self.g
+        M, S, sw, ms, nb, Mp = m.latent_depth, m.num_slices, self.sw, self.maxsup, self.nb, self.Mp
+        mid = self.mid
+        c0 = mid[0]
+        Pw = self.PW
+        Pb = self.Pbuf
+        eP = Pb.element_size()
+        pbase = Pb.data_ptr()
+        off_mean, off_lrp, off_scale = 0, S * c0, 2 * S * c0
+        esz = self.SUPY.element_size()
+        supy, ypre, yh = self.SUPY.data_ptr(), self.YPRE.data_ptr(), self.YH.data_ptr()
+        e4 = 4
+        # latent-channel partial sums of all first convs
+        ops.conv3x3(self.LM, M, M, B, g, g, self.w_pre_ml, None, pbase + off_mean * eP, Pw, 2 * S * c0, dt,
+                    y_f32=True)
+        ops.conv3x3(self.LS, M, M, B, g, g, self.w_pre_s, None, pbase + off_scale * eP, Pw, S * c0, dt, y_f32=True)
+
+        cm = [t.data_ptr() for t in self.CM]
+        cl = [t.data_ptr() for t in self.CL]
+        musig = self.MUSIG.data_ptr()
+        cm_s1 = [nb * Mp * c for c in mid[:-1]]
+        ms_s1 = nb * Mp * sw
+
+        def ms_stack(first, layers, x1, c1, i0, nbs):
+            """mean+scale stacks for slices i0.. (nbs problems per type) -> MUSIG"""
+            w, b = first
+            ops.conv3x3(x1, c1, M, B, g, g, w, b, cm[0], c0, c0, dt, act=ops.ACT_GELU,
+                        addend=pbase + (off_mean + i0 * c0) * eP, ld_add=Pw, nb=(2, nbs),
+                        strides={"w": (w[0].numel(), w[0][0].numel() if nbs > 1 else 0),
+                                 "b": (b[0].numel(), c0 if nbs > 1 else 0),
+                                 "a": (off_scale - off_mean, c0), "y": (cm_s1[0], Mp * c0)})
+            for j, (w, b) in enumerate(layers):
+                cin, cout = mid[j], mid[j + 1]
+                last = j == len(layers) - 1
+                y = musig if last else cm[j + 1]
+                ys1 = ms_s1 if last else cm_s1[j + 1]
+                ops.conv3x3(cm[j], cin, cin, B, g, g, w, b, y, cout, cout, dt,
+                            act=ops.ACT_NONE if last else ops.ACT_GELU, y_f32=last, nb=(2, nbs),
+                            strides={"x1": (cm_s1[j], Mp * cin), "w": (w[0].numel(), w[0][0].numel() if nbs > 1 else 0),
+                                     "b": (b[0].numel(), cout if nbs > 1 else 0), "y": (ys1, Mp * cout)})
+
+        def lrp_stack(first, layers, i0, nbs, x2=None):
+            w, b = first
+            if x2 is None:  # single slice i0: input = y_hat slots 0..i0 (contiguous)
+                ops.conv3x3(supy, sw * (i0 + 1), M, B, g, g, w, b, cl[0], c0, c0, dt, act=ops.ACT_GELU,
+                            addend=pbase + (off_lrp + i0 * c0) * eP, ld_add=Pw)
+            else:           # batched slices: shared slots 0..ms-1 + own pre-LRP slot
+                ops.conv3x3(supy, sw * ms, M, B, g, g, w, b, cl[0], c0, c0, dt, act=ops.ACT_GELU,
+                            x2=x2, c2=sw, ld2=M, addend=pbase + (off_lrp + i0 * c0) * eP, ld_add=Pw, nb=(1, nbs),
+                            strides={"x2": (0, sw), "w": (0, w[0].numel()), "b": (0, c0), "a": (0, c0),
+                                     "y": (0, Mp * c0)})
+            for j, (w, b) in enumerate(layers):
+                cin, cout = mid[j], mid[j + 1]
+                if j < len(layers) - 1:
+                    ops.conv3x3(cl[j], cin, cin, B, g, g, w, b, cl[j + 1], cout, cout, dt, act=ops.ACT_GELU,
+                                nb=(1, nbs), strides={"x1": (0, Mp * cin), "w": (0, w[0].numel() if nbs > 1 else 0),
+                                                      "b": (0, cout if nbs > 1 else 0), "y": (0, Mp * cout)})
+                else:  # y_hat = y_hat_pre + 0.5 tanh(lrp) -> YH (and the support slot for i < ms)
+                    ops.conv3x3(cl[j], cin, cin, B, g, g, w, b, yh + i0 * sw * esz, M, cout, dt,
+                                y_f32=(dt == torch.float32), lrp_src=ypre + i0 * sw * e4, ld_src=M,
+                                y2=(supy + i0 * sw * esz) if nbs == 1 else None, ldy2=M, nb=(1, nbs),
+                                strides={"x1": (0, Mp * cin), "w": (0, w[0].numel() if nbs > 1 else 0),
+                                         "b": (0, cout if nbs > 1 else 0), "src": (0, sw), "y": (0, sw),
+                                         "y2": (0, sw)})
+
+        # slices 0..ms-1: serial (slice i conditions on y_hat 0..i-1)
+        for i in range(ms):
+            ms_stack(self.ms_first[i], self.ms_layers[i], supy, sw * i, i, 1)
+            ops.gc_slices(self.Y32, M, i * sw, musig, musig + ms_s1 * e4, Mp * sw, sw, y_noise, self.YLIK, M, supy,
+                          dt, M, ypre, M, B, g * g, 1, sw)
+            lrp_stack(self.lrp_first[i], self.lrp_layers[i], i, 1)
+        # slices ms..S-1: batched on the fixed support y_hat 0..ms-1
+        if nb > 0:
+            ms_stack(self.b_ms_first, self.b_ms_layers, supy, sw * ms, ms, nb)
+            ops.gc_slices(self.Y32, M, ms * sw, musig, musig + ms_s1 * e4, Mp * sw, sw, y_noise, self.YLIK, M, supy,
+                          dt, M, ypre, M, B, g * g, nb, sw)
+            lrp_stack(self.b_lrp_first, self.b_lrp_layers, ms, nb, x2=supy + ms * sw * esz)

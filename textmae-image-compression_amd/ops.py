@@ -6,14 +6,16 @@ the library never allocates) unless an `out=` buffer is passed.
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 from . import _lib
-from ._lib import ACT_GELU, ACT_NONE, TMAE_BF16, TMAE_F32, EBParams
+from ._lib import ACT_GELU, ACT_NONE, TMAE_BF16, TMAE_F32, ConvArgs, EBParams
 
 __all__ = [
     "ids_shuffle", "layernorm", "linear", "linear_residual", "patch_embed", "cls_rows", "mha", "decoder_embed",
-    "mask_rows", "decoder_pred", "conv3x3", "conv3x3_gaussian", "conv3x3_lrp", "eb_likelihood", "eb_aux_loss",
+    "mask_rows", "decoder_pred", "conv3x3", "gc_slices", "eb_likelihood", "eb_aux_loss",
     "gc_likelihood", "nhwc_to_nchw", "dtype_code", "TMAE_F32", "TMAE_BF16", "ACT_NONE", "ACT_GELU",
 ]
 
@@ -72,7 +74,7 @@ def layernorm(x, weight, bias, eps, out_dtype, rows=None, row_group=None, group_
 
 
 def linear(x, w, b, dtype, act=ACT_NONE, out=None, out_dtype=None, M=None, ldx=None, row_group=None, group_stride=0,
-           row_offset=0):
+           row_offset=0, out32=None):
     """y = act(x W^T + b); x f32 or `dtype`; W [N][K] in `dtype`."""
     N, K = w.shape
     M = x.numel() // x.shape[-1] if M is None else M
@@ -87,7 +89,8 @@ def linear(x, w, b, dtype, act=ACT_NONE, out=None, out_dtype=None, M=None, ldx=N
     if code == TMAE_F32 and (x.dtype != torch.float32 or out.dtype != torch.float32):
         raise ValueError("f32 path needs f32 tensors")
     _lib.call("tmae_linear_fwd", x.data_ptr(), x_f32, ldx, row_group or M, group_stride, row_offset, w.data_ptr(),
-              _p(b), out.data_ptr(), int(out.dtype == torch.float32), out.shape[-1], M, N, K, act, code, _stream())
+              _p(b), out.data_ptr(), int(out.dtype == torch.float32), out.shape[-1], _p(out32),
+              0 if out32 is None else out32.shape[-1], M, N, K, act, code, _stream())
     return out
 
 
@@ -140,23 +143,38 @@ def decoder_pred(x, w, b, imgs, n, L, patch, dtype):
 
 
 # --------------------------------------------------------------------------------------- LIC
-def conv3x3(x1, c1, ld1, n, H, W, w, b, y, ldy, cout, dtype, stride=1, act=ACT_NONE, pixel_shuffle=False, x2=None,
-            c2=0, ld2=0):
-    _lib.call("tmae_conv3x3_fwd", _p(x1), c1, ld1, _p(x2), c2, ld2, n, H, W, stride, _p(w), _p(b),
-              _p(y), ldy, cout, act, int(pixel_shuffle), dtype_code(dtype), _stream())
+def conv3x3(x1, c1, ld1, n, H, W, w, b, y, ldy, cout, dtype, stride=1, act=ACT_NONE, pixel_shuffle=False,
+            x2=None, c2=0, ld2=0, y_f32=None, y32=None, ld32=0, addend=None, ld_add=0, lrp_src=None, ld_src=0,
+            y2=None, ldy2=0, nb=(1, 1), strides=None):
+    """Batched 3x3 conv (tmae_conv3x3).  Pointer arguments: tensors or raw device addresses.
+    `strides` maps operand name (x1, x2, w, b, y, y32, a, src, y2) -> (s1, s2) element strides for the
+    nb[0] x nb[1] problems."""
+    a = ConvArgs()
+    a.x1, a.c1, a.ld1 = _p(x1), c1, ld1
+    a.x2, a.c2, a.ld2 = _p(x2), c2, ld2
+    a.n, a.H, a.W, a.stride = n, H, W, stride
+    a.w, a.bias = _p(w), _p(b)
+    a.cout, a.act, a.pixel_shuffle = cout, act, int(pixel_shuffle)
+    if dtype == torch.float32:
+        y_f32 = True  # the f32 path writes f32 everywhere
+    elif y_f32 is None:
+        y_f32 = isinstance(y, torch.Tensor) and y.dtype == torch.float32
+    a.y, a.y_f32, a.ldy = _p(y), int(y_f32), ldy
+    a.y32, a.ld32 = _p(y32), ld32
+    a.addend, a.ld_add = _p(addend), ld_add
+    a.lrp_src, a.ld_src = _p(lrp_src), ld_src
+    a.y2, a.ldy2 = _p(y2), ldy2
+    a.nb1, a.nb2 = nb
+    for name, (s1, s2) in (strides or {}).items():
+        setattr(a, f"{name}_s1", s1)
+        setattr(a, f"{name}_s2", s2)
+    _lib.call("tmae_conv3x3", ctypes.byref(a), dtype_code(dtype), _stream())
 
 
-def conv3x3_gaussian(x1, c1, ld1, n, H, W, w, b, cout, y, ldy, yoff, mu, ldmu, noise, lik, Mtot, yhat, ldh, dtype,
-                     x2=None, c2=0, ld2=0):
-    _lib.call("tmae_conv3x3_gaussian_fwd", _p(x1), c1, ld1, _p(x2), c2, ld2, n, H, W, _p(w),
-              _p(b), cout, _p(y), ldy, yoff, _p(mu), ldmu, _p(noise), _p(lik), Mtot,
-              _p(yhat), ldh, dtype_code(dtype), _stream())
-
-
-def conv3x3_lrp(x1, c1, ld1, n, H, W, w, b, cout, src, ld_src, dst1, ld_dst1, dst2, ld_dst2, dtype, x2=None,
-                c2=0, ld2=0):
-    _lib.call("tmae_conv3x3_lrp_fwd", _p(x1), c1, ld1, _p(x2), c2, ld2, n, H, W, _p(w), _p(b),
-              cout, _p(src), ld_src, _p(dst1), ld_dst1, _p(dst2), ld_dst2, dtype_code(dtype), _stream())
+def gc_slices(y, ldy, yoff, mu, sigma, ms_stride, ld_ms, noise, lik, Mtot, yhat, yhat_dtype, ld_yhat, yhat32, ld32, n,
+              HW, nslices, sw):
+    _lib.call("tmae_gc_slices_fwd", _p(y), ldy, yoff, _p(mu), _p(sigma), ms_stride, ld_ms, _p(noise), _p(lik), Mtot,
+              _p(yhat), dtype_code(yhat_dtype), ld_yhat, _p(yhat32), ld32, n, HW, nslices, sw, _stream())
 
 
 def _eb_params(eb) -> EBParams:
@@ -171,7 +189,7 @@ def _eb_params(eb) -> EBParams:
 
 
 def eb_likelihood(eb, z_nhwc, n, C, HW, noise=None, lik=None, zhat=None, table=None):
-    """EntropyBottleneck forward on NHWC z: returns (lik NCHW, z_hat NHWC)."""
+    """EntropyBottleneck forward on NHWC z: returns (lik NCHW, z_hat NHWC in zhat's dtype, default f32)."""
     dev = z_nhwc.device
     if lik is None:
         lik = torch.empty((n, C, HW), dtype=torch.float32, device=dev)
@@ -181,7 +199,7 @@ def eb_likelihood(eb, z_nhwc, n, C, HW, noise=None, lik=None, zhat=None, table=N
         table = torch.empty((C, 59), dtype=torch.float32, device=dev)
     params = _eb_params(eb)
     _lib.call("tmae_eb_likelihood_fwd", z_nhwc.data_ptr(), params, _p(noise), lik.data_ptr(), _p(zhat),
-              table.data_ptr(), n, C, HW, _stream())
+              dtype_code(zhat.dtype), table.data_ptr(), n, C, HW, _stream())
     return lik, zhat
 
 
