@@ -146,6 +146,11 @@ int tmae_eb_aux_loss(const tmae_eb_params* params, const float* target, float* o
 int tmae_gc_likelihood_fwd(const float* x, const float* scales, const float* means, const float* noise,
                            float* x_tilde, float* lik, int total, float scale_bound, void* stream);
 
+/* RateDistortionLoss bpp (models/Compression/loss/rd_loss.py:19-20): out[0] = (sum log y_lik + sum log z_lik)
+ * / (-ln2 * num_pixels), deterministic two-pass f64 reduction.  work: >= 512 doubles of device scratch. */
+int tmae_bpp_sum(const float* y_lik, long long ny, const float* z_lik, long long nz, double* work, float* out,
+                 double num_pixels, void* stream);
+
 /* layout helper: NHWC (channel stride ldx) -> NCHW */
 int tmae_nhwc_to_nchw(const float* x, int ldx, float* y, int n, int C, int HW, void* stream);
 

@@ -73,6 +73,11 @@ def test_mcm_vs_reference_golden(golden_dir, tmae, name, cfgd, seed, mode):
     np.testing.assert_allclose(float(out["loss"][0]), f[f"{mode}_ssim_loss"], rtol=1e-3)
     np.testing.assert_allclose(float(out["loss"][1]), f[f"{mode}_l1_loss"], rtol=1e-3)
     np.testing.assert_allclose(float(m.aux_loss()), f["aux_loss"], rtol=1e-4)
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    rd = RateDistortionLoss(lmbda=1e-4)(out, imgs)
+    np.testing.assert_allclose(float(rd["bpp_loss"]), f[f"{mode}_bpp_loss"], rtol=1e-3)
+    np.testing.assert_allclose(float(rd["loss"]), f[f"{mode}_loss"], rtol=1e-3)
 
 
 @pytest.fixture(scope="module")

@@ -62,6 +62,7 @@ SIGNATURES = {
     "tmae_eb_aux_loss": [ctypes.POINTER(EBParams), P, P, P, I, P],
     "tmae_gc_likelihood_fwd": [P, P, P, P, P, P, I, F, P],
     "tmae_nhwc_to_nchw": [P, I, P, I, I, I, P],
+    "tmae_bpp_sum": [P, LL, P, LL, P, P, ctypes.c_double, P],
 }
 
 _lib = None

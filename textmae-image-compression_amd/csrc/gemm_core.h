@@ -18,6 +18,8 @@
 //   bf16: v_mfma_f32_16x16x32_bf16 (f32 accumulate)       f32: v_mfma_f32_16x16x4_f32 (exact f32)
 #pragma once
 
+#include <algorithm>
+
 #include "common.h"
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -138,13 +140,10 @@ template <typename T> struct PatchSrc {
 };
 
 // ------------------------------------------------------------------ tile order
-// blockIdx.x -> (n tile, m tile).  xcd_remap gives each XCD a contiguous run of logical tiles (blocks
-// b and b+8 share an XCD); inside that run tiles go in groups of 8 M-tiles x all N-tiles, M fastest,
-// so the ~64 workgroups co-resident on one XCD touch ~8 activation panels and ~8 weight panels —
-// a working set that fits the XCD's 4 MiB L2 instead of streaming the whole weight per M panel.
-__device__ __forceinline__ void tile_order(int ntn, int ntm, int& tn, int& tm) {
+// logical tile id -> (n tile, m tile): groups of 8 M-tiles x all N-tiles, M fastest, so workgroups
+// running together share a few activation panels and weight panels in L2.
+__device__ __forceinline__ void tile_order(int t, int ntn, int ntm, int& tn, int& tm) {
   constexpr int GM = 8;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int group = GM * ntn;
   const int first_m = (t / group) * GM;
   const int gm = min(ntm - first_m, GM);
@@ -219,7 +218,11 @@ __device__ __forceinline__ void epilogue(const EPI& epi, const f32x4 (&acc)[TN][
   }
 }
 
-// ------------------------------------------------------------------ glds kernel
+// ------------------------------------------------------------------ glds kernel (persistent)
+// Each workgroup walks tiles t = blockIdx.x, blockIdx.x + gridDim.x, ... of its problem as ONE
+// continuous K-step stream over a 2-stage LDS ring: the first K-step of the next tile is already
+// in flight while the current tile's epilogue runs, so the per-tile prologue latency is paid once
+// per workgroup instead of once per tile (the hot-path GEMMs have only 8-16 K-steps per tile).
 template <typename T, int BN, int BM, int WGN, class WS, class XS, class EPI>
 __global__ void __launch_bounds__(256, 2)
 gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
@@ -239,28 +242,25 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave % WGN, wm = wave / WGN;
-  int tn, tm;
-  tile_order((N + BN - 1) / BN, (M + BM - 1) / BM, tn, tm);
-  const int n0 = tn * BN, m0 = tm * BM;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int ntiles = ntn * ntm;
+  const int nk = (K + BKE - 1) / BKE;
 
-  // this lane's rows / logical chunks for every glds it issues (constant over K)
   const int lr = 8 * wave + (lane >> 3);
   const int pch = lane & 7;
-  typename WS::Row wrow[WJ];
-  typename XS::Row xrow[XJ];
   int wc[WJ], xc[XJ];
 #pragma unroll
-  for (int j = 0; j < WJ; ++j) {
-    const int r = 32 * j + lr;
-    wrow[j] = ws.row(n0 + r);
-    wc[j] = pch ^ ((r >> 1) & 7);
-  }
+  for (int j = 0; j < WJ; ++j) wc[j] = pch ^ (((32 * j + lr) >> 1) & 7);
 #pragma unroll
-  for (int j = 0; j < XJ; ++j) {
-    const int r = 32 * j + lr;
-    xrow[j] = xs.row(m0 + r);
-    xc[j] = pch ^ ((r >> 1) & 7);
-  }
+  for (int j = 0; j < XJ; ++j) xc[j] = pch ^ (((32 * j + lr) >> 1) & 7);
+  typename WS::Row wrow[WJ];
+  typename XS::Row xrow[XJ];
+  auto set_rows = [&](int tn, int tm) {
+#pragma unroll
+    for (int j = 0; j < WJ; ++j) wrow[j] = ws.row(tn * BN + 32 * j + lr);
+#pragma unroll
+    for (int j = 0; j < XJ; ++j) xrow[j] = xs.row(tm * BM + 32 * j + lr);
+  };
   const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
   auto issue = [&](int stage, int kt) {
@@ -277,17 +277,52 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (K + BKE - 1) / BKE;
-  if (nk > 0) issue(0, 0);
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  int tn, tm;
+  tile_order(t, ntn, ntm, tn, tm);
+  if (nk == 0) {  // epilogue-only problems (e.g. an empty y_hat support)
+    for (; t < ntiles; t += gridDim.x) {
+      tile_order(t, ntn, ntm, tn, tm);
+      epilogue<TN, TM, WN, WM>(epi, acc, tn * BN, tm * BM, wn, wm, lane, M, N);
+    }
+    return;
+  }
+  set_rows(tn, tm);
+  issue(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) issue((kt + 1) & 1, kt + 1);
-    mfma_tile<T, BN, WN, WM, TN, TM>(lds + (kt & 1) * ROWS * 8, wn, wm, lane, acc);
+  int stage = 0, kt = 0;
+  while (true) {
+    // prefetch the next K-step: of this tile, or the first one of the next tile
+    const int tn_cur = tn, tm_cur = tm;
+    bool more = true;
+    if (kt + 1 < nk) {
+      issue(stage ^ 1, kt + 1);
+    } else if (t + (int)gridDim.x < ntiles) {
+      tile_order(t + gridDim.x, ntn, ntm, tn, tm);
+      set_rows(tn, tm);
+      issue(stage ^ 1, 0);
+    } else {
+      more = false;
+    }
+    mfma_tile<T, BN, WN, WM, TN, TM>(lds + stage * ROWS * 8, wn, wm, lane, acc);
+    if (kt + 1 == nk) {
+      epilogue<TN, TM, WN, WM>(epi, acc, tn_cur * BN, tm_cur * BM, wn, wm, lane, M, N);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      t += gridDim.x;
+      kt = 0;
+    } else {
+      ++kt;
+    }
+    if (!more) break;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    stage ^= 1;
   }
-  epilogue<TN, TM, WN, WM>(epi, acc, n0, m0, wn, wm, lane, M, N);
 }
 
 // ------------------------------------------------------------------ register-staged kernel
@@ -309,7 +344,7 @@ gemm_reg_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave % WGN, wm = wave / WGN;
   int tn, tm;
-  tile_order((N + BN - 1) / BN, (M + BM - 1) / BM, tn, tm);
+  tile_order(xcd_remap(blockIdx.x, gridDim.x), (N + BN - 1) / BN, (M + BM - 1) / BM, tn, tm);
   const int n0 = tn * BN, m0 = tm * BM;
   const int ch = tid & 7, r0 = tid >> 3;
 
@@ -384,14 +419,20 @@ static inline TileChoice choose_tile(int M, int N, int batch) {
 template <bool GLDS, typename T, int BN, int BM, int WGN, class WS, class XS, class EPI>
 static int launch_one(const char* name, const WS& ws, const XS& xs, const EPI& epi, int M, int N, int K, int n1,
                       int n2, hipStream_t st) {
-  const int grid = ceil_div(N, BN) * ceil_div(M, BM);
-  if (grid == 0 || n1 * n2 == 0) return TMAE_OK;
-  if constexpr (GLDS)
-    hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, WS, XS, EPI>), dim3(grid, n1 * n2), dim3(256), 0, st, ws, xs,
+  const int tiles = ceil_div(N, BN) * ceil_div(M, BM);
+  if (tiles == 0 || n1 * n2 == 0) return TMAE_OK;
+  if constexpr (GLDS) {
+    // persistent: about 2 resident workgroups per CU (LDS: 2 stages x (BN+BM) x 128 B), spread over problems
+    const int lds_bytes = 2 * (BN + BM) * 128;
+    const int per_cu = std::min(4, (160 * 1024) / lds_bytes);
+    const int slots = 256 * per_cu;
+    const int grid = std::max(1, std::min(tiles, ceil_div(slots, n1 * n2)));
+    hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, WS, XS, EPI>), dim3(grid, n1 * n2), dim3(256), 0, st, ws,
+                       xs, epi, M, N, K, n2);
+  } else {
+    hipLaunchKernelGGL((gemm_reg_kernel<T, BN, BM, WGN, WS, XS, EPI>), dim3(tiles, n1 * n2), dim3(256), 0, st, ws, xs,
                        epi, M, N, K, n2);
-  else
-    hipLaunchKernelGGL((gemm_reg_kernel<T, BN, BM, WGN, WS, XS, EPI>), dim3(grid, n1 * n2), dim3(256), 0, st, ws, xs,
-                       epi, M, N, K, n2);
+  }
   TMAE_LAUNCH_CHECK(name);
 }
 

@@ -79,3 +79,53 @@ extern "C" int tmae_nhwc_to_nchw(const float* x, int ldx, float* y, int n, int C
                      C, HW);
   TMAE_LAUNCH_CHECK("tmae_nhwc_to_nchw");
 }
+
+// ------------------------------------------------------------------ rate (bits per pixel)
+// RateDistortionLoss bpp term (reference models/Compression/loss/rd_loss.py:19-20):
+//   sum over both likelihood tensors of log(lik) / (-ln 2 * N*H*W)
+// Two deterministic passes: per-block partial sums in f64 (fixed grid), then one block folds them
+// in index order, so the result does not depend on scheduling.
+#define BPP_BLOCKS 512
+
+__global__ void __launch_bounds__(256)
+log_sum_partial_kernel(const float* __restrict__ a, long long na, const float* __restrict__ b, long long nb,
+                       double* __restrict__ part) {
+  __shared__ double red[256];
+  double s = 0.0;
+  const long long total = na + nb;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const float v = i < na ? a[i] : b[i - na];
+    s += (double)logf(v);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) log_sum_final_kernel(const double* __restrict__ part, int np, double scale,
+                                                            float* __restrict__ out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < np; i += 256) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (float)(red[0] * scale);
+}
+
+extern "C" int tmae_bpp_sum(const float* y_lik, long long ny, const float* z_lik, long long nz, double* work,
+                            float* out, double num_pixels, void* stream) {
+  TMAE_REQUIRE(work != nullptr && out != nullptr && num_pixels > 0, "tmae_bpp_sum: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(log_sum_partial_kernel, dim3(BPP_BLOCKS), dim3(256), 0, st, y_lik, ny, z_lik, nz, work);
+  hipLaunchKernelGGL(log_sum_final_kernel, dim3(1), dim3(256), 0, st, work, BPP_BLOCKS,
+                     1.0 / (-0.69314718055994530942 * num_pixels), out);
+  TMAE_LAUNCH_CHECK("tmae_bpp_sum");
+}

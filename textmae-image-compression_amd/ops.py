@@ -16,7 +16,7 @@ from ._lib import ACT_GELU, ACT_NONE, TMAE_BF16, TMAE_F32, ConvArgs, EBParams
 __all__ = [
     "ids_shuffle", "layernorm", "linear", "linear_residual", "patch_embed", "cls_rows", "mha", "decoder_embed",
     "mask_rows", "decoder_pred", "conv3x3", "gc_slices", "eb_likelihood", "eb_aux_loss",
-    "gc_likelihood", "nhwc_to_nchw", "dtype_code", "TMAE_F32", "TMAE_BF16", "ACT_NONE", "ACT_GELU",
+    "gc_likelihood", "nhwc_to_nchw", "bpp", "dtype_code", "TMAE_F32", "TMAE_BF16", "ACT_NONE", "ACT_GELU",
 ]
 
 
@@ -226,4 +226,20 @@ def gc_likelihood(x, scales, means=None, noise=None, scale_bound=0.11):
 def nhwc_to_nchw(x, ldx, n, C, H, W, out=None):
     out = torch.empty((n, C, H, W), dtype=torch.float32, device=x.device) if out is None else out
     _lib.call("tmae_nhwc_to_nchw", x.data_ptr(), ldx, out.data_ptr(), n, C, H * W, _stream())
+    return out
+
+
+_BPP_WORK = {}
+
+
+def bpp(y_lik, z_lik, num_pixels):
+    """sum(log y_lik) + sum(log z_lik), / (-ln 2 * num_pixels): a 0-d f32 device tensor (rd_loss.py:19-20)."""
+    y = _need(y_lik.contiguous(), torch.float32, "y likelihood")
+    z = _need(z_lik.contiguous(), torch.float32, "z likelihood")
+    work = _BPP_WORK.get(y.device)
+    if work is None:
+        work = _BPP_WORK[y.device] = torch.empty(512, dtype=torch.float64, device=y.device)
+    out = torch.empty((), dtype=torch.float32, device=y.device)
+    _lib.call("tmae_bpp_sum", y.data_ptr(), y.numel(), z.data_ptr(), z.numel(), work.data_ptr(), out.data_ptr(),
+              float(num_pixels), _stream())
     return out

@@ -1,0 +1,56 @@
+"""Micro-benchmark of the MFMA GEMM on the hot path's token-GEMM shapes, beside torch.matmul
+(hipBLASLt) on the same shapes as an achievable-speed reference.  Interleaved rounds, one process."""
+import json
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+import textmae_amd  # noqa: E402
+from textmae_amd import ops  # noqa: E402
+
+SHAPES = {  # name: (M, N, K, act)
+    "enc_qkv": (9280, 2304, 768, 0), "enc_fc1": (9280, 3072, 768, 1), "enc_fc2": (9280, 768, 3072, 0),
+    "enc_proj": (9280, 768, 768, 0), "dec_qkv": (16448, 1536, 512, 0), "dec_fc1": (16448, 2048, 512, 1),
+    "dec_fc2": (16448, 512, 2048, 0), "big": (8192, 8192, 8192, 0),
+}
+
+
+def ev_time(fn, reps):
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps * 1e-3
+
+
+def main():
+    dt = torch.bfloat16
+    out = {}
+    names = sys.argv[1:] or list(SHAPES)
+    for name in names:
+        M, N, K, act = SHAPES[name]
+        x = torch.randn(M, K, device="cuda").to(dt)
+        w = (torch.randn(N, K, device="cuda") / K ** 0.5).to(dt)
+        b = torch.randn(N, device="cuda")
+        y = torch.empty(M, N, device="cuda", dtype=dt)
+        mine = lambda: ops.linear(x, w, b, dt, act=act, out=y)
+        ref = lambda: torch.nn.functional.linear(x, w, b.to(dt))
+        reps = 20 if name != "big" else 5
+        tm, tr = [], []
+        for _ in range(5):
+            tm.append(ev_time(mine, reps))
+            tr.append(ev_time(ref, reps))
+        fl = 2.0 * M * N * K
+        out[name] = {"mine_us": round(min(tm) * 1e6, 1), "torch_us": round(min(tr) * 1e6, 1),
+                     "mine_tf": round(fl / min(tm) / 1e12, 1), "torch_tf": round(fl / min(tr) / 1e12, 1)}
+        print(name, out[name], flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
