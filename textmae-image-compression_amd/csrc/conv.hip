@@ -25,6 +25,25 @@ template <typename OT, int ACT> struct EpiPixelShuffle2 {
       out[(((size_t)b * 2 * H + oy) * 2 * W + ox) * ldo + c] = to_out<OT>(o);
     }
   }
+  // 8 columns = output channels c, c+1 of the 4 sub-pixels: four 2-channel stores
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
+    const int hw = H * W;
+    const int b = m / hw, rem = m - b * hw;
+    const int y = rem / W, x = rem - y * W;
+    f32x4 b0, b1;
+    load8f(bias + n, b0, b1);
+    lo += b0; hi += b1;
+    const int c = n >> 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float o0 = lo[j], o1 = hi[j];
+      if (ACT == TMAE_ACT_GELU) { o0 = gelu_erf(o0); o1 = gelu_erf(o1); }
+      const int oy = 2 * y + (j >> 1), ox = 2 * x + (j & 1);
+      OT* p = out + (((size_t)b * 2 * H + oy) * 2 * W + ox) * ldo + c;
+      p[0] = to_out<OT>(o0);
+      p[1] = to_out<OT>(o1);
+    }
+  }
 };
 
 // last lrp_transform conv: y_hat = y_hat_pre + 0.5 * tanh(acc + bias)  (MCM.py:779-784)
@@ -50,6 +69,16 @@ template <typename OT> struct EpiLRP {
     for (int j = 0; j < 4; ++j) o[j] = o[j] + 0.5f * tanhf(v[j]);
     store4(out + (size_t)m * ldo + n, o);
     if (out2) store4(out2 + (size_t)m * ldo2 + n, o);
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
+    f32x4 b0, b1, o0, o1;
+    load8f(bias + n, b0, b1);
+    load8f(src + (size_t)m * lds + n, o0, o1);
+    lo += b0; hi += b1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { o0[j] += 0.5f * tanhf(lo[j]); o1[j] += 0.5f * tanhf(hi[j]); }
+    store8(out + (size_t)m * ldo + n, o0, o1);
+    if (out2) store8(out2 + (size_t)m * ldo2 + n, o0, o1);
   }
 };
 

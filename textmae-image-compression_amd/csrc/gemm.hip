@@ -31,6 +31,17 @@ struct EpiResidual {
     if (bias) v += load4f(bias + n);
     store4(p, load4f(p) + v);
   }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
+    float* p = out + (size_t)m * ldo + n;
+    f32x4 r0, r1;
+    load8f(p, r0, r1);
+    if (bias) {
+      f32x4 b0, b1;
+      load8f(bias + n, b0, b1);
+      lo += b0; hi += b1;
+    }
+    store8(p, r0 + lo, r1 + hi);
+  }
 };
 
 // patch embed: token row b*(keep+1) + 1 + k  <-  acc + bias + pos[1 + p]   (MCM.py:615-626)
@@ -47,6 +58,14 @@ struct EpiPatchEmbed {
     v += load4f(bias + n);
     v += load4f(pos + (size_t)(1 + p) * D + n);
     store4(tok + ((size_t)b * (keep + 1) + 1 + k) * D + n, v);
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
+    const int b = m / keep, k = m - b * keep;
+    const int p = (int)ids[(size_t)b * L + k];
+    f32x4 b0, b1, p0, p1;
+    load8f(bias + n, b0, b1);
+    load8f(pos + (size_t)(1 + p) * D + n, p0, p1);
+    store8(tok + ((size_t)b * (keep + 1) + 1 + k) * D + n, lo + b0 + p0, hi + b1 + p1);
   }
 };
 
@@ -65,6 +84,14 @@ struct EpiDecoderEmbed {
     v += load4f(bias + n);
     v += load4f(pos + (size_t)row * D + n);
     store4(out + ((size_t)b * (L + 1) + row) * D + n, v);
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
+    const int b = m / ntok, k = m - b * ntok;
+    const int row = (k == 0) ? 0 : 1 + (int)ids[(size_t)b * L + (k - 1)];
+    f32x4 b0, b1, p0, p1;
+    load8f(bias + n, b0, b1);
+    load8f(pos + (size_t)row * D + n, p0, p1);
+    store8(out + ((size_t)b * (L + 1) + row) * D + n, lo + b0 + p0, hi + b1 + p1);
   }
 };
 

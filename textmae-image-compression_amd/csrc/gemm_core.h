@@ -18,7 +18,12 @@
 //   bf16: v_mfma_f32_16x16x32_bf16 (f32 accumulate)       f32: v_mfma_f32_16x16x4_f32 (exact f32)
 #pragma once
 
+#include <stdlib.h>
+
 #include <algorithm>
+#include <cmath>
+#include <type_traits>
+#include <utility>
 
 #include "common.h"
 
@@ -35,6 +40,7 @@ static __device__ __attribute__((aligned(64))) uint4 g_tmae_zero_page[4] = {};
 // M0 is saved/restored inside the statement (cdna_hip_programming.md §5.7).
 __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_addr) {
   unsigned keep;
+  lds_addr = __builtin_amdgcn_readfirstlane(lds_addr);  // wave-uniform by construction; pin it to an SGPR
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
                : "v"(gsrc), "s"(lds_addr)
@@ -203,36 +209,78 @@ __device__ __forceinline__ void mfma_tile(const uint4* base, int wn, int wm, int
   }
 }
 
-template <int TN, int TM, int WN, int WM, class EPI>
-__device__ __forceinline__ void epilogue(const EPI& epi, const f32x4 (&acc)[TN][TM], int n0, int m0, int wn, int wm,
-                                         int lane, int M, int N) {
+// ------------------------------------------------------------------ epilogue
+// In the MFMA layout a lane holds 4 consecutive output columns of one row per 16x16 block, so
+// direct stores write 16 rows x 32 B per instruction: measured 0.9-1.4 TB/s, the epilogue took ~40 %
+// of a K=768 GEMM.  Instead each wave transposes its accumulators through its own LDS region
+// (16 rows x WN columns of f32 at a time, rows padded by 16 B: conflict-free ds_write_b128) and
+// every lane then emits 8 CONSECUTIVE columns of one row: per instruction WN/8 lanes cover a row
+// segment of WN columns (full 128-256 B lines for bf16 out).
+//
+// Functors provide operator()(m, n, f32x4) for 4 columns and optionally wide(m, n, lo, hi) for 8.
+template <class E, class = void> struct HasWide : std::false_type {};
+template <class E>
+struct HasWide<E, std::void_t<decltype(std::declval<const E&>().wide(0, 0, f32x4{}, f32x4{}))>> : std::true_type {};
+
+template <class EPI>
+__device__ __forceinline__ void epi_emit8(const EPI& epi, int m, int n, f32x4 lo, f32x4 hi, int N) {
+  if constexpr (HasWide<EPI>::value) {
+    if (n + 8 <= N) {
+      epi.wide(m, n, lo, hi);
+      return;
+    }
+  }
+  if (n < N) epi(m, n, lo);
+  if (n + 4 < N) epi(m, n + 4, hi);
+}
+
+template <int WN> struct EpiRegion {
+  static constexpr int ST = WN + 4;          // row stride (floats)
+  static constexpr int FLOATS = 16 * ST;     // one wave's region
+};
+
+// acc[i][j]: rows n = 16 i + 4 fq + r of D (weight side), column m = 16 j + fr (activation side)
+template <int TN, int TM, int WN, class EPI>
+__device__ __forceinline__ void epilogue_lds(const EPI& epi, const f32x4 (&acc)[TN][TM], float* region, int n0,
+                                             int m0, int lane, int M, int N) {
+  static_assert(WN >= 32 && WN % 32 == 0, "epilogue_lds: WN must be a multiple of 32");
+  constexpr int ST = EpiRegion<WN>::ST;
+  constexpr int LPR = WN / 8;   // lanes per row
+  constexpr int RPI = 64 / LPR; // rows per read round
   const int fr = lane & 15, fq = lane >> 4;
+  const int rr = lane / LPR, cc = lane - rr * LPR;
 #pragma unroll
-  for (int i = 0; i < TN; ++i) {
-    const int n = n0 + wn * WN + 16 * i + 4 * fq;
+  for (int j = 0; j < TM; ++j) {
 #pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int m = m0 + wm * WM + 16 * j + fr;
-      if (m < M && n < N) epi(m, n, acc[i][j]);
+    for (int i = 0; i < TN; ++i) *reinterpret_cast<f32x4*>(region + fr * ST + 16 * i + 4 * fq) = acc[i][j];
+#pragma unroll
+    for (int q = 0; q < 16 / RPI; ++q) {
+      const int row = q * RPI + rr;
+      const float* src = region + row * ST + 8 * cc;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
+      const int m = m0 + 16 * j + row;
+      if (m < M) epi_emit8(epi, m, n0 + 8 * cc, lo, hi, N);
     }
   }
 }
 
-// ------------------------------------------------------------------ glds kernel (persistent)
-// Each workgroup walks tiles t = blockIdx.x, blockIdx.x + gridDim.x, ... of its problem as ONE
-// continuous K-step stream over a 2-stage LDS ring: the first K-step of the next tile is already
-// in flight while the current tile's epilogue runs, so the per-tile prologue latency is paid once
-// per workgroup instead of once per tile (the hot-path GEMMs have only 8-16 K-steps per tile).
-template <typename T, int BN, int BM, int WGN, class WS, class XS, class EPI>
-__global__ void __launch_bounds__(256, 2)
-gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
+// ------------------------------------------------------------------ glds kernel
+// One output tile per workgroup (XCD-aware tile order), 2-stage LDS ring: the next K-step's
+// LDS-DMA is in flight under the current K-step's MFMAs.  After the last K-step the ring is reused
+// as the epilogue's transpose buffer.  (A persistent walk with the next tile's first K-step in flight
+// under the epilogue measured no better on the hot shapes and was dropped.)
+template <typename T, int BN, int BM, int WGN, int NW, class WS, class XS, class EPI>
+__global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2)
+gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
   constexpr int BKE = 8 * Elt<T>::EPC;
-  constexpr int WGM = 4 / WGN;
+  constexpr int WGM = NW / WGN;
   constexpr int WN = BN / WGN, WM = BM / WGM;
   constexpr int TN = WN / 16, TM = WM / 16;
-  constexpr int WJ = BN / 32, XJ = BM / 32;  // glds instructions per wave per stage
+  constexpr int PR = 8 * NW;                 // rows covered by one glds round of all waves
+  constexpr int WJ = BN / PR, XJ = BM / PR;  // glds instructions per wave per stage
   constexpr int ROWS = BN + BM;
-  static_assert(TN >= 1 && TM >= 1 && WJ >= 1 && XJ >= 1, "bad tile");
+  static_assert(TN >= 1 && TM >= 1 && WJ >= 1 && XJ >= 1 && BN % PR == 0 && BM % PR == 0, "bad tile");
   __shared__ __attribute__((aligned(16))) uint4 lds[2 * ROWS * 8];
 
   const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
@@ -243,32 +291,32 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave % WGN, wm = wave / WGN;
   const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
-  const int ntiles = ntn * ntm;
   const int nk = (K + BKE - 1) / BKE;
 
   const int lr = 8 * wave + (lane >> 3);
   const int pch = lane & 7;
   int wc[WJ], xc[XJ];
 #pragma unroll
-  for (int j = 0; j < WJ; ++j) wc[j] = pch ^ (((32 * j + lr) >> 1) & 7);
+  for (int j = 0; j < WJ; ++j) wc[j] = pch ^ (((PR * j + lr) >> 1) & 7);
 #pragma unroll
-  for (int j = 0; j < XJ; ++j) xc[j] = pch ^ (((32 * j + lr) >> 1) & 7);
+  for (int j = 0; j < XJ; ++j) xc[j] = pch ^ (((PR * j + lr) >> 1) & 7);
   typename WS::Row wrow[WJ];
   typename XS::Row xrow[XJ];
   auto set_rows = [&](int tn, int tm) {
 #pragma unroll
-    for (int j = 0; j < WJ; ++j) wrow[j] = ws.row(tn * BN + 32 * j + lr);
+    for (int j = 0; j < WJ; ++j) wrow[j] = ws.row(tn * BN + PR * j + lr);
 #pragma unroll
-    for (int j = 0; j < XJ; ++j) xrow[j] = xs.row(tm * BM + 32 * j + lr);
+    for (int j = 0; j < XJ; ++j) xrow[j] = xs.row(tm * BM + PR * j + lr);
   };
   const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
   auto issue = [&](int stage, int kt) {
+    if (diag & 4) return;  // timing diagnostic: no staging
     const unsigned sb = lds_base + (unsigned)stage * ROWS * 128u;
 #pragma unroll
-    for (int j = 0; j < WJ; ++j) glds16(ws.addr(wrow[j], kt, wc[j]), sb + (32u * j + 8u * wave_u) * 128u);
+    for (int j = 0; j < WJ; ++j) glds16(ws.addr(wrow[j], kt, wc[j]), sb + (unsigned)(PR * j + 8 * wave_u) * 128u);
 #pragma unroll
-    for (int j = 0; j < XJ; ++j) glds16(xs.addr(xrow[j], kt, xc[j]), sb + (BN + 32u * j + 8u * wave_u) * 128u);
+    for (int j = 0; j < XJ; ++j) glds16(xs.addr(xrow[j], kt, xc[j]), sb + (unsigned)(BN + PR * j + 8 * wave_u) * 128u);
   };
 
   f32x4 acc[TN][TM];
@@ -277,52 +325,26 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  int t = blockIdx.x;
-  if (t >= ntiles) return;
   int tn, tm;
-  tile_order(t, ntn, ntm, tn, tm);
-  if (nk == 0) {  // epilogue-only problems (e.g. an empty y_hat support)
-    for (; t < ntiles; t += gridDim.x) {
-      tile_order(t, ntn, ntm, tn, tm);
-      epilogue<TN, TM, WN, WM>(epi, acc, tn * BN, tm * BM, wn, wm, lane, M, N);
-    }
-    return;
-  }
-  set_rows(tn, tm);
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int stage = 0, kt = 0;
-  while (true) {
-    // prefetch the next K-step: of this tile, or the first one of the next tile
-    const int tn_cur = tn, tm_cur = tm;
-    bool more = true;
-    if (kt + 1 < nk) {
-      issue(stage ^ 1, kt + 1);
-    } else if (t + (int)gridDim.x < ntiles) {
-      tile_order(t + gridDim.x, ntn, ntm, tn, tm);
-      set_rows(tn, tm);
-      issue(stage ^ 1, 0);
-    } else {
-      more = false;
-    }
-    mfma_tile<T, BN, WN, WM, TN, TM>(lds + stage * ROWS * 8, wn, wm, lane, acc);
-    if (kt + 1 == nk) {
-      epilogue<TN, TM, WN, WM>(epi, acc, tn_cur * BN, tm_cur * BM, wn, wm, lane, M, N);
-#pragma unroll
-      for (int i = 0; i < TN; ++i)
-#pragma unroll
-        for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      t += gridDim.x;
-      kt = 0;
-    } else {
-      ++kt;
-    }
-    if (!more) break;
+  tile_order(xcd_remap(blockIdx.x, gridDim.x), ntn, ntm, tn, tm);
+  if (nk > 0) {
+    set_rows(tn, tm);
+    issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    stage ^= 1;
+    int stage = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) issue(stage ^ 1, kt + 1);
+      if (!(diag & 2)) mfma_tile<T, BN, WN, WM, TN, TM>(lds + stage * ROWS * 8, wn, wm, lane, acc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      stage ^= 1;
+    }
   }
+  static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= 2 * ROWS * 128, "epilogue region exceeds the LDS ring");
+  if (!(diag & 1))
+    epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
+                             tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
 }
 
 // ------------------------------------------------------------------ register-staged kernel
@@ -391,44 +413,53 @@ gemm_reg_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
     if (kt + 1 < nk) swrite((kt + 1) & 1);
     __syncthreads();
   }
-  epilogue<TN, TM, WN, WM>(epi, acc, n0, m0, wn, wm, lane, M, N);
+  static_assert(4 * EpiRegion<WN>::FLOATS * 4 <= 2 * ROWS * 128, "epilogue region exceeds the LDS ring");
+  epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS, n0 + wn * WN,
+                           m0 + wm * WM, lane, M, N);
 }
 
 // ------------------------------------------------------------------ launch with tile selection
-struct TileChoice { int bn, bm; };
+// host-side tuning knobs (environment, read once): experiments without rebuilding
+static inline int gemm_knob(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
 
-// pick the tile that maximises (useful fraction of padded MFMA work) x (fill of 2 WGs/CU) x (tile
-// efficiency of larger tiles); ties go to the larger tile
-static inline TileChoice choose_tile(int M, int N, int batch) {
-  const int cand[5][2] = {{128, 128}, {64, 128}, {32, 128}, {64, 64}, {32, 64}};
-  const double eff[5] = {1.0, 0.86, 0.70, 0.72, 0.55};
+struct TileChoice { int bn, bm, nw; };
+
+// Tile candidates: 4-wave tiles run 2 workgroups per CU, the 8-wave 256x256 tile one (128 KiB LDS).
+// Score = (useful fraction of the padded MFMA work) x (tail quantisation: tiles / (rounds x slots))
+// x (relative per-CU throughput of the tile shape at full occupancy).  TMAE_GEMM_TILE=<index>
+// forces a candidate (tuning experiments without rebuilding).
+static constexpr int kTileCand[6][3] = {{256, 256, 8}, {128, 128, 4}, {64, 128, 4}, {32, 128, 4}, {64, 64, 4}, {32, 64, 4}};
+static inline TileChoice choose_tile(int M, int N, int batch, bool allow_big) {
+  const double eff[6] = {1.45, 1.0, 0.86, 0.70, 0.72, 0.55};
+  const int forced = gemm_knob("TMAE_GEMM_TILE", -1);
+  if (forced >= 0 && forced < 6 && (allow_big || forced > 0))
+    return TileChoice{kTileCand[forced][0], kTileCand[forced][1], kTileCand[forced][2]};
   double best = -1.0;
-  TileChoice tc{128, 128};
-  for (int i = 0; i < 5; ++i) {
-    const int bn = cand[i][0], bm = cand[i][1];
+  TileChoice tc{128, 128, 4};
+  for (int i = allow_big ? 0 : 1; i < 6; ++i) {
+    const int bn = kTileCand[i][0], bm = kTileCand[i][1];
     const double tn = ceil_div(N, bn), tm = ceil_div(M, bm);
     const double useful = ((double)N / (tn * bn)) * ((double)M / (tm * bm));
     const double wgs = tn * tm * batch;
-    const double fill = wgs >= 512.0 ? 1.0 : wgs / 512.0;
-    const double score = useful * fill * eff[i];
-    if (score > best + 1e-9) { best = score; tc = TileChoice{bn, bm}; }
+    const double slots = kTileCand[i][2] == 8 ? 256.0 : 512.0;
+    const double quant = wgs / (std::ceil(wgs / slots) * slots);
+    const double score = useful * quant * eff[i];
+    if (score > best + 1e-9) { best = score; tc = TileChoice{bn, bm, kTileCand[i][2]}; }
   }
   return tc;
 }
 
-template <bool GLDS, typename T, int BN, int BM, int WGN, class WS, class XS, class EPI>
+template <bool GLDS, typename T, int BN, int BM, int WGN, int NW, class WS, class XS, class EPI>
 static int launch_one(const char* name, const WS& ws, const XS& xs, const EPI& epi, int M, int N, int K, int n1,
                       int n2, hipStream_t st) {
   const int tiles = ceil_div(N, BN) * ceil_div(M, BM);
   if (tiles == 0 || n1 * n2 == 0) return TMAE_OK;
   if constexpr (GLDS) {
-    // persistent: about 2 resident workgroups per CU (LDS: 2 stages x (BN+BM) x 128 B), spread over problems
-    const int lds_bytes = 2 * (BN + BM) * 128;
-    const int per_cu = std::min(4, (160 * 1024) / lds_bytes);
-    const int slots = 256 * per_cu;
-    const int grid = std::max(1, std::min(tiles, ceil_div(slots, n1 * n2)));
-    hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, WS, XS, EPI>), dim3(grid, n1 * n2), dim3(256), 0, st, ws,
-                       xs, epi, M, N, K, n2);
+    hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, NW, WS, XS, EPI>), dim3(tiles, n1 * n2), dim3(64 * NW), 0,
+                       st, ws, xs, epi, M, N, K, n2, gemm_knob("TMAE_GEMM_DIAG", 0));
   } else {
     hipLaunchKernelGGL((gemm_reg_kernel<T, BN, BM, WGN, WS, XS, EPI>), dim3(tiles, n1 * n2), dim3(256), 0, st, ws, xs,
                        epi, M, N, K, n2);
@@ -440,12 +471,16 @@ template <bool GLDS, typename T, class XS, class EPI>
 static int launch_gemm(const char* name, const T* w, long long ws1, long long ws2, int N, int K, const XS& xs,
                        const EPI& epi, int M, int n1 = 1, int n2 = 1, hipStream_t st = 0) {
   DenseSrc<T> ws{w, K, N, K, 1 << 30, 0, 0, BStride{ws1, ws2}};
-  const TileChoice tc = choose_tile(M, N, n1 * n2);
-  if (tc.bn == 128) return launch_one<GLDS, T, 128, 128, 2>(name, ws, xs, epi, M, N, K, n1, n2, st);
-  if (tc.bn == 64 && tc.bm == 128) return launch_one<GLDS, T, 64, 128, 1>(name, ws, xs, epi, M, N, K, n1, n2, st);
-  if (tc.bn == 32 && tc.bm == 128) return launch_one<GLDS, T, 32, 128, 1>(name, ws, xs, epi, M, N, K, n1, n2, st);
-  if (tc.bn == 64) return launch_one<GLDS, T, 64, 64, 2>(name, ws, xs, epi, M, N, K, n1, n2, st);
-  return launch_one<GLDS, T, 32, 64, 1>(name, ws, xs, epi, M, N, K, n1, n2, st);
+  // the 8-wave tile is built for the bf16 glds path only (the f32 path is the parity path)
+  const TileChoice tc = choose_tile(M, N, n1 * n2, GLDS && sizeof(T) == 2);
+  if constexpr (GLDS && sizeof(T) == 2) {
+    if (tc.nw == 8) return launch_one<GLDS, T, 256, 256, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
+  }
+  if (tc.bn == 128) return launch_one<GLDS, T, 128, 128, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
+  if (tc.bn == 64 && tc.bm == 128) return launch_one<GLDS, T, 64, 128, 1, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
+  if (tc.bn == 32 && tc.bm == 128) return launch_one<GLDS, T, 32, 128, 1, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
+  if (tc.bn == 64) return launch_one<GLDS, T, 64, 64, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
+  return launch_one<GLDS, T, 32, 64, 1, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
 }
 
 // ------------------------------------------------------------------ shared epilogues
@@ -474,6 +509,24 @@ template <typename OT, int ACT> struct EpiStore {
     }
     store4(out + (size_t)m * ldo + n, v);
     if (out32) store4(out32 + (size_t)m * ld32 + n, v);
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
+    if (bias) {
+      f32x4 b0, b1;
+      load8f(bias + n, b0, b1);
+      lo += b0; hi += b1;
+    }
+    if (addend) {
+      f32x4 a0, a1;
+      load8f(addend + (size_t)m * ld_add + n, a0, a1);
+      lo += a0; hi += a1;
+    }
+    if (ACT == TMAE_ACT_GELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { lo[j] = gelu_erf(lo[j]); hi[j] = gelu_erf(hi[j]); }
+    }
+    store8(out + (size_t)m * ldo + n, lo, hi);
+    if (out32) store8(out32 + (size_t)m * ld32 + n, lo, hi);
   }
 };
 

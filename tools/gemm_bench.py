@@ -1,6 +1,7 @@
 """Micro-benchmark of the MFMA GEMM on the hot path's token-GEMM shapes, beside torch.matmul
 (hipBLASLt) on the same shapes as an achievable-speed reference.  Interleaved rounds, one process."""
 import json
+import os
 import sys
 import time
 
@@ -41,13 +42,25 @@ def main():
         mine = lambda: ops.linear(x, w, b, dt, act=act, out=y)
         ref = lambda: torch.nn.functional.linear(x, w, b.to(dt))
         reps = 20 if name != "big" else 5
-        tm, tr = [], []
-        for _ in range(5):
-            tm.append(ev_time(mine, reps))
-            tr.append(ev_time(ref, reps))
         fl = 2.0 * M * N * K
-        out[name] = {"mine_us": round(min(tm) * 1e6, 1), "torch_us": round(min(tr) * 1e6, 1),
-                     "mine_tf": round(fl / min(tm) / 1e12, 1), "torch_tf": round(fl / min(tr) / 1e12, 1)}
+        res = {}
+        for tile in os.environ.get("GEMM_TILES", "auto").split(","):
+            if tile == "auto":
+                os.environ.pop("TMAE_GEMM_TILE", None)
+            else:
+                os.environ["TMAE_GEMM_TILE"] = tile
+            for diag in os.environ.get("GEMM_DIAG", "0").split(","):
+                os.environ["TMAE_GEMM_DIAG"] = diag
+                tm = [ev_time(mine, reps) for _ in range(5)]
+                key = f"t{tile}" + (f"d{diag}" if diag != "0" else "")
+                res[key + "_us"] = round(min(tm) * 1e6, 1)
+                if diag == "0":
+                    res[key + "_tf"] = round(fl / min(tm) / 1e12, 1)
+        os.environ.pop("TMAE_GEMM_TILE", None)
+        os.environ.pop("TMAE_GEMM_DIAG", None)
+        tr = [ev_time(ref, reps) for _ in range(5)]
+        res["torch_tf"] = round(fl / min(tr) / 1e12, 1)
+        out[name] = res
         print(name, out[name], flush=True)
     print(json.dumps(out))
 
