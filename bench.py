@@ -91,7 +91,8 @@ def dominant_kernel_roofline(model, batch, reps, dtype):
             traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    return {"kernel": "gemm_kernel<bf16,128,128> enc fc1+GELU (M=%d,N=%d,K=%d)" % (M, N, K), "bound": "mfma",
+    plan = ops.gemm_plan(M, N, K, dtype)
+    return {"kernel": "%s enc fc1+GELU (M=%d,N=%d,K=%d)" % (plan, M, N, K), "bound": "mfma",
             "achieved": round(ach, 2), "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s", "frac": round(ach * 1e12 / PEAK_BF16, 4),
             "traffic": traffic, "avg_launch_us": round(t * 1e6, 2), "flops_per_launch": flops}
 

@@ -154,6 +154,37 @@ int tmae_bpp_sum(const float* y_lik, long long ny, const float* z_lik, long long
 /* layout helper: NHWC (channel stride ldx) -> NCHW */
 int tmae_nhwc_to_nchw(const float* x, int ldx, float* y, int n, int C, int HW, void* stream);
 
+/* ---------------------------------------------------------------- entropy coding (host, no device work)
+ * compressai 1.2.4's coder restated (csrc/rans.cpp; not vendored in the reference): 64-bit rANS, 16-bit
+ * precision, bypass-escaped tails.  CDF tables are int32 [ncdf][cdf_stride] rows with cdf_sizes[c] valid
+ * entries each (= _quantized_cdf / _cdf_length / _offset of an entropy model). */
+
+/* compressai pmf_to_quantized_cdf (EntropyModel._pmf_to_cdf; update() at testing.py:223): cdf[n + 1] */
+int tmae_pmf_to_quantized_cdf(const float* pmf, int n, int precision, int32_t* cdf);
+
+/* BufferedRansEncoder (MCM.py:845): create, encode_with_indexes (882-887) any number of times, flush
+ * (890; *nbytes = stream length), take the bytes, destroy. */
+int tmae_rans_encoder_create(void** handle);
+int tmae_rans_encode_with_indexes(void* handle, const int32_t* symbols, const int32_t* indexes, long long n,
+                                  const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes,
+                                  const int32_t* offsets, int ncdf);
+int tmae_rans_encoder_flush(void* handle, long long* nbytes);
+int tmae_rans_encoder_take(void* handle, uint8_t* out, long long cap);
+int tmae_rans_encoder_destroy(void* handle);
+
+/* RansDecoder (MCM.py:917-918): set_stream = create (the bytes are copied), decode_stream (941-943) any
+ * number of times, each consuming the next n symbols, destroy. */
+int tmae_rans_decoder_create(const uint8_t* data, long long len, void** handle);
+int tmae_rans_decode_with_indexes(void* handle, const int32_t* indexes, long long n, const int32_t* cdfs,
+                                  int cdf_stride, const int32_t* cdf_sizes, const int32_t* offsets, int ncdf,
+                                  int32_t* out);
+int tmae_rans_decoder_destroy(void* handle);
+
+/* diagnostics (no device work): writes into out[len] the name of the MFMA GEMM variant that
+ * tmae_linear_fwd / tmae_conv3x3 launch for an M x N x K problem batched `batch` times (tile shape,
+ * waves per workgroup, LDS ring), e.g. "ring<bf16,256x256,8w,BK32x4>". */
+int tmae_gemm_plan(int M, int N, int K, int batch, int dtype, char* out, int len);
+
 #ifdef __cplusplus
 }
 #endif

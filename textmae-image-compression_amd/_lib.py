@@ -63,6 +63,16 @@ SIGNATURES = {
     "tmae_gc_likelihood_fwd": [P, P, P, P, P, P, I, F, P],
     "tmae_nhwc_to_nchw": [P, I, P, I, I, I, P],
     "tmae_bpp_sum": [P, LL, P, LL, P, P, ctypes.c_double, P],
+    "tmae_gemm_plan": [I, I, I, I, I, ctypes.c_char_p, I],
+    "tmae_pmf_to_quantized_cdf": [P, I, I, P],
+    "tmae_rans_encoder_create": [ctypes.POINTER(ctypes.c_void_p)],
+    "tmae_rans_encode_with_indexes": [P, P, P, LL, P, I, P, P, I],
+    "tmae_rans_encoder_flush": [P, ctypes.POINTER(ctypes.c_longlong)],
+    "tmae_rans_encoder_take": [P, P, LL],
+    "tmae_rans_encoder_destroy": [P],
+    "tmae_rans_decoder_create": [P, LL, ctypes.POINTER(ctypes.c_void_p)],
+    "tmae_rans_decode_with_indexes": [P, P, LL, P, I, P, P, I, P],
+    "tmae_rans_decoder_destroy": [P],
 }
 
 _lib = None

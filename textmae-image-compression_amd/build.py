@@ -18,12 +18,15 @@ LIB_PATH = os.path.join(LIB_DIR, "libtmae.so")
 INCLUDE = os.path.join(os.path.dirname(PKG_DIR), "include")
 ARCH = os.environ.get("TMAE_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", "g++")
 
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", "-Wno-unused-result"]
+HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"-I{INCLUDE}", "-Wall"]
 
 
 def _sources():
-    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip"))
+    """device sources (*.hip, hipcc) and host-only sources (*.cpp: the entropy coder, g++)"""
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
 
 
 def _deps_mtime():
@@ -36,12 +39,15 @@ def _compile(src: str, hdr_mtime: float, verbose: bool) -> str:
     obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
         return obj
-    cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    if src.endswith(".cpp"):
+        cmd = [CXX, *HOST_FLAGS, "-c", src, "-o", obj]
+    else:
+        cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr}")
+        raise RuntimeError(f"{cmd[0]} failed for {src}:\n{r.stderr}")
     return obj
 
 

@@ -1,5 +1,7 @@
 // Token-matrix GEMMs of the ViT encoder/decoder and the 1x1 LIC transforms, on the MFMA core
 // (gemm_core.h).  Entry points and the reference computation each replaces: include/tmae.h.
+#include <stdio.h>
+
 #include "gemm_core.h"
 
 
@@ -238,4 +240,16 @@ extern "C" int tmae_decoder_pred_fwd(const void* x, const void* w, const float* 
                                      int Din, int C, int H, int W, int patch, int dtype, void* stream) {
   if (dtype == TMAE_BF16) return dec_pred_t<bf16>(x, w, bias, imgs, n, L, Din, C, H, W, patch, (hipStream_t)stream);
   return dec_pred_t<float>(x, w, bias, imgs, n, L, Din, C, H, W, patch, (hipStream_t)stream);
+}
+
+// ------------------------------------------------------------------ diagnostics
+extern "C" int tmae_gemm_plan(int M, int N, int K, int batch, int dtype, char* out, int len) {
+  TMAE_REQUIRE(out != nullptr && len > 0 && M >= 0 && N >= 0 && K >= 0 && batch >= 1, "tmae_gemm_plan: bad arguments");
+  const bool bf = dtype == TMAE_BF16;
+  const TileChoice tc = choose_tile(M, N, batch, bf);
+  if (tc.nw == 8 && gemm_knob("TMAE_GEMM_RING", 0))
+    snprintf(out, len, "ring<bf16,%dx%d,8w,BK32x4>", tc.bn, tc.bm);
+  else
+    snprintf(out, len, "glds<%s,%dx%d,%dw,BK%dx2>", bf ? "bf16" : "f32", tc.bn, tc.bm, tc.nw, bf ? 64 : 32);
+  return TMAE_OK;
 }

@@ -80,9 +80,11 @@ template <typename T> struct DenseSrc {
     const int sm = (m / G) * Gs + off + (m % G);
     return {p + (size_t)sm * ld};
   }
-  __device__ const void* addr(const Row& r, int kt, int c) const {
-    const int k = kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC;
+  __device__ const void* addr_k(const Row& r, int k) const {
     return (r.ptr && k < K) ? (const void*)(r.ptr + k) : (const void*)g_tmae_zero_page;
+  }
+  __device__ const void* addr(const Row& r, int kt, int c) const {
+    return addr_k(r, kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC);
   }
   __device__ uint4 load(const Row& r, int kt, int c) const { return *reinterpret_cast<const uint4*>(addr(r, kt, c)); }
 };
@@ -105,7 +107,9 @@ template <typename T> struct ConvSrc {
     return {b * H * W, oy * stride - 1, ox * stride - 1, true};
   }
   __device__ const void* addr(const Row& r, int kt, int c) const {
-    const int k = kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC;
+    return addr_k(r, kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC);
+  }
+  __device__ const void* addr_k(const Row& r, int k) const {
     if (!r.ok || k >= K) return g_tmae_zero_page;
     int tap = (int)((float)k * inv_cin);
     if (tap * Cin > k) --tap;
@@ -335,13 +339,172 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
     int stage = 0;
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) issue(stage ^ 1, kt + 1);
+      if (diag & 8) __builtin_amdgcn_s_setprio(1);
       if (!(diag & 2)) mfma_tile<T, BN, WN, WM, TN, TM>(lds + stage * ROWS * 8, wn, wm, lane, acc);
+      if (diag & 8) __builtin_amdgcn_s_setprio(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       stage ^= 1;
     }
   }
   static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= 2 * ROWS * 128, "epilogue region exceeds the LDS ring");
+  if (!(diag & 1))
+    epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
+                             tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
+}
+
+// ------------------------------------------------------------------ ring kernel (8 waves, bf16)
+// BK = 32 (64-B LDS rows, 4 x 16-B chunks), a 4-slot LDS ring of (BN+BM) x 64 B, up to 4 K-steps of
+// LDS-DMA in flight, and the MFMA fragments register-double-buffered: right after the barrier that
+// certifies step k+1 has landed, every wave issues step k+1's ds_reads and only then runs step k's
+// MFMAs (from registers read one iteration earlier), so the LDS latency hides under the MFMAs
+// instead of draining the pipe at every barrier (the 2-stage kernel above runs its MFMA phase alone
+// at ~60 % of peak, all waves waiting on their first fragments together).  The slot of step k is
+// refilled with step k+4 once every wave holds step k's fragments.  Counted s_waitcnt vmcnt and a
+// raw s_barrier: a __syncthreads fence would drain every DMA in flight.
+// Chunk c of row r sits in slot c ^ (((r >> 3) & 1) << 1): the 16-row x 4-chunk ds_read_b128
+// fragment reads are conflict-free in all four lane groups (exhaustive search over the
+// MI355X_MICROARCH.md lane-group table).
+template <int N>
+__device__ __forceinline__ void wait_vm_barrier() {
+  static_assert(N == 0 || N == 4 || N == 8 || N == 12, "ring depth");
+  if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ int ring_slot(int r, int c) { return c ^ (((r >> 3) & 1) << 1); }
+
+template <int BN, int BM, int WGN, class WS, class XS, class EPI>
+__global__ void __launch_bounds__(512, 1)
+gemm_ring_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
+  constexpr int NW = 8, BK = 32, NS = 4;
+  constexpr int WGM = NW / WGN;
+  constexpr int WN = BN / WGN, WM = BM / WGM;
+  constexpr int TN = WN / 16, TM = WM / 16;
+  constexpr int ROWS = BN + BM;
+  constexpr int PIECES = ROWS / 16 / NW;  // 1-KiB DMA pieces per wave per stage (16 rows x 64 B)
+  constexpr int WP = BN / 16 / NW;        // of which weight pieces
+  constexpr int STAGE = ROWS * 64;        // bytes
+  static_assert(TN >= 1 && TM >= 1 && PIECES == 4 && BN % (16 * NW) == 0 && BM % (16 * NW) == 0, "bad tile");
+  static_assert(TN % 2 == 0, "MFMA halves split over the weight fragments");
+  __shared__ __attribute__((aligned(16))) uint4 lds[NS * STAGE / 16];
+
+  const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
+  ws.batch(b1, b2);
+  xs.batch(b1, b2);
+  epi.batch(b1, b2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave % WGN, wm = wave / WGN;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int nk = (K + BK - 1) / BK;
+  int tn, tm;
+  tile_order(xcd_remap(blockIdx.x, gridDim.x), ntn, ntm, tn, tm);
+
+  // DMA piece p of this wave: rows 16 * (wave + NW p) + (lane >> 2), slot lane & 3
+  const int prow = lane >> 2, pslot = lane & 3;
+  typename WS::Row wrow[WP];
+  typename XS::Row xrow[PIECES - WP];
+  int koff[PIECES];
+#pragma unroll
+  for (int p = 0; p < PIECES; ++p) {
+    const int r = 16 * (wave + NW * p) + prow;  // tile row (weights first)
+    koff[p] = 8 * ring_slot(r, pslot);           // source chunk for this LDS slot
+    if (p < WP) wrow[p] = ws.row(tn * BN + r);
+    else xrow[p - WP] = xs.row(tm * BM + r - BN);
+  }
+  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
+  const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool dma = !(diag & 4);
+  auto issue = [&](int p, int kt) {
+    const unsigned dst = lds_base + (unsigned)(kt & (NS - 1)) * STAGE + (wave_u + NW * p) * 1024u;
+    if (p < WP) glds16(ws.addr_k(wrow[p], kt * BK + koff[p]), dst);
+    else glds16(xs.addr_k(xrow[p - WP], kt * BK + koff[p]), dst);
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  int aoff[TN], boff[TM];  // byte offsets of this lane's fragments inside a stage
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int r = wn * WN + 16 * i + fr;
+    aoff[i] = r * 64 + 16 * ring_slot(r, fq);
+  }
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int r = BN + wm * WM + 16 * j + fr;
+    boff[j] = r * 64 + 16 * ring_slot(r, fq);
+  }
+  bf16x8 a[2][TN], b[2][TM];
+  auto read_frags = [&](int kt, int set) {
+    const char* stage = reinterpret_cast<const char*>(lds) + (kt & (NS - 1)) * STAGE;
+#pragma unroll
+    for (int i = 0; i < TN; ++i) a[set][i] = *reinterpret_cast<const bf16x8*>(stage + aoff[i]);
+#pragma unroll
+    for (int j = 0; j < TM; ++j) b[set][j] = *reinterpret_cast<const bf16x8*>(stage + boff[j]);
+  };
+  auto mfma_half = [&](int set, int i0) {
+#pragma unroll
+    for (int i = i0; i < i0 + TN / 2; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[set][i], b[set][j], acc[i][j], 0, 0, 0);
+  };
+
+  if (nk > 0) {
+    if (dma) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        if (s < nk) {
+#pragma unroll
+          for (int p = 0; p < PIECES; ++p) issue(p, s);
+        }
+    }
+    const int ahead = dma ? min(NS - 1, nk - 1) : 0;  // stages allowed in flight once stage 0 landed
+    if (ahead == 3) wait_vm_barrier<3 * PIECES>();
+    else if (ahead == 2) wait_vm_barrier<2 * PIECES>();
+    else if (ahead == 1) wait_vm_barrier<PIECES>();
+    else wait_vm_barrier<0>();
+    read_frags(0, 0);
+  }
+  // two iterations per loop trip so the fragment sets are compile-time indices
+  auto step = [&](int kt, int cur) {
+    if (kt + 1 < nk) {
+      const int after = dma ? min(kt + NS - 1, nk - 1) - (kt + 1) : 0;
+      if (after >= 2) wait_vm_barrier<2 * PIECES>();
+      else if (after == 1) wait_vm_barrier<PIECES>();
+      else wait_vm_barrier<0>();
+      read_frags(kt + 1, cur ^ 1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (diag & 8) __builtin_amdgcn_s_setprio(1);
+    if (!(diag & 2)) mfma_half(cur, 0);
+    if (diag & 8) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (dma && kt + NS < nk) {
+#pragma unroll
+      for (int p = 0; p < PIECES; ++p) issue(p, kt + NS);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (diag & 8) __builtin_amdgcn_s_setprio(1);
+    if (!(diag & 2)) mfma_half(cur, TN / 2);
+    if (diag & 8) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, 0);
+    step(kt + 1, 1);
+  }
+  if (kt < nk) step(kt, 0);
+  wait_vm_barrier<0>();  // every wave is done with the ring before it becomes the epilogue buffer
+  static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= NS * STAGE, "epilogue region exceeds the LDS ring");
   if (!(diag & 1))
     epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
                              tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
@@ -467,6 +630,16 @@ static int launch_one(const char* name, const WS& ws, const XS& xs, const EPI& e
   TMAE_LAUNCH_CHECK(name);
 }
 
+template <int BN, int BM, int WGN, class WS, class XS, class EPI>
+static int launch_ring(const char* name, const WS& ws, const XS& xs, const EPI& epi, int M, int N, int K, int n1,
+                       int n2, hipStream_t st) {
+  const int tiles = ceil_div(N, BN) * ceil_div(M, BM);
+  if (tiles == 0 || n1 * n2 == 0) return TMAE_OK;
+  hipLaunchKernelGGL((gemm_ring_kernel<BN, BM, WGN, WS, XS, EPI>), dim3(tiles, n1 * n2), dim3(512), 0, st, ws, xs, epi,
+                     M, N, K, n2, gemm_knob("TMAE_GEMM_DIAG", 0));
+  TMAE_LAUNCH_CHECK(name);
+}
+
 template <bool GLDS, typename T, class XS, class EPI>
 static int launch_gemm(const char* name, const T* w, long long ws1, long long ws2, int N, int K, const XS& xs,
                        const EPI& epi, int M, int n1 = 1, int n2 = 1, hipStream_t st = 0) {
@@ -474,7 +647,10 @@ static int launch_gemm(const char* name, const T* w, long long ws1, long long ws
   // the 8-wave tile is built for the bf16 glds path only (the f32 path is the parity path)
   const TileChoice tc = choose_tile(M, N, n1 * n2, GLDS && sizeof(T) == 2);
   if constexpr (GLDS && sizeof(T) == 2) {
-    if (tc.nw == 8) return launch_one<GLDS, T, 256, 256, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
+    if (tc.nw == 8) {
+      if (gemm_knob("TMAE_GEMM_RING", 0)) return launch_ring<256, 256, 2>(name, ws, xs, epi, M, N, K, n1, n2, st);
+      return launch_one<GLDS, T, 256, 256, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
+    }
   }
   if (tc.bn == 128) return launch_one<GLDS, T, 128, 128, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
   if (tc.bn == 64 && tc.bm == 128) return launch_one<GLDS, T, 64, 128, 1, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);

@@ -16,7 +16,7 @@ from ._lib import ACT_GELU, ACT_NONE, TMAE_BF16, TMAE_F32, ConvArgs, EBParams
 __all__ = [
     "ids_shuffle", "layernorm", "linear", "linear_residual", "patch_embed", "cls_rows", "mha", "decoder_embed",
     "mask_rows", "decoder_pred", "conv3x3", "gc_slices", "eb_likelihood", "eb_aux_loss",
-    "gc_likelihood", "nhwc_to_nchw", "bpp", "dtype_code", "TMAE_F32", "TMAE_BF16", "ACT_NONE", "ACT_GELU",
+    "gc_likelihood", "nhwc_to_nchw", "bpp", "gemm_plan", "dtype_code", "TMAE_F32", "TMAE_BF16", "ACT_NONE", "ACT_GELU",
 ]
 
 
@@ -47,6 +47,13 @@ def dtype_code(dt: torch.dtype) -> int:
     if dt == torch.bfloat16:
         return TMAE_BF16
     raise ValueError(f"unsupported compute dtype {dt}")
+
+
+def gemm_plan(M: int, N: int, K: int, dtype: torch.dtype, batch: int = 1) -> str:
+    """name of the MFMA GEMM variant the library launches for this problem (no device work)"""
+    buf = ctypes.create_string_buffer(96)
+    _lib.call("tmae_gemm_plan", M, N, K, batch, dtype_code(dtype), buf, len(buf))
+    return buf.value.decode()
 
 
 # --------------------------------------------------------------------------------------- masking
