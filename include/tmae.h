@@ -154,6 +154,43 @@ int tmae_bpp_sum(const float* y_lik, long long ny, const float* z_lik, long long
 /* layout helper: NHWC (channel stride ldx) -> NCHW */
 int tmae_nhwc_to_nchw(const float* x, int ldx, float* y, int n, int C, int HW, void* stream);
 
+/* ---------------------------------------------------------------- entropy coding, device side
+ * (MCM.compress / decompress, MCM.py:805-968; compressai semantics restated, see rans.cpp) */
+
+/* MCM.compress slice step (MCM.py:864-872): tmae_gc_slices_fwd's eval outputs (y_hat, likelihood) plus
+ * symbols = round(y - mu) and indexes = build_indexes(sigma) against scale_table[nscale], both written in
+ * the coder's order [slice][image][channel][pixel] starting at slice 0 of this launch. */
+int tmae_gc_slices_code(const float* y, int ldy, int yoff, const float* mu, const float* sigma, long long ms_stride,
+                        int ld_ms, float* lik, int Mtot, void* yhat, int yhat_dtype, int ld_yhat, float* yhat32,
+                        int ld32, int n, int HW, int nslices, int sw, int* symbols, int* indexes,
+                        const float* scale_table, int nscale, void* stream);
+
+/* GaussianConditional.build_indexes (MCM.py:938) for nslices slices of sigma rows (layout as above) */
+int tmae_gc_indexes(const float* sigma, long long ms_stride, int ld_ms, int n, int HW, int nslices, int sw,
+                    const float* scale_table, int nscale, float scale_bound, int* indexes, void* stream);
+
+/* GaussianConditional.dequantize (MCM.py:946): y_hat = symbols + mu into channels yoff.. of y_hat rows */
+int tmae_gc_dequantize(const int* symbols, const float* mu, long long ms_stride, int ld_ms, int n, int HW,
+                       int nslices, int sw, int yoff, void* yhat, int yhat_dtype, int ld_yhat, float* yhat32, int ld32,
+                       void* stream);
+
+/* GaussianConditional.update (update_scale_table): pmf[n][max_length], tail[n] for the CDF builder */
+int tmae_gc_pmf(const float* scale_table, const int* pmf_center, int n, int max_length, float* pmf, float* tail,
+                void* stream);
+
+/* EntropyBottleneck.update: pmf[C][max_length] at pmf_start[c] + j, tail[C] */
+int tmae_eb_pmf(const tmae_eb_params* params, float* table, const float* pmf_start, int C, int max_length, float* pmf,
+                float* tail, void* stream);
+
+/* EntropyBottleneck.compress / decompress value maps: symbols NCHW int32 <-> z / z_hat NHWC */
+int tmae_eb_symbols(const float* z, const tmae_eb_params* params, float* table, int n, int C, int HW, int* symbols,
+                    void* stream);
+int tmae_eb_dequantize(const int* symbols, const tmae_eb_params* params, float* table, int n, int C, int HW, void* zhat,
+                       int zhat_dtype, void* stream);
+
+/* inverse[b][perm[b][j]] = j (ids_shuffle from ids_restore for MCM.decompress) */
+int tmae_invert_permutation(const int64_t* perm, int64_t* inverse, int n, int L, void* stream);
+
 /* ---------------------------------------------------------------- entropy coding (host, no device work)
  * compressai 1.2.4's coder restated (csrc/rans.cpp; not vendored in the reference): 64-bit rANS, 16-bit
  * precision, bypass-escaped tails.  CDF tables are int32 [ncdf][cdf_stride] rows with cdf_sizes[c] valid

@@ -64,6 +64,14 @@ SIGNATURES = {
     "tmae_nhwc_to_nchw": [P, I, P, I, I, I, P],
     "tmae_bpp_sum": [P, LL, P, LL, P, P, ctypes.c_double, P],
     "tmae_gemm_plan": [I, I, I, I, I, ctypes.c_char_p, I],
+    "tmae_gc_slices_code": [P, I, I, P, P, LL, I, P, I, P, I, I, P, I, I, I, I, I, P, P, P, I, P],
+    "tmae_gc_indexes": [P, LL, I, I, I, I, I, P, I, F, P, P],
+    "tmae_gc_dequantize": [P, P, LL, I, I, I, I, I, I, P, I, I, P, I, P],
+    "tmae_gc_pmf": [P, P, I, I, P, P, P],
+    "tmae_eb_pmf": [ctypes.POINTER(EBParams), P, P, I, I, P, P, P],
+    "tmae_eb_symbols": [P, ctypes.POINTER(EBParams), P, I, I, I, P, P],
+    "tmae_eb_dequantize": [P, ctypes.POINTER(EBParams), P, I, I, I, P, I, P],
+    "tmae_invert_permutation": [P, P, I, I, P],
     "tmae_pmf_to_quantized_cdf": [P, I, I, P],
     "tmae_rans_encoder_create": [ctypes.POINTER(ctypes.c_void_p)],
     "tmae_rans_encode_with_indexes": [P, P, P, LL, P, I, P, P, I],

@@ -157,12 +157,13 @@ extern "C" int tmae_conv3x3(const tmae_conv_args* args, int dtype, void* stream)
 // for `nslices` consecutive slices of width sw, and y_hat = round(y - mu) + mu (quantize_ste forward
 // value, MCM.py:767-776).  Element (pixel m, slice j, channel c) of the latent channel
 // ch = yoff + j*sw + c; mu/sigma of slice j at mu[j*ms_stride + m*ld_ms + c].
-template <typename YT>
+template <typename YT, bool CODE>
 __global__ void __launch_bounds__(256)
 gc_slices_kernel(const float* __restrict__ y, int ldy, int yoff, const float* __restrict__ mu,
                  const float* __restrict__ sigma, long long ms_stride, int ld_ms, const float* __restrict__ noise,
                  float* __restrict__ lik, int Mtot, YT* __restrict__ yhat, int ld_yhat, float* __restrict__ yhat32,
-                 int ld32, int HW, int nslices, int sw, int total) {
+                 int ld32, int n, int HW, int nslices, int sw, int total, int* __restrict__ sym,
+                 int* __restrict__ idx, const float* __restrict__ scale_table, int nscale) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int per_pix = nslices * sw;
@@ -174,7 +175,8 @@ gc_slices_kernel(const float* __restrict__ y, int ldy, int yoff, const float* __
   const float mv = mu[j * ms_stride + (size_t)m * ld_ms + c];
   const float sv = sigma[j * ms_stride + (size_t)m * ld_ms + c];
   const size_t nchw = ((size_t)b * Mtot + ch) * HW + pix;
-  const float q = rintf(yv - mv) + mv;
+  const float qi = rintf(yv - mv);
+  const float q = qi + mv;
   const float xt = noise ? yv + noise[nchw] : q;
   const float s = fmaxf(sv, 0.11f);
   const float val = fabsf(xt - mv);
@@ -184,20 +186,51 @@ gc_slices_kernel(const float* __restrict__ y, int ldy, int yoff, const float* __
   lik[nchw] = fmaxf(up - lo, 1e-9f);
   yhat[(size_t)m * ld_yhat + ch] = to_out<YT>(q);
   if (yhat32) yhat32[(size_t)m * ld32 + ch] = q;
+  if constexpr (CODE) {
+    // MCM.compress (MCM.py:867-872): symbols = round(y - mu) (quantize "symbols"), indexes =
+    // GaussianConditional.build_indexes(sigma); reference order per slice = [N][sw][H][W], slice-major
+    const size_t pos = (size_t)j * n * sw * HW + ((size_t)b * sw + c) * HW + pix;
+    sym[pos] = (int)qi;
+    int id = nscale - 1;
+    for (int t = 0; t < nscale - 1; ++t) id -= (s <= scale_table[t]) ? 1 : 0;
+    idx[pos] = id;
+  }
+}
+
+template <bool CODE>
+static int gc_slices_launch(const float* y, int ldy, int yoff, const float* mu, const float* sigma,
+                            long long ms_stride, int ld_ms, const float* noise, float* lik, int Mtot, void* yhat,
+                            int yhat_dtype, int ld_yhat, float* yhat32, int ld32, int n, int HW, int nslices, int sw,
+                            int* sym, int* idx, const float* scale_table, int nscale, hipStream_t st) {
+  const int total = n * HW * nslices * sw;
+  if (total <= 0) return TMAE_OK;
+  const dim3 grid(ceil_div(total, 256));
+  if (yhat_dtype == TMAE_BF16)
+    hipLaunchKernelGGL((gc_slices_kernel<bf16, CODE>), grid, dim3(256), 0, st, y, ldy, yoff, mu, sigma, ms_stride,
+                       ld_ms, noise, lik, Mtot, (bf16*)yhat, ld_yhat, yhat32, ld32, n, HW, nslices, sw, total, sym, idx,
+                       scale_table, nscale);
+  else
+    hipLaunchKernelGGL((gc_slices_kernel<float, CODE>), grid, dim3(256), 0, st, y, ldy, yoff, mu, sigma, ms_stride,
+                       ld_ms, noise, lik, Mtot, (float*)yhat, ld_yhat, yhat32, ld32, n, HW, nslices, sw, total, sym,
+                       idx, scale_table, nscale);
+  TMAE_LAUNCH_CHECK(CODE ? "tmae_gc_slices_code" : "tmae_gc_slices_fwd");
 }
 
 extern "C" int tmae_gc_slices_fwd(const float* y, int ldy, int yoff, const float* mu, const float* sigma,
                                   long long ms_stride, int ld_ms, const float* noise, float* lik, int Mtot,
                                   void* yhat, int yhat_dtype, int ld_yhat, float* yhat32, int ld32, int n, int HW,
                                   int nslices, int sw, void* stream) {
-  const int total = n * HW * nslices * sw;
-  if (total <= 0) return TMAE_OK;
-  const dim3 grid(ceil_div(total, 256));
-  if (yhat_dtype == TMAE_BF16)
-    hipLaunchKernelGGL(gc_slices_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, y, ldy, yoff, mu, sigma,
-                       ms_stride, ld_ms, noise, lik, Mtot, (bf16*)yhat, ld_yhat, yhat32, ld32, HW, nslices, sw, total);
-  else
-    hipLaunchKernelGGL(gc_slices_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, y, ldy, yoff, mu, sigma,
-                       ms_stride, ld_ms, noise, lik, Mtot, (float*)yhat, ld_yhat, yhat32, ld32, HW, nslices, sw, total);
-  TMAE_LAUNCH_CHECK("tmae_gc_slices_fwd");
+  return gc_slices_launch<false>(y, ldy, yoff, mu, sigma, ms_stride, ld_ms, noise, lik, Mtot, yhat, yhat_dtype,
+                                 ld_yhat, yhat32, ld32, n, HW, nslices, sw, nullptr, nullptr, nullptr, 0,
+                                 (hipStream_t)stream);
+}
+
+extern "C" int tmae_gc_slices_code(const float* y, int ldy, int yoff, const float* mu, const float* sigma,
+                                   long long ms_stride, int ld_ms, float* lik, int Mtot, void* yhat, int yhat_dtype,
+                                   int ld_yhat, float* yhat32, int ld32, int n, int HW, int nslices, int sw,
+                                   int* symbols, int* indexes, const float* scale_table, int nscale, void* stream) {
+  TMAE_REQUIRE(symbols && indexes && scale_table && nscale >= 1, "tmae_gc_slices_code: symbols/indexes/scale_table required");
+  return gc_slices_launch<true>(y, ldy, yoff, mu, sigma, ms_stride, ld_ms, nullptr, lik, Mtot, yhat, yhat_dtype,
+                                ld_yhat, yhat32, ld32, n, HW, nslices, sw, symbols, indexes, scale_table, nscale,
+                                (hipStream_t)stream);
 }

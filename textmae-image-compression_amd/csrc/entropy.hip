@@ -153,3 +153,86 @@ extern "C" int tmae_gc_likelihood_fwd(const float* x, const float* scales, const
                      means, noise, x_tilde, lik, total, scale_bound);
   TMAE_LAUNCH_CHECK("tmae_gc_likelihood_fwd");
 }
+
+// ------------------------------------------------------------------ entropy-coding support (MCM.compress / decompress)
+// EntropyBottleneck.update (compressai; called through CompressionModel.update, testing.py:223):
+// pmf[c][j] = |sigmoid(s f(x + 1/2)) - sigmoid(s f(x - 1/2))| at x = pmf_start[c] + j, s = -sign(lower + upper),
+// tail[c] = sigmoid(lower[c][0]) + sigmoid(-upper[c][max_length - 1])  (upstream uses the LAST sample of the
+// padded range for every channel, not of the channel's own length; restated as is).
+__global__ void __launch_bounds__(256)
+eb_pmf_kernel(const float* __restrict__ tab, const float* __restrict__ pmf_start, int C, int max_length,
+              float* __restrict__ pmf, float* __restrict__ tail) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C * max_length) return;
+  const int c = i / max_length, j = i - c * max_length;
+  const float* t = tab + (size_t)c * EB_PACK;
+  const float x = (float)j + pmf_start[c];
+  const float lower = eb_logits(t, x - 0.5f);
+  const float upper = eb_logits(t, x + 0.5f);
+  const float sum = lower + upper;
+  const float sgn = sum > 0.0f ? -1.0f : (sum < 0.0f ? 1.0f : -0.0f);
+  pmf[i] = fabsf(sigmoid_t(sgn * upper) - sigmoid_t(sgn * lower));
+  if (j == 0) {
+    const float xl = (float)(max_length - 1) + pmf_start[c];
+    tail[c] = sigmoid_t(lower) + sigmoid_t(-eb_logits(t, xl + 0.5f));
+  }
+}
+
+extern "C" int tmae_eb_pmf(const tmae_eb_params* params, float* table, const float* pmf_start, int C, int max_length,
+                           float* pmf, float* tail, void* stream) {
+  TMAE_REQUIRE(params && table && pmf_start && pmf && tail && C > 0 && max_length > 0, "tmae_eb_pmf: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, st, *params, table, C);
+  hipLaunchKernelGGL(eb_pmf_kernel, dim3(ceil_div(C * max_length, 256)), dim3(256), 0, st, table, pmf_start, C,
+                     max_length, pmf, tail);
+  TMAE_LAUNCH_CHECK("tmae_eb_pmf");
+}
+
+// EntropyBottleneck.compress: symbols = round(z - median) (quantize "symbols"); z NHWC [n*HW][C],
+// symbols NCHW [n][C][HW] (compressai codes symbols[i].reshape(-1) per image, channel-major)
+__global__ void __launch_bounds__(256)
+eb_symbols_kernel(const float* __restrict__ z, const float* __restrict__ tab, int C, int HW, int total,
+                  int* __restrict__ sym) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = i % C, m = i / C;
+  const int b = m / HW, pix = m - b * HW;
+  sym[((size_t)b * C + c) * HW + pix] = (int)rintf(z[i] - tab[(size_t)c * EB_PACK + 58]);
+}
+
+// EntropyBottleneck.decompress: z_hat = symbols + median (dequantize), symbols NCHW -> z_hat NHWC
+__global__ void __launch_bounds__(256)
+eb_dequantize_kernel(const int* __restrict__ sym, const float* __restrict__ tab, int C, int HW, int total,
+                     void* __restrict__ zhat, int zhat_bf16) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = i % C, m = i / C;
+  const int b = m / HW, pix = m - b * HW;
+  const float v = (float)sym[((size_t)b * C + c) * HW + pix] + tab[(size_t)c * EB_PACK + 58];
+  if (zhat_bf16) ((bf16*)zhat)[i] = (bf16)v;
+  else ((float*)zhat)[i] = v;
+}
+
+extern "C" int tmae_eb_symbols(const float* z, const tmae_eb_params* params, float* table, int n, int C, int HW,
+                               int* symbols, void* stream) {
+  TMAE_REQUIRE(z && params && table && symbols, "tmae_eb_symbols: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, st, *params, table, C);
+  const int total = n * HW * C;
+  if (total > 0)
+    hipLaunchKernelGGL(eb_symbols_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, z, table, C, HW, total,
+                       symbols);
+  TMAE_LAUNCH_CHECK("tmae_eb_symbols");
+}
+
+extern "C" int tmae_eb_dequantize(const int* symbols, const tmae_eb_params* params, float* table, int n, int C, int HW,
+                                  void* zhat, int zhat_dtype, void* stream) {
+  TMAE_REQUIRE(symbols && params && table && zhat, "tmae_eb_dequantize: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, st, *params, table, C);
+  const int total = n * HW * C;
+  if (total > 0)
+    hipLaunchKernelGGL(eb_dequantize_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, symbols, table, C, HW,
+                       total, zhat, zhat_dtype == TMAE_BF16);
+  TMAE_LAUNCH_CHECK("tmae_eb_dequantize");
+}

@@ -52,6 +52,62 @@ class EntropyModel(nn.Module):
     def cdf_length(self):
         return self._cdf_length
 
+    def _check_cdf(self):
+        if self._offset.numel() == 0 or self._quantized_cdf.numel() == 0 or self._cdf_length.numel() == 0:
+            raise ValueError("Uninitialized CDFs. Run update() first")
+
+    def _pmf_to_cdf(self, pmf, tail_mass, pmf_length, max_length):
+        """EntropyModel._pmf_to_cdf: per row, pmf[:len] + tail -> quantized CDF (host C++ builder)"""
+        from .coder import pmf_to_quantized_cdf
+
+        pmf_h = pmf.detach().float().cpu().numpy()
+        tail_h = tail_mass.detach().float().reshape(-1).cpu().numpy()
+        lengths = pmf_length.detach().reshape(-1).cpu().tolist()
+        cdf = torch.zeros((len(lengths), max_length + 2), dtype=torch.int32)
+        for i, n in enumerate(lengths):
+            prob = np.concatenate([pmf_h[i, :n], tail_h[i:i + 1]]).astype(np.float32)
+            row = pmf_to_quantized_cdf(prob, self.entropy_coder_precision)
+            cdf[i, :len(row)] = torch.tensor(row, dtype=torch.int32)
+        return cdf.to(pmf.device)
+
+    def host_tables(self):
+        """(cdf int32 [n][len], cdf_length int32 [n], offset int32 [n]) as numpy, cached until the buffers change"""
+        self._check_cdf()
+        key = tuple((t.data_ptr(), t._version) for t in (self._quantized_cdf, self._cdf_length, self._offset))
+        cache = getattr(self, "_host_tables_cache", None)
+        if cache is None or cache[0] != key:
+            tabs = tuple(np.ascontiguousarray(t.detach().cpu().numpy().astype(np.int32))
+                         for t in (self._quantized_cdf, self._cdf_length.reshape(-1), self._offset.reshape(-1)))
+            cache = (key, tabs)
+            self._host_tables_cache = cache
+        return cache[1]
+
+    @staticmethod
+    def quantize_symbols(inputs, means=None):
+        """quantize(inputs, "symbols", means): round(inputs - means).int() (module-level convenience)"""
+        x = inputs - means if means is not None else inputs
+        return torch.round(x).int()
+
+    @staticmethod
+    def dequantize(inputs, means=None, dtype=torch.float):
+        outputs = inputs.type(dtype)
+        return outputs + means if means is not None else outputs
+
+    def _code(self, symbols, indexes):
+        """RansEncoder.encode_with_indexes over one image's flattened symbols"""
+        from .coder import RansEncoder
+
+        cdf, sizes, offsets = self.host_tables()
+        return RansEncoder().encode_with_indexes(symbols, indexes, cdf, sizes, offsets)
+
+    def _decode(self, string, indexes):
+        from .coder import RansDecoder
+
+        cdf, sizes, offsets = self.host_tables()
+        dec = RansDecoder()
+        dec.set_stream(string)
+        return dec.decode_stream_array(indexes, cdf, sizes, offsets)
+
 
 class EntropyBottleneck(EntropyModel):
     """Factorized prior: per-channel monotone MLP 1-3-3-3-3-1 density model."""
@@ -104,6 +160,48 @@ class EntropyBottleneck(EntropyModel):
     def loss(self):
         return ops.eb_aux_loss(self)
 
+    @torch.no_grad()
+    def update(self, force=False):
+        """EntropyBottleneck.update: per-channel integer support around the median, pmf of every
+        integer (device kernel), quantized CDF with the tail mass as the escape bin."""
+        if self._offset.numel() > 0 and not force:
+            return False
+        medians = self.quantiles[:, 0, 1]
+        minima = torch.clamp(torch.ceil(medians - self.quantiles[:, 0, 0]).int(), min=0)
+        maxima = torch.clamp(torch.ceil(self.quantiles[:, 0, 2] - medians).int(), min=0)
+        self._offset = -minima
+        pmf_start = medians - minima
+        pmf_length = maxima + minima + 1
+        max_length = int(pmf_length.max().item())
+        pmf, tail = ops.eb_pmf(self, pmf_start, max_length)
+        self._quantized_cdf = self._pmf_to_cdf(pmf, tail, pmf_length, max_length)
+        self._cdf_length = pmf_length + 2
+        return True
+
+    def _channel_indexes(self, hw):
+        return np.repeat(np.arange(self.channels, dtype=np.int32), hw)
+
+    @torch.no_grad()
+    def compress(self, x):
+        """x NCHW -> one rANS string per image (symbols round(x - median), channel-indexed CDFs)"""
+        n, c, h, w = x.shape
+        z = x.float().permute(0, 2, 3, 1).contiguous()
+        sym = ops.eb_symbols(self, z, n, c, h * w).cpu().numpy()
+        idx = self._channel_indexes(h * w)
+        return [self._code(sym[i].reshape(-1), idx) for i in range(n)]
+
+    @torch.no_grad()
+    def decompress(self, strings, size):
+        """strings -> z_hat NCHW f32 (symbols + median)"""
+        h, w = int(size[0]), int(size[1])
+        n, c = len(strings), self.channels
+        idx = self._channel_indexes(h * w)
+        sym = np.stack([self._decode(s, idx) for s in strings]).astype(np.int32)
+        dev = self.quantiles.device
+        zhat = torch.empty((n * h * w, c), dtype=torch.float32, device=dev)
+        ops.eb_dequantize(self, torch.from_numpy(sym).to(dev), n, c, h * w, zhat)
+        return zhat.view(n, h, w, c).permute(0, 3, 1, 2).contiguous()
+
 
 class GaussianConditional(EntropyModel):
     def __init__(self, scale_table, *args, scale_bound=0.11, tail_mass=1e-9, **kwargs):
@@ -123,6 +221,60 @@ class GaussianConditional(EntropyModel):
         bound = float(self.scale_bound) if self.scale_bound is not None else 0.0
         return ops.gc_likelihood(inputs.float(), scales.float(), None if means is None else means.float(),
                                  noise if training else None, bound)
+
+    @staticmethod
+    def _prepare_scale_table(scale_table):
+        return torch.Tensor(tuple(float(s) for s in scale_table))
+
+    @staticmethod
+    def _standardized_quantile(quantile):
+        from scipy.stats import norm
+
+        return float(norm.ppf(quantile))
+
+    @torch.no_grad()
+    def update_scale_table(self, scale_table, force=False):
+        if self._offset.numel() > 0 and not force:
+            return False
+        device = self.scale_table.device
+        self.scale_table = self._prepare_scale_table(scale_table).to(device)
+        self.update()
+        return True
+
+    @torch.no_grad()
+    def update(self):
+        """GaussianConditional.update: one discretised-Gaussian CDF per scale-table entry, support
+        +-ceil(scale * Phi^-1(1 - tail_mass / 2)) (pmf on the device, CDF builder on the host)."""
+        multiplier = -self._standardized_quantile(self.tail_mass / 2)
+        pmf_center = torch.ceil(self.scale_table * multiplier).int()
+        pmf_length = 2 * pmf_center + 1
+        max_length = int(torch.max(pmf_length).item())
+        pmf, tail = ops.gc_pmf(self.scale_table.float(), pmf_center, max_length)
+        self._quantized_cdf = self._pmf_to_cdf(pmf, tail, pmf_length, max_length)
+        self._offset = -pmf_center
+        self._cdf_length = pmf_length + 2
+
+    def build_indexes(self, scales):
+        """index of the smallest table scale >= max(scales, bound) (module-level convenience; MCM.compress
+        computes indexes inside the fused slice kernel)"""
+        scales = self.lower_bound_scale(scales)
+        indexes = scales.new_full(scales.size(), len(self.scale_table) - 1).int()
+        for s in self.scale_table[:-1]:
+            indexes -= (scales <= s).int()
+        return indexes
+
+    @torch.no_grad()
+    def compress(self, inputs, indexes, means=None):
+        sym = self.quantize_symbols(inputs, means).cpu().numpy().reshape(inputs.shape[0], -1)
+        idx = indexes.int().cpu().numpy().reshape(inputs.shape[0], -1)
+        return [self._code(sym[i], idx[i]) for i in range(sym.shape[0])]
+
+    @torch.no_grad()
+    def decompress(self, strings, indexes, dtype=torch.float, means=None):
+        idx = indexes.int().cpu().numpy().reshape(len(strings), -1)
+        out = torch.from_numpy(np.stack([self._decode(s, idx[i]) for i, s in enumerate(strings)]))
+        out = out.reshape(indexes.shape).to(indexes.device)
+        return self.dequantize(out, means, dtype)
 
 
 def get_scale_table(min_=0.11, max_=256, levels=64):
@@ -152,6 +304,18 @@ class CompressionModel(nn.Module):
 
     def aux_loss(self):
         return sum(m.loss() for m in self.modules() if isinstance(m, EntropyBottleneck))
+
+    def update(self, scale_table=None, force=False):
+        """CompressionModel.update (testing.py:223): build the CDF tables of every entropy model"""
+        if scale_table is None:
+            scale_table = get_scale_table()
+        updated = False
+        for _, module in self.named_modules():
+            if isinstance(module, EntropyBottleneck):
+                updated |= module.update(force=force)
+            if isinstance(module, GaussianConditional):
+                updated |= module.update_scale_table(scale_table, force=force)
+        return updated
 
     def load_state_dict(self, state_dict, strict=True):
         for name, module in self.named_modules():

@@ -16,6 +16,7 @@ from __future__ import annotations
 
 from functools import partial
 
+import numpy as np
 import torch
 import torch.nn as nn
 
@@ -213,10 +214,30 @@ class MCM(CompressionModel):
         return self.entropy_bottleneck.loss()
 
     def compress(self, imgs, total_scores):
-        raise NotImplementedError("MCM.compress: entropy coding (rANS) is the next §8f row, not in this build")
+        """MCM.compress (MCM.py:805-894) -> {"string": [[y_string], z_strings], "shape", "ids_restore"}.
+        Needs the CDF tables: call update(force=True) first (testing.py:223), as with compressai."""
+        if not imgs.is_cuda:
+            raise ValueError("MCM.compress runs on the MI355X kernels: move the model and inputs to the GPU")
+        self.entropy_bottleneck._check_cdf()
+        self.gaussian_conditional._check_cdf()
+        with torch.no_grad():
+            ex = self._executor(imgs.shape[0], imgs.device)
+            return ex.compress(imgs, total_scores)
 
     def decompress(self, strings, shape, ids_restore=None):
-        raise NotImplementedError("MCM.decompress: entropy coding (rANS) is the next §8f row, not in this build")
+        """MCM.decompress (MCM.py:896-968) -> {"x_hat"}.  Batch = number of z strings; the reference's
+        reshape(1, ...) at MCM.py:944 limits it to one image, this handles any batch the y string holds."""
+        assert isinstance(strings, list) and len(strings) == 2
+        if ids_restore is None:
+            raise ValueError("MCM.decompress needs ids_restore (the decoder unshuffles by it, MCM.py:667-669)")
+        self.entropy_bottleneck._check_cdf()
+        self.gaussian_conditional._check_cdf()
+        dev = next(self.parameters()).device
+        if dev.type != "cuda":
+            raise ValueError("MCM.decompress runs on the MI355X kernels: move the model to the GPU")
+        with torch.no_grad():
+            ex = self._executor(len(strings[1]), dev)
+            return {"x_hat": ex.decompress(strings, shape, ids_restore)}
 
 
 def _interleave(layers):
@@ -389,14 +410,16 @@ class _Executor:
         self.w_dp = cast(m.decoder_pred.weight)
 
     # ------------------------------------------------------------------ forward
-    def run(self, imgs, scores, training, noise):
-        m, dt, B = self.m, self.dtype, self.batch
-        E, Dd, M, N, S = m.encoder_embed_dim, m.decoder_embed_dim, m.latent_depth, m.hyperprior_depth, m.num_slices
-        K, L, P, g, hz = m.num_keep_patches, self.L, self.P, self.g, self.hz
-        Te, Td = K + 1, L + 1
+    def _check_imgs(self, imgs):
         imgs = imgs.float().contiguous()
-        if imgs.shape[1:] != (m.encoder_embed.proj.in_channels, self.img, self.img):
+        if imgs.shape[1:] != (self.m.encoder_embed.proj.in_channels, self.img, self.img):
             raise ValueError(f"Input image size {tuple(imgs.shape[2:])} doesn't match model ({self.img})")
+        return imgs
+
+    def run(self, imgs, scores, training, noise):
+        m, B = self.m, self.batch
+        M, N, g, hz = m.latent_depth, m.hyperprior_depth, self.g, self.hz
+        imgs = self._check_imgs(imgs)
         if training:
             if noise is not None:
                 z_noise, y_noise = (t.float().contiguous() for t in noise)
@@ -406,6 +429,76 @@ class _Executor:
         else:
             z_noise = y_noise = None
 
+        shuf, rest = self._front(imgs, scores)
+
+        # ---- entropy bottleneck + z_hat (MCM.py:741-744)
+        ops.eb_likelihood(m.entropy_bottleneck, self.Z, B, N, hz * hz, noise=z_noise, lik=self.ZLIK, zhat=self.ZHAT,
+                          table=self.eb_table)
+
+        # ---- h_s (MCM.py:747-748)
+        self._h_s(self.hss_w, self.LS)
+        self._h_s(self.hsm_w, self.LM)
+
+        # ---- slice loop (MCM.py:751-787)
+        self._slices(self._gc_forward(y_noise))
+
+        x_hat = self._back(shuf, imgs.shape[1])
+        return {"x_hat": x_hat, "y": self.YLIK.clone(), "z": self.ZLIK.clone(), "ids_restore": rest,
+                "ids_shuffle": shuf}
+
+    # ------------------------------------------------------------------ compress / decompress
+    def compress(self, imgs, scores):
+        """MCM.compress (MCM.py:805-894): the eval forward's analysis path with symbol/index outputs, then
+        the host rANS coder: one z string per image, ONE y string for the whole batch (slice-major)."""
+        from .coder import BufferedRansEncoder
+
+        m, B = self.m, self.batch
+        N, S, hz, sw, HW = m.hyperprior_depth, m.num_slices, self.hz, self.sw, self.g * self.g
+        eb, gc = m.entropy_bottleneck, m.gaussian_conditional
+        imgs = self._check_imgs(imgs)
+        shuf, rest = self._front(imgs, scores)
+        # z: symbols round(z - median); z_hat = symbols + median (= EB.decompress of its own strings)
+        ops.eb_likelihood(eb, self.Z, B, N, hz * hz, lik=self.ZLIK, zhat=self.ZHAT, table=self.eb_table)
+        zsym = ops.eb_symbols(eb, self.Z, B, N, hz * hz, table=self.eb_table)
+        self._h_s(self.hss_w, self.LS)
+        self._h_s(self.hsm_w, self.LM)
+        sym = torch.empty(S * B * sw * HW, dtype=torch.int32, device=self.device)
+        idx = torch.empty_like(sym)
+        self._slices(self._gc_compress(sym, idx))
+        zsym_h, sym_h, idx_h = zsym.cpu().numpy(), sym.cpu().numpy(), idx.cpu().numpy()
+        self.last_streams = {"z_symbols": zsym_h, "y_symbols": sym_h, "y_indexes": idx_h}  # rate diagnostics
+        zidx = eb._channel_indexes(hz * hz)
+        z_strings = [eb._code(zsym_h[b].reshape(-1), zidx) for b in range(B)]
+        enc = BufferedRansEncoder()
+        enc.encode_with_indexes(sym_h, idx_h, *gc.host_tables())
+        return {"string": [[enc.flush()], z_strings], "shape": torch.Size([hz, hz]), "ids_restore": rest}
+
+    def decompress(self, strings, shape, ids_restore):
+        """MCM.decompress (MCM.py:896-968): z strings -> z_hat -> h_s -> slice loop decoding each slice's
+        symbols from the y string with indexes built on the device -> g_s -> decoder."""
+        from .coder import RansDecoder
+
+        m, B = self.m, self.batch
+        N, hz = m.hyperprior_depth, self.hz
+        eb = m.entropy_bottleneck
+        if tuple(int(v) for v in shape) != (hz, hz):
+            raise ValueError(f"shape {tuple(shape)} does not match this model's z grid ({hz}, {hz})")
+        zidx = eb._channel_indexes(hz * hz)
+        zsym = np.stack([eb._decode(s, zidx) for s in strings[1]]).astype(np.int32)
+        ops.eb_dequantize(eb, torch.from_numpy(zsym).to(self.device), B, N, hz * hz, self.ZHAT, table=self.eb_table)
+        self._h_s(self.hss_w, self.LS)
+        self._h_s(self.hsm_w, self.LM)
+        decoder = RansDecoder()
+        decoder.set_stream(strings[0][0])
+        self._slices(self._gc_decompress(decoder))
+        shuf = ops.invert_permutation(ids_restore.to(self.device))
+        return self._back(shuf, m.encoder_embed.proj.in_channels)
+
+    def _front(self, imgs, scores):
+        """encoder + g_a + h_a (MCM.py:590-634, 729-739): tokens -> Y32/YT -> Z; returns (ids_shuffle, ids_restore)"""
+        m, dt, B = self.m, self.dtype, self.batch
+        E, M, K, P, g = m.encoder_embed_dim, m.latent_depth, m.num_keep_patches, self.P, self.g
+        Te = K + 1
         # ---- encoder (MCM.py:590-634): ids on device, embed only the kept patches
         shuf, rest = ops.ids_shuffle(scores, K, m.sum_lanes)
         pos_e = m.encoder_pos_embed.detach()
@@ -437,18 +530,13 @@ class _Executor:
                         act=ops.ACT_NONE if last else ops.ACT_GELU)
             H = (H + 2 - 3) // stride + 1
             x, cin = out, cout
+        return shuf, rest
 
-        # ---- entropy bottleneck + z_hat (MCM.py:741-744)
-        ops.eb_likelihood(m.entropy_bottleneck, self.Z, B, N, hz * hz, noise=z_noise, lik=self.ZLIK, zhat=self.ZHAT,
-                          table=self.eb_table)
-
-        # ---- h_s (MCM.py:747-748)
-        self._h_s(self.hss_w, self.LS)
-        self._h_s(self.hsm_w, self.LM)
-
-        # ---- slice loop (MCM.py:751-787)
-        self._slices(y_noise)
-
+    def _back(self, shuf, in_chans):
+        """g_s + decoder + unpatchify (MCM.py:636-688, 790-797) from YH; returns x_hat NCHW f32"""
+        m, dt, B = self.m, self.dtype, self.batch
+        Dd, K, L, P = m.decoder_embed_dim, m.num_keep_patches, self.L, self.P
+        Td = L + 1
         # ---- g_s (MCM.py:790-792): transposed 1x1 convs back to E-dim tokens
         x = self.YH
         for j, (w, b) in enumerate(self.gs_w):
@@ -464,10 +552,50 @@ class _Executor:
             run_block(self.dec, w, B, Td, dt, self.dec_s)
         ops.layernorm(self.dec, m.decoder_norm.weight, m.decoder_norm.bias, m.decoder_norm.eps, dt, rows=B * L,
                       row_group=L, group_stride=Td, row_offset=1, out=self.dn)
-        x_hat = torch.empty((B, imgs.shape[1], self.img, self.img), dtype=torch.float32, device=self.device)
+        x_hat = torch.empty((B, in_chans, self.img, self.img), dtype=torch.float32, device=self.device)
         ops.decoder_pred(self.dn, self.w_dp, m.decoder_pred.bias.detach(), x_hat, B, L, P, dt)
-        return {"x_hat": x_hat, "y": self.YLIK.clone(), "z": self.ZLIK.clone(), "ids_restore": rest,
-                "ids_shuffle": shuf}
+        return x_hat
+
+    # ------------------------------------------------------------------ Gaussian-conditional slice steps
+    # Each is called with (i0, nbs, mu, sigma, ms_stride): slices i0..i0+nbs-1, mu/sigma device addresses
+    # of rows [Mp][sw] per slice, ms_stride elements apart; it must leave y_hat (pre-LRP) in SUPY (operand
+    # dtype) and YPRE (f32) at channels i0*sw.. .
+    def _gc_forward(self, y_noise):
+        M, sw, B, HW, dt = self.m.latent_depth, self.sw, self.batch, self.g * self.g, self.dtype
+
+        def step(i0, nbs, mu, sigma, ms_stride):
+            ops.gc_slices(self.Y32, M, i0 * sw, mu, sigma, ms_stride, sw, y_noise, self.YLIK, M, self.SUPY, dt, M,
+                          self.YPRE, M, B, HW, nbs, sw)
+        return step
+
+    def _gc_compress(self, sym, idx):
+        """eval step + int32 symbols / scale indexes in the coder's [slice][image][channel][pixel] order"""
+        M, sw, B, HW, dt = self.m.latent_depth, self.sw, self.batch, self.g * self.g, self.dtype
+        table = self.m.gaussian_conditional.scale_table
+        per = B * sw * HW
+
+        def step(i0, nbs, mu, sigma, ms_stride):
+            ops.gc_slices_code(self.Y32, M, i0 * sw, mu, sigma, ms_stride, sw, self.YLIK, M, self.SUPY, dt, M,
+                               self.YPRE, M, B, HW, nbs, sw, sym[i0 * per:], idx[i0 * per:], table)
+        return step
+
+    def _gc_decompress(self, decoder):
+        """indexes on the device -> host rANS decode of the next slices' symbols -> y_hat = symbols + mu"""
+        gc = self.m.gaussian_conditional
+        M, sw, B, HW, dt = self.m.latent_depth, self.sw, self.batch, self.g * self.g, self.dtype
+        cdf, sizes, offsets = gc.host_tables()
+        bound = float(gc.scale_bound) if gc.scale_bound is not None else 0.11
+        per = B * sw * HW
+        idx_dev = torch.empty(self.m.num_slices * per, dtype=torch.int32, device=self.device)
+
+        def step(i0, nbs, mu, sigma, ms_stride):
+            n = nbs * per
+            ops.gc_indexes(sigma, ms_stride, sw, B, HW, nbs, sw, gc.scale_table, bound, idx_dev)
+            idx = idx_dev[:n].cpu().numpy()
+            vals = decoder.decode_stream_array(idx, cdf, sizes, offsets)
+            sym = torch.from_numpy(vals).to(self.device)
+            ops.gc_dequantize(sym, mu, ms_stride, sw, B, HW, nbs, sw, i0 * sw, self.SUPY, dt, M, self.YPRE, M)
+        return step
 
     def _h_s(self, layers, out_final):
         B, dt = self.batch, self.dtype
@@ -485,7 +613,7 @@ class _Executor:
                 cin = cout
             x = out
 
-    def _slices(self, y_noise):
+    def _slices(self, gc_step):
         m, dt, B, g = self.m, self.dtype, self.batch, self.g
         M, S, sw, ms, nb, Mp = m.latent_depth, m.num_slices, self.sw, self.maxsup, self.nb, self.Mp
         mid = self.mid
@@ -554,12 +682,10 @@ class _Executor:
         # slices 0..ms-1: serial (slice i conditions on y_hat 0..i-1)
         for i in range(ms):
             ms_stack(self.ms_first[i], self.ms_layers[i], supy, sw * i, i, 1)
-            ops.gc_slices(self.Y32, M, i * sw, musig, musig + ms_s1 * e4, Mp * sw, sw, y_noise, self.YLIK, M, supy,
-                          dt, M, ypre, M, B, g * g, 1, sw)
+            gc_step(i, 1, musig, musig + ms_s1 * e4, Mp * sw)
             lrp_stack(self.lrp_first[i], self.lrp_layers[i], i, 1)
         # slices ms..S-1: batched on the fixed support y_hat 0..ms-1
         if nb > 0:
             ms_stack(self.b_ms_first, self.b_ms_layers, supy, sw * ms, ms, nb)
-            ops.gc_slices(self.Y32, M, ms * sw, musig, musig + ms_s1 * e4, Mp * sw, sw, y_noise, self.YLIK, M, supy,
-                          dt, M, ypre, M, B, g * g, nb, sw)
+            gc_step(ms, nb, musig, musig + ms_s1 * e4, Mp * sw)
             lrp_stack(self.b_lrp_first, self.b_lrp_layers, ms, nb, x2=supy + ms * sw * esz)

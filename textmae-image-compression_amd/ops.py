@@ -16,7 +16,8 @@ from ._lib import ACT_GELU, ACT_NONE, TMAE_BF16, TMAE_F32, ConvArgs, EBParams
 __all__ = [
     "ids_shuffle", "layernorm", "linear", "linear_residual", "patch_embed", "cls_rows", "mha", "decoder_embed",
     "mask_rows", "decoder_pred", "conv3x3", "gc_slices", "eb_likelihood", "eb_aux_loss",
-    "gc_likelihood", "nhwc_to_nchw", "bpp", "gemm_plan", "dtype_code", "TMAE_F32", "TMAE_BF16", "ACT_NONE", "ACT_GELU",
+    "gc_likelihood", "nhwc_to_nchw", "bpp", "gemm_plan", "dtype_code", "gc_slices_code", "gc_indexes",
+    "gc_dequantize", "gc_pmf", "eb_pmf", "eb_symbols", "eb_dequantize", "invert_permutation", "TMAE_F32", "TMAE_BF16", "ACT_NONE", "ACT_GELU",
 ]
 
 
@@ -182,6 +183,79 @@ def gc_slices(y, ldy, yoff, mu, sigma, ms_stride, ld_ms, noise, lik, Mtot, yhat,
               HW, nslices, sw):
     _lib.call("tmae_gc_slices_fwd", _p(y), ldy, yoff, _p(mu), _p(sigma), ms_stride, ld_ms, _p(noise), _p(lik), Mtot,
               _p(yhat), dtype_code(yhat_dtype), ld_yhat, _p(yhat32), ld32, n, HW, nslices, sw, _stream())
+
+
+def gc_slices_code(y, ldy, yoff, mu, sigma, ms_stride, ld_ms, lik, Mtot, yhat, yhat_dtype, ld_yhat, yhat32, ld32, n,
+                   HW, nslices, sw, symbols, indexes, scale_table):
+    """eval slice step of MCM.compress: gc_slices outputs + int32 symbols / scale indexes in coder order"""
+    st = _need(scale_table.contiguous(), torch.float32, "scale_table")
+    _lib.call("tmae_gc_slices_code", _p(y), ldy, yoff, _p(mu), _p(sigma), ms_stride, ld_ms, _p(lik), Mtot, _p(yhat),
+              dtype_code(yhat_dtype), ld_yhat, _p(yhat32), ld32, n, HW, nslices, sw, _p(symbols), _p(indexes),
+              st.data_ptr(), st.numel(), _stream())
+
+
+def gc_indexes(sigma, ms_stride, ld_ms, n, HW, nslices, sw, scale_table, scale_bound, indexes):
+    st = _need(scale_table.contiguous(), torch.float32, "scale_table")
+    _lib.call("tmae_gc_indexes", _p(sigma), ms_stride, ld_ms, n, HW, nslices, sw, st.data_ptr(), st.numel(),
+              float(scale_bound), _p(indexes), _stream())
+
+
+def gc_dequantize(symbols, mu, ms_stride, ld_ms, n, HW, nslices, sw, yoff, yhat, yhat_dtype, ld_yhat, yhat32, ld32):
+    _lib.call("tmae_gc_dequantize", _p(symbols), _p(mu), ms_stride, ld_ms, n, HW, nslices, sw, yoff, _p(yhat),
+              dtype_code(yhat_dtype), ld_yhat, _p(yhat32), ld32, _stream())
+
+
+def gc_pmf(scale_table, pmf_center, max_length):
+    """GaussianConditional.update pmf rows + tail masses (device tensors)"""
+    st = _need(scale_table.contiguous(), torch.float32, "scale_table")
+    c = _need(pmf_center.to(torch.int32).contiguous(), torch.int32, "pmf_center")
+    pmf = torch.empty((st.numel(), max_length), dtype=torch.float32, device=st.device)
+    tail = torch.empty(st.numel(), dtype=torch.float32, device=st.device)
+    _lib.call("tmae_gc_pmf", st.data_ptr(), c.data_ptr(), st.numel(), max_length, pmf.data_ptr(), tail.data_ptr(),
+              _stream())
+    return pmf, tail
+
+
+def eb_pmf(eb, pmf_start, max_length):
+    """EntropyBottleneck.update pmf rows + tail masses (device tensors)"""
+    C = eb.channels
+    dev = eb.quantiles.device
+    start = _need(pmf_start.float().contiguous(), torch.float32, "pmf_start")
+    pmf = torch.empty((C, max_length), dtype=torch.float32, device=dev)
+    tail = torch.empty(C, dtype=torch.float32, device=dev)
+    table = torch.empty((C, 59), dtype=torch.float32, device=dev)
+    params = _eb_params(eb)
+    _lib.call("tmae_eb_pmf", params, table.data_ptr(), start.data_ptr(), C, max_length, pmf.data_ptr(),
+              tail.data_ptr(), _stream())
+    return pmf, tail
+
+
+def eb_symbols(eb, z_nhwc, n, C, HW, out=None, table=None):
+    """round(z - median) as int32 NCHW [n, C, HW] from NHWC z"""
+    dev = z_nhwc.device
+    out = torch.empty((n, C, HW), dtype=torch.int32, device=dev) if out is None else out
+    table = torch.empty((C, 59), dtype=torch.float32, device=dev) if table is None else table
+    params = _eb_params(eb)
+    _lib.call("tmae_eb_symbols", z_nhwc.data_ptr(), params, table.data_ptr(), n, C, HW, _p(out), _stream())
+    return out
+
+
+def eb_dequantize(eb, symbols, n, C, HW, zhat, table=None):
+    """z_hat (NHWC, zhat's dtype) = symbols (NCHW int32) + median"""
+    dev = zhat.device
+    table = torch.empty((C, 59), dtype=torch.float32, device=dev) if table is None else table
+    params = _eb_params(eb)
+    _lib.call("tmae_eb_dequantize", _p(symbols), params, table.data_ptr(), n, C, HW, _p(zhat), dtype_code(zhat.dtype),
+              _stream())
+    return zhat
+
+
+def invert_permutation(perm):
+    p = _need(perm.to(torch.int64).contiguous(), torch.int64, "permutation")
+    n, L = p.shape
+    inv = torch.empty_like(p)
+    _lib.call("tmae_invert_permutation", p.data_ptr(), inv.data_ptr(), n, L, _stream())
+    return inv
 
 
 def _eb_params(eb) -> EBParams:
