@@ -154,6 +154,17 @@ int tmae_bpp_sum(const float* y_lik, long long ny, const float* z_lik, long long
 /* layout helper: NHWC (channel stride ldx) -> NCHW */
 int tmae_nhwc_to_nchw(const float* x, int ldx, float* y, int n, int C, int HW, void* stream);
 
+/* ---------------------------------------------------------------- MaskedAutoencoderViT (models/MAE/models_mae.py)
+ * random_masking (123-148): ids_shuffle = stable ascending argsort(noise) per row, ids_restore = its
+ * inverse, mask[b][l] = 1 where rank >= len_keep (mask may be NULL).  L <= 2048. */
+int tmae_mae_masking(const float* noise, int64_t* ids_shuffle, int64_t* ids_restore, float* mask, int n, int L,
+                     int len_keep, void* stream);
+
+/* forward_loss (198-214): mean over masked patches of mean((pred - patchify(imgs))^2), per-patch normalised
+ * targets if norm_pix_loss.  pred [n*L][P*P*C] f32, imgs NCHW f32 (H == W), work >= 1024 doubles, out[0]. */
+int tmae_mae_loss(const float* pred, const float* imgs, const int64_t* ids_restore, int n, int C, int H, int W, int P,
+                  int len_keep, int norm_pix_loss, double* work, float* out, void* stream);
+
 /* ---------------------------------------------------------------- entropy coding, device side
  * (MCM.compress / decompress, MCM.py:805-968; compressai semantics restated, see rans.cpp) */
 

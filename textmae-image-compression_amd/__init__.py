@@ -8,7 +8,11 @@ from . import ops  # noqa: F401
 from ._lib import LIB_PATH, load as load_library  # noqa: F401
 from .entropy import CompressionModel, EntropyBottleneck, GaussianConditional, get_scale_table  # noqa: F401
 from .layers import Block, PatchEmbed  # noqa: F401
+from .mae import (MaskedAutoencoderViT, mae_vit_base_patch16, mae_vit_base_patch16_dec512d8b,  # noqa: F401
+                  mae_vit_huge_patch14, mae_vit_huge_patch14_dec512d8b, mae_vit_large_patch16,
+                  mae_vit_large_patch16_dec512d8b)
 from .mcm import MCM  # noqa: F401
 
-__all__ = ["MCM", "Block", "PatchEmbed", "EntropyBottleneck", "GaussianConditional", "CompressionModel", "ops",
+__all__ = ["MCM", "MaskedAutoencoderViT", "mae_vit_base_patch16_dec512d8b", "mae_vit_large_patch16_dec512d8b",
+           "mae_vit_huge_patch14_dec512d8b", "Block", "PatchEmbed", "EntropyBottleneck", "GaussianConditional", "CompressionModel", "ops",
            "load_library", "LIB_PATH", "get_scale_table"]

@@ -23,7 +23,7 @@
 // every index.  softmax uses exp rounded from double + sequential sum + reciprocal multiply
 // (identical to the oracle bit-for-bit; vs torch's Sleef exp this can only differ
 // when softmax*target lands within a few ulp of .5 — 0 of 3.6M sampled groups).
-#include "common.h"
+#include "sort.h"
 
 #define IDS_MAXL 1024
 #define IDS_THREADS 256
@@ -33,14 +33,6 @@
 __constant__ unsigned kPercentileBits[9] = {0x3dcccccdu, 0x3e4ccccdu, 0x3e99999au, 0x3ecccccdu, 0x3f000000u,
                                             0x3f19999au, 0x3f333333u, 0x3f4ccccdu, 0x3f666666u};
 
-__device__ __forceinline__ unsigned f2key(float f) {
-  unsigned u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float key2f(unsigned k) {
-  unsigned u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
-  return __uint_as_float(u);
-}
 
 // ---- torch CPU float32 sum order (aten SumKernel.cpp cascade_sum / multi_row_sum / row_sum).
 // acc: 4 levels x 4 ilp rows x W lanes scratch (LDS).  Valid for n <= 65536 (level_power = 4).
@@ -146,19 +138,7 @@ ids_shuffle_kernel(const float* __restrict__ scores, int64_t* __restrict__ ids_s
   __syncthreads();
 
   // 2. bitonic sort ascending by (value, index)
-  for (int k = 2; k <= P; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = t; i < P; i += IDS_THREADS) {
-        int ixj = i ^ j;
-        if (ixj > i) {
-          unsigned long long a = key[i], c = key[ixj];
-          bool up = ((i & k) == 0);
-          if ((a > c) == up) { key[i] = c; key[ixj] = a; }
-        }
-      }
-      __syncthreads();
-    }
-  }
+  lds_bitonic_sort<IDS_THREADS>(key, P);
 
   // 3. runs of equal values (float equality)
   for (int p = t; p < L; p += IDS_THREADS) {

@@ -17,7 +17,8 @@ __all__ = [
     "ids_shuffle", "layernorm", "linear", "linear_residual", "patch_embed", "cls_rows", "mha", "decoder_embed",
     "mask_rows", "decoder_pred", "conv3x3", "gc_slices", "eb_likelihood", "eb_aux_loss",
     "gc_likelihood", "nhwc_to_nchw", "bpp", "gemm_plan", "dtype_code", "gc_slices_code", "gc_indexes",
-    "gc_dequantize", "gc_pmf", "eb_pmf", "eb_symbols", "eb_dequantize", "invert_permutation", "TMAE_F32", "TMAE_BF16", "ACT_NONE", "ACT_GELU",
+    "gc_dequantize", "gc_pmf", "eb_pmf", "eb_symbols", "eb_dequantize", "invert_permutation", "mae_masking",
+    "mae_loss", "TMAE_F32", "TMAE_BF16", "ACT_NONE", "ACT_GELU",
 ]
 
 
@@ -183,6 +184,35 @@ def gc_slices(y, ldy, yoff, mu, sigma, ms_stride, ld_ms, noise, lik, Mtot, yhat,
               HW, nslices, sw):
     _lib.call("tmae_gc_slices_fwd", _p(y), ldy, yoff, _p(mu), _p(sigma), ms_stride, ld_ms, _p(noise), _p(lik), Mtot,
               _p(yhat), dtype_code(yhat_dtype), ld_yhat, _p(yhat32), ld32, n, HW, nslices, sw, _stream())
+
+
+def mae_masking(noise: torch.Tensor, len_keep: int):
+    """models_mae.random_masking indices: (ids_shuffle, ids_restore) int64 and the binary mask f32 [n, L]"""
+    nz = _need(noise.float().contiguous(), name="noise")
+    n, L = nz.shape
+    shuf = torch.empty((n, L), dtype=torch.int64, device=nz.device)
+    rest = torch.empty_like(shuf)
+    mask = torch.empty((n, L), dtype=torch.float32, device=nz.device)
+    _lib.call("tmae_mae_masking", nz.data_ptr(), shuf.data_ptr(), rest.data_ptr(), mask.data_ptr(), n, L, len_keep,
+              _stream())
+    return shuf, rest, mask
+
+
+_MAE_WORK = {}
+
+
+def mae_loss(pred, imgs, ids_restore, len_keep, patch, norm_pix_loss):
+    """models_mae.forward_loss -> 0-d f32 device tensor"""
+    p = _need(pred.contiguous(), torch.float32, "pred")
+    x = _need(imgs.contiguous(), torch.float32, "imgs")
+    n, C, H, W = x.shape
+    work = _MAE_WORK.get(x.device)
+    if work is None:
+        work = _MAE_WORK[x.device] = torch.empty(1024, dtype=torch.float64, device=x.device)
+    out = torch.empty((), dtype=torch.float32, device=x.device)
+    _lib.call("tmae_mae_loss", p.data_ptr(), x.data_ptr(), _need(ids_restore, torch.int64, "ids_restore").data_ptr(),
+              n, C, H, W, patch, len_keep, int(bool(norm_pix_loss)), work.data_ptr(), out.data_ptr(), _stream())
+    return out
 
 
 def gc_slices_code(y, ldy, yoff, mu, sigma, ms_stride, ld_ms, lik, Mtot, yhat, yhat_dtype, ld_yhat, yhat32, ld32, n,

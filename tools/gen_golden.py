@@ -177,12 +177,7 @@ def gen_forward(MCM, name, cfgd, batch, seed):
 
 # ---------------------------------------------------------------------------------------- F6
 def gen_mae_masking():
-    import importlib.util
-
-    spec = importlib.util.spec_from_file_location("ref_models_mae", os.path.join(REF, "models/MAE/models_mae.py"))
-    mm = importlib.util.module_from_spec(spec)
-    sys.modules["util.pos_embed"] = sys.modules["models.Compression.common.pos_embed"]
-    spec.loader.exec_module(mm)
+    mm = _ref_mae_module()
     data = {}
     for seed in (0, 1, 2):
         torch.manual_seed(seed)
@@ -193,6 +188,55 @@ def gen_mae_masking():
         data[f"s{seed}_ids_restore"] = rest.numpy()
     np.savez_compressed(os.path.join(OUT, "mae_masking.npz"), **data)
     print("mae_masking.npz")
+
+
+def _ref_mae_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("ref_models_mae", os.path.join(REF, "models/MAE/models_mae.py"))
+    mm = importlib.util.module_from_spec(spec)
+    sys.modules["util.pos_embed"] = sys.modules["models.Compression.common.pos_embed"]
+    spec.loader.exec_module(mm)
+    return mm
+
+
+def gen_mae_forward():
+    """mae_vit_base_patch16_dec512d8b built after torch.manual_seed(0), imgs =
+    randn(4,3,224,224) from a generator seeded 1, torch.manual_seed(2) right before forward(mask_ratio=0.75);
+    plus a tiny norm_pix_loss=True model.  pred is stored on every 7th patch row (size)."""
+    from functools import partial
+
+    mm = _ref_mae_module()
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    torch.manual_seed(0)
+    model = mm.mae_vit_base_patch16_dec512d8b()
+    sd = model.state_dict()
+    init_sha = sha16(np.concatenate([v.float().numpy().ravel() for v in sd.values() if v.numel()]))
+    imgs = torch.randn(4, 3, 224, 224, generator=torch.Generator().manual_seed(1))
+    torch.manual_seed(2)
+    noise = torch.rand(4, 196)
+    torch.manual_seed(2)
+    with torch.no_grad():
+        loss, pred, mask = model(imgs, mask_ratio=0.75)
+    data = {"init_sha_seed0": np.array(init_sha), "noise": noise.numpy(), "loss": loss.numpy(),
+            "mask": mask.numpy(), "pred_rows": pred[:, ::7].numpy(), "pred_sum": pred.double().sum((1, 2)).numpy()}
+    # tiny norm_pix_loss model (every shape of the path, small enough to store whole)
+    torch.manual_seed(5)
+    tiny = mm.MaskedAutoencoderViT(img_size=64, patch_size=16, in_chans=3, embed_dim=64, depth=2, num_heads=2,
+                                   decoder_embed_dim=32, decoder_depth=1, decoder_num_heads=1, mlp_ratio=4.0,
+                                   norm_layer=partial(torch.nn.LayerNorm, eps=1e-6), norm_pix_loss=True)
+    timgs = torch.randn(2, 3, 64, 64, generator=torch.Generator().manual_seed(6))
+    torch.manual_seed(7)
+    tnoise = torch.rand(2, 16)
+    torch.manual_seed(7)
+    with torch.no_grad():
+        tl, tp_, tm = tiny(timgs, mask_ratio=0.6)
+    data.update(tiny_imgs=timgs.numpy(), tiny_noise=tnoise.numpy(), tiny_loss=tl.numpy(), tiny_pred=tp_.numpy(),
+                tiny_mask=tm.numpy())
+    for k, v in tiny.state_dict().items():
+        data["tiny_sd." + k] = v.numpy()
+    np.savez_compressed(os.path.join(OUT, "mae_forward.npz"), **data)
+    print("mae_forward.npz", float(loss), float(tl))
 
 
 def gen_state_keys(MCM):
@@ -220,6 +264,7 @@ def main():
     gen_forward(MCM, "tiny", TINY, batch=2, seed=7)
     gen_forward(MCM, "small12", SMALL12, batch=2, seed=11)
     gen_mae_masking()
+    gen_mae_forward()
     gen_state_keys(MCM)
 
 
