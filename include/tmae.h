@@ -113,6 +113,9 @@ typedef struct tmae_conv_args {
   const float* lrp_src; int ld_src; long long src_s1, src_s2;
   void* y2; int ldy2; long long y2_s1, y2_s2;
   int nb1, nb2;
+  /* training: optional pre-activation copy (GELU input; the last lrp conv's pre-tanh value, f32) in the
+   * output's dtype and layout (pixel-shuffled for subpel convs), rows ldp apart (lrp) */
+  void* pre; int ldp; long long pre_s1, pre_s2;
 } tmae_conv_args;
 int tmae_conv3x3(const tmae_conv_args* args, int dtype, void* stream);
 
@@ -227,6 +230,127 @@ int tmae_rans_decode_with_indexes(void* handle, const int32_t* indexes, long lon
                                   int cdf_stride, const int32_t* cdf_sizes, const int32_t* offsets, int ncdf,
                                   int32_t* out);
 int tmae_rans_decoder_destroy(void* handle);
+
+/* ================================================================ training (MCM.forward backward,
+ * driven by utils/engine.py:75-91: loss.backward(), clip_grad_norm_, Adam, aux Adam)
+ * Every gradient is f32; GEMM operands are in `dtype` like the forward. */
+
+/* forward extras: tmae_linear_fwd + the pre-activation (GELU input) copy `pre` (dtype of y, ld ldp) */
+int tmae_linear_fwd_pre(const void* x, int x_f32, int ldx, int row_group, int group_stride, int row_offset,
+                        const void* w, const float* bias, void* y, int y_f32, int ldy, void* pre, int ldp, int M,
+                        int N, int K, int act, int dtype, void* stream);
+/* out = resid + x w^T + bias, out-of-place (autograd keeps the block input) */
+int tmae_linear_residual_out(const void* x, int ldx, const void* w, const float* bias, const float* resid, float* out,
+                             int ld, int M, int N, int K, int dtype, void* stream);
+/* tmae_mha_fwd + the per-row log2-sum-exp lse[b][h][t] (base-2, of scores * scale * log2 e) */
+int tmae_mha_fwd_lse(const void* qkv, void* out, float* lse, int B, int T, int H, int dh, float scale, int dtype,
+                     void* stream);
+/* timm Attention backward: dqkv [B*T][3*H*dh] (dtype) from qkv, o (forward output), dO, lse */
+int tmae_mha_bwd(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv, int B, int T, int H,
+                 int dh, float scale, int dtype, void* stream);
+/* kept-patch im2col for the patch-embed weight gradient: out[n*keep][C*P*P] (dtype) */
+int tmae_patch_gather(const float* imgs, const int64_t* ids_shuffle, void* out, int n, int C, int H, int W, int patch,
+                      int L, int keep, int dtype, void* stream);
+
+/* weight gradient (split-K TN GEMM on the operands as the forward stored them):
+ * out[m][n] = sum_k A(k, m) B(k, n); A dense (row k = source row (k/a_G)*a_Gs + a_off + k%a_G, lda);
+ * B dense (same remap) or, b_conv = 1, the implicit im2col of a 3x3 conv (padding 1, stride b_stride) over
+ * NHWC maps (channels [0, b_c1) from b, the rest from b2; column = tap * b_Cin + ci).  The split-K partials
+ * ([splits][M][N] f32 in work, see tmae_wgrad_workspace) are summed in a fixed order and written to
+ * out[o_base + m*o_sm + (n % o_cp)*o_sc + (n / o_cp)*o_st] (= or += with accumulate). */
+typedef struct tmae_wgrad_args {
+  const void* a; int lda; int a_G, a_Gs, a_off;
+  const void* b; int ldb; int b_G, b_Gs, b_off;
+  int b_conv; const void* b2; int b_c1, b_ld2, b_H, b_W, b_stride, b_Cin;
+  int M, N, K;
+  float* work; long long work_elems;
+  float* out; long long o_base, o_sm, o_sc, o_st; int o_cp; int accumulate;
+} tmae_wgrad_args;
+int tmae_wgrad(const tmae_wgrad_args* args, int dtype, void* stream);
+long long tmae_wgrad_workspace(int M, int N, int K, int dtype);
+
+/* data gradient of y = x w^T: dx[M][K] = dy[M][N] wt[K][N]^T (wt = w transposed, dtype); dy rows remapped
+ * like tmae_linear_fwd.  out (dtype, or f32 with out_f32) = dx * gelu'(pre) when pre is given (the GELU
+ * before this layer), acc32 (optional) += the same in f32. */
+int tmae_dgrad_linear(const void* dy, int ldy, int row_group, int group_stride, int row_offset, const void* wt, int M,
+                      int N, int K, void* out, int out_f32, int ldo, const void* pre, int ldp, float* acc32, int ld32,
+                      int dtype, void* stream);
+
+/* data gradient of a 3x3 conv (padding 1, stride 1 or 2) as a transposed-conv implicit GEMM:
+ * dx [n*H*W][cin] from dy [n*Ho*Wo][cout] (dtype) and wd = weight as [cin][3][3][cout] (dtype).
+ * Single output (out, dtype or f32, optionally * gelu'(pre)) or, acc[0] != NULL, routed f32 accumulation:
+ * input channels [0, lim0) += into acc[0], [lim0, lim1) into acc[1], [lim1, cin) into acc[2]
+ * (torch.cat inputs, MCM.py:761,766,780). */
+typedef struct tmae_conv_dgrad_args {
+  const void* dy; int ldy;
+  int n, H, W, stride, cout, cin;
+  const void* wd;
+  void* out; int out_f32, ldo; const void* pre; int ldp;
+  float* acc[3]; int ld_acc[3]; int lim[3];
+} tmae_conv_dgrad_args;
+int tmae_conv_dgrad(const tmae_conv_dgrad_args* args, int dtype, void* stream);
+
+/* weight re-layout: dst (contiguous [d0][d1][d2][d3], dst_dtype) = src[i0*s0 + i1*s1 + i2*s2 + i3*s3] (f32) */
+int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0, int d1, int d2, int d3, long long s0, long long s1,
+                  long long s2, long long s3, void* stream);
+
+/* bias gradient: out[c] (=/+=) sum over rows r of x[(r/G)*Gs + off + r%G][c]; work >= 256*C floats */
+int tmae_colsum(const void* x, int x_dtype, int ld, int rows, int C, int row_group, int group_stride, int row_offset,
+                float* work, long long work_elems, float* out, int accumulate, void* stream);
+
+/* LayerNorm backward (x rows remapped as in the forward, dy dense f32): dx32[sr] = dres[sr] (optional) + dx,
+ * dxop (optional, op_dtype) = the same; dgamma / dbeta (=/+=).  work >= 2*D*(rows/8 + 4) floats. */
+int tmae_layernorm_bwd(const float* x, const float* gamma, const float* dy, const float* dres, float* dx32, void* dxop,
+                       int op_dtype, int rows, int D, int row_group, int group_stride, int row_offset, float eps,
+                       float* work, long long work_elems, float* dgamma, float* dbeta, int accumulate, void* stream);
+
+/* subpel_conv3x3 (PixelShuffle(2)) backward: dpre [n*H*W][C4] = unshuffle(dy) * gelu'(pre) (pre optional) */
+int tmae_unshuffle_bwd(const void* dy, int dy_f32, int ldy, const void* pre, int ldp, void* out, int n, int H, int W,
+                       int C4, int dtype, void* stream);
+/* out = dy * gelu'(pre), elementwise */
+int tmae_gelu_bwd(const void* dy, int dy_f32, const void* pre, void* out, long long total, int dtype, void* stream);
+/* y_hat = y_hat_pre + 0.5 tanh(t) (MCM.py:782-783): g = g32 (f32) + g16 (dtype), either optional;
+ * dt = g * 0.5 (1 - tanh^2 t) (dtype), gsum = g (f32, optional) */
+int tmae_lrp_bwd(const float* g32, int ld32, const void* g16, int ld16, const float* t, int ldt, void* dt, int lddt,
+                 float* gsum, int ldgs, int rows, int C, int dtype, void* stream);
+/* strided 2-D copy, element size esz (2 or 4 bytes) */
+int tmae_copy2d(const void* src, int lds, void* dst, int ldd, int rows, int cols, int esz, void* stream);
+/* GaussianConditional likelihood + quantize_ste backward for one slice (MCM.py:767-776) */
+int tmae_gc_bwd(const float* y, int ldy, int yoff, const float* mu, const float* sigma, int ld_ms, const float* noise,
+                int Mtot, const float* glik, const float* gyp, int ldg, float* dy, int lddy, void* dmu, void* dsigma,
+                int ldd, int n, int HW, int sw, int dtype, void* stream);
+/* EntropyBottleneck likelihood backward (MCM.py:741-744): dz NHWC (= gzhat pass-through + likelihood path) and
+ * every density parameter's gradient into `grads` (same struct, f32 gradient buffers; =/+=) */
+int tmae_eb_bwd(const tmae_eb_params* params, const float* z, const float* noise, const float* glik,
+                const float* gzhat, float* dz, int n, int C, int HW, const tmae_eb_params* grads, int accumulate,
+                void* stream);
+/* aux_loss backward w.r.t. quantiles (utils/engine.py:87) */
+int tmae_eb_aux_bwd(const tmae_eb_params* params, const float* target, const float* gout, float* dquantiles, int C,
+                    int accumulate, void* stream);
+/* rate backward (rd_loss.py:19-20): dlik = gout[0] / (lik * -ln2 * num_pixels) */
+int tmae_bpp_bwd(const float* lik, const float* gout, float* dlik, long long n, double num_pixels, void* stream);
+/* patchify of the reconstruction gradient: out [n*L][P*P*C] (dtype) */
+int tmae_patchify(const float* imgs, void* out, int n, int C, int H, int W, int patch, int dtype, void* stream);
+/* decoder_embed backward: gather the kept tokens' rows of the decoder gradient (off-by-one cls, MCM.py:664-672)
+ * into tok_grad [n*ntok][D] (dtype) and the mask_token gradient (mask_part >= n*D floats) */
+int tmae_decoder_embed_bwd_gather(const float* dec_grad, const int64_t* ids_shuffle, void* tok_grad, int n, int ntok,
+                                  int L, int D, int dtype, float* mask_part, float* dmask, int accumulate,
+                                  void* stream);
+/* out = a + b (f32) */
+int tmae_add(const float* a, const float* b, float* out, long long n, void* stream);
+
+/* optimizer over flat f32 buffers: torch.optim.Adam step `step` (1-based), gradients scaled by clip[0]
+ * when clip != NULL */
+int tmae_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2, float eps,
+              float weight_decay, int step, const float* clip, void* stream);
+/* the same over many tensors in one launch: table (device int64) = ntensors x {p, g, m, v, n, first_chunk},
+ * chunks of 1024 elements, nchunks in total */
+int tmae_adam_multi(const long long* table, int ntensors, long long nchunks, float lr, float beta1, float beta2,
+                    float eps, float weight_decay, int step, const float* clip, void* stream);
+/* clip_grad_norm_: out[0] = ||g||_2, out[1] = min(1, max_norm / (norm + 1e-6)); work >= 512 doubles */
+int tmae_grad_norm(const float* g, long long n, double* work, float max_norm, float* out, void* stream);
+/* g *= scale[0] */
+int tmae_scale(float* g, long long n, const float* scale, void* stream);
 
 /* diagnostics (no device work): writes into out[len] the name of the MFMA GEMM variant that
  * tmae_linear_fwd / tmae_conv3x3 launch for an M x N x K problem batched `batch` times (tile shape,

@@ -1,0 +1,333 @@
+"""Training path on the MI355X: backward kernels vs torch autograd (fp32 CPU), and the whole
+MCM.forward backward vs the autograd-faithful oracle (oracle/train_oracle.py).
+
+Tolerances: f32 operand path max|a-b| / max|b| <= 1e-3 per tensor (bit-level GELU / erf approximations
+and summation order); bf16 operand path relative L2 <= 3e-2 against the fp32 reference.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    den = b.abs().max().item()
+    return (a - b).abs().max().item() / (den if den > 0 else 1.0)
+
+
+def _rel2(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    den = b.norm().item()
+    return (a - b).norm().item() / (den if den > 0 else 1.0)
+
+
+@pytest.fixture(scope="module")
+def T():
+    import textmae_amd  # noqa: F401
+    from textmae_amd import train_ops
+
+    return train_ops
+
+
+def _rnd(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+# ------------------------------------------------------------------------------ wgrad (TN GEMM)
+@pytest.mark.parametrize("K,M,N", [(300, 256, 136), (1000, 72, 200), (9280, 768, 3072), (16448, 1536, 512)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_wgrad_dense(T, K, M, N, dt):
+    if dt == torch.float32 and K * M * N > 3e9:
+        pytest.skip("f32 parity path checked on the smaller shapes")
+    a, b = _rnd(K, M, seed=1), _rnd(K, N, seed=2)
+    ref = (a.to(dt).double().t() @ b.to(dt).double()).float()
+    out = torch.empty(M, N, device="cuda")
+    T.wgrad(a.cuda().to(dt), b.cuda().to(dt), M, N, K, out, dt)
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < (1e-5 if dt == torch.float32 else 2e-3)
+
+
+def test_wgrad_remap_transposed_accumulate(T):
+    # A rows remapped (drop one row per group of 5: the encoder's cls rows), output transposed, accumulate
+    G, K0 = 4, 60
+    a_full, b = _rnd(K0 // G * (G + 1), 64, seed=3), _rnd(K0, 48, seed=4)
+    rows = torch.tensor([(k // G) * (G + 1) + 1 + k % G for k in range(K0)])
+    ref = (a_full[rows].double().t() @ b.double()).float().t()
+    out = torch.ones(48, 64, device="cuda")
+    T.wgrad(a_full.cuda(), b.cuda(), 64, 48, K0, out, torch.float32, a_remap=(G, G + 1, 1), layout="dense_t",
+            accumulate=True)
+    torch.cuda.synchronize()
+    assert _rel(out - 1, ref) < 1e-5
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_wgrad_conv(T, stride, dt):
+    n, H, cin, cout = 3, 12, 48, 40
+    x = _rnd(n, cin, H, H, seed=5)
+    Ho = (H + 2 - 3) // stride + 1
+    dy = _rnd(n, cout, Ho, Ho, seed=6)
+    xq, dyq = x.to(dt).float(), dy.to(dt).float()
+    ref = torch.nn.grad.conv2d_weight(xq.double(), (cout, cin, 3, 3), dyq.double(), stride=stride, padding=1).float()
+    x_nhwc = xq.permute(0, 2, 3, 1).contiguous().reshape(-1, cin).cuda().to(dt)
+    dy_nhwc = dyq.permute(0, 2, 3, 1).contiguous().reshape(-1, cout).cuda().to(dt)
+    out = torch.empty(cout, cin, 3, 3, device="cuda")
+    T.wgrad(dy_nhwc, x_nhwc, cout, 9 * cin, n * Ho * Ho, out, dt, conv=dict(c1=cin, H=H, W=H, stride=stride, cin=cin),
+            layout="conv")
+    torch.cuda.synchronize()
+    assert _rel(out, ref) < (1e-5 if dt == torch.float32 else 2e-3)
+
+
+def test_wgrad_conv_two_sources(T):
+    # torch.cat([x1, x2], 1) without a copy, written into a channel slice of a wider weight
+    n, H, c1, c2, cout = 2, 6, 16, 8, 24
+    x1, x2, dy = _rnd(n, c1, H, H, seed=7), _rnd(n, c2, H, H, seed=8), _rnd(n, cout, H, H, seed=9)
+    ref = torch.nn.grad.conv2d_weight(torch.cat([x1, x2], 1).double(), (cout, c1 + c2, 3, 3), dy.double(),
+                                      padding=1).float()
+    out = torch.zeros(cout, c1 + c2 + 8, 3, 3, device="cuda")
+    nh = lambda t: t.permute(0, 2, 3, 1).contiguous().reshape(-1, t.shape[1]).cuda()  # noqa: E731
+    T.wgrad(nh(dy), nh(x1), cout, 9 * (c1 + c2), n * H * H, out, torch.float32,
+            conv=dict(x2=nh(x2), c1=c1, ld2=c2, H=H, W=H, cin=c1 + c2), layout="conv", cin_total=c1 + c2 + 8,
+            ci_off=8)
+    torch.cuda.synchronize()
+    assert _rel(out[:, 8:], ref) < 1e-5 and out[:, :8].abs().max().item() == 0
+
+
+# ------------------------------------------------------------------------------ data gradients
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_dgrad_linear_gelu(T, dt):
+    M, N, K = 290, 256, 136
+    dy, w, pre = _rnd(M, N, seed=10), _rnd(N, K, seed=11) / 16, _rnd(M, K, seed=12)
+    dyq, wq, preq = dy.to(dt).float(), w.to(dt).float(), pre.to(dt).float()
+    x = preq.clone().requires_grad_(True)
+    (F.gelu(x) * (dyq @ wq)).sum().backward()
+    ref = x.grad
+    wt = wq.t().contiguous().cuda().to(dt)
+    out = torch.empty(M, K, device="cuda", dtype=torch.float32)
+    T.dgrad_linear(dyq.cuda().to(dt), wt, M, N, K, dt, out=out, pre=preq.cuda().to(dt))
+    acc = torch.ones(M, K, device="cuda")
+    T.dgrad_linear(dyq.cuda().to(dt), wt, M, N, K, dt, acc32=acc)
+    torch.cuda.synchronize()
+    tol = 1e-4 if dt == torch.float32 else 1e-2
+    assert _rel(out, ref) < tol
+    assert _rel(acc - 1, dyq @ wq) < tol
+
+
+@pytest.mark.parametrize("stride", [1, 2])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv_dgrad(T, stride, dt):
+    n, H, cin, cout = 2, 12, 40, 48
+    Ho = (H + 2 - 3) // stride + 1
+    w, dy, pre = _rnd(cout, cin, 3, 3, seed=13) / 8, _rnd(n, cout, Ho, Ho, seed=14), _rnd(n, cin, H, H, seed=15)
+    wq, dyq, preq = w.to(dt).float(), dy.to(dt).float(), pre.to(dt).float()
+    dx = torch.nn.grad.conv2d_input((n, cin, H, H), wq.double(), dyq.double(), stride=stride, padding=1).float()
+    x = preq.clone().requires_grad_(True)
+    (F.gelu(x) * dx).sum().backward()
+    nh = lambda t: t.permute(0, 2, 3, 1).contiguous().reshape(-1, t.shape[1])  # noqa: E731
+    wd = wq.permute(1, 2, 3, 0).contiguous().reshape(cin, -1).cuda().to(dt)
+    out = torch.empty(n * H * H, cin, device="cuda")
+    T.conv_dgrad(nh(dyq).cuda().to(dt), wd, n, H, H, stride, cout, cin, dt, out=out, pre=nh(preq).cuda().to(dt))
+    # routed f32 accumulation of the same data gradient: channels [0,16) / [16,24) / [24,40)
+    r0, r1, r2 = (torch.ones(n * H * H, c, device="cuda") for c in (16, 8, 16))
+    T.conv_dgrad(nh(dyq).cuda().to(dt), wd, n, H, H, stride, cout, cin, dt, routes=[(r0, 16, 16), (r1, 8, 8), (r2, 16, 16)])
+    torch.cuda.synchronize()
+    tol = 1e-4 if dt == torch.float32 else 1e-2
+    assert _rel(out, nh(x.grad)) < tol
+    assert _rel(torch.cat([r0, r1, r2], 1) - 1, nh(dx)) < tol
+
+
+def test_layernorm_bwd_remap(T):
+    B, Tn, D = 3, 7, 128
+    x = _rnd(B * Tn, D, seed=16)
+    gamma, beta = 1 + 0.1 * _rnd(D, seed=17), 0.1 * _rnd(D, seed=18)
+    rows = torch.tensor([b * Tn + 1 + k for b in range(B) for k in range(Tn - 1)])  # drop cls rows
+    dy = _rnd(len(rows), D, seed=19)
+    xr, g_, b_ = x.clone().requires_grad_(True), gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    (F.layer_norm(xr[rows], (D,), g_, b_, 1e-6) * dy).sum().backward()
+    dres = _rnd(B * Tn, D, seed=20)
+    dx = torch.zeros(B * Tn, D, device="cuda")
+    dxop = torch.zeros(B * Tn, D, device="cuda", dtype=torch.bfloat16)
+    dg, db = torch.empty(D, device="cuda"), torch.empty(D, device="cuda")
+    T.layernorm_bwd(x.cuda(), gamma.cuda(), dy.cuda(), dx, len(rows), D, 1e-6, dg, db, dres=dres.cuda(), dxop=dxop,
+                    row_group=Tn - 1, group_stride=Tn, row_offset=1)
+    torch.cuda.synchronize()
+    ref = xr.grad.clone()
+    ref[rows] += dres[rows]
+    assert _rel(dx, ref) < 1e-5
+    assert _rel(dxop.float(), ref) < 1e-2
+    assert _rel(dg, g_.grad) < 1e-5 and _rel(db, b_.grad) < 1e-5
+
+
+# ------------------------------------------------------------------------------ attention
+@pytest.mark.parametrize("T_,H,dh", [(145, 12, 64), (257, 16, 32), (20, 2, 64)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_mha_bwd(T, T_, H, dh, dt):
+    from textmae_amd import ops
+
+    B = 2
+    D = H * dh
+    qkv = _rnd(B * T_, 3 * D, seed=21).to(dt).float()
+    do = _rnd(B * T_, D, seed=22).to(dt).float()
+    scale = dh ** -0.5
+    q_ = qkv.clone().requires_grad_(True)
+    t = q_.reshape(B, T_, 3, H, dh).permute(2, 0, 3, 1, 4)
+    att = ((t[0] @ t[1].transpose(-2, -1)) * scale).softmax(-1)
+    o = (att @ t[2]).transpose(1, 2).reshape(B * T_, D)
+    (o * do).sum().backward()
+    qg = qkv.cuda().to(dt)
+    out = torch.empty(B * T_, D, device="cuda", dtype=dt)
+    lse = torch.empty(B * H * T_, device="cuda")
+    T.mha_lse(qg, B, T_, H, dh, scale, dt, out, lse)
+    dq = torch.empty(B * T_, 3 * D, device="cuda", dtype=dt)
+    T.mha_bwd(qg, out, do.cuda().to(dt), lse, dq, B, T_, H, dh, scale, dt)
+    o_plain = ops.mha(qg, B, T_, H, dh, scale, dt)
+    torch.cuda.synchronize()
+    assert torch.equal(out, o_plain)  # the lse variant computes the same output
+    if dt == torch.float32:
+        assert _rel(out, o) < 1e-5
+        assert _rel(dq, q_.grad) < 1e-4
+    else:
+        assert _rel2(dq.float(), q_.grad) < 2e-2
+
+
+# ------------------------------------------------------------------------------ optimizer
+def test_adam_matches_torch(T):
+    n = 1000
+    p0, g = _rnd(n, seed=23), _rnd(n, seed=24)
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([ref], lr=1e-3, weight_decay=0.01)
+    p, m, v = p0.cuda(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    clip = torch.tensor([0.5, 0.5], device="cuda")
+    for step in range(1, 4):
+        ref.grad = g * 0.5
+        opt.step()
+        T.adam(p, g.cuda(), m, v, 1e-3, 0.9, 0.999, 1e-8, 0.01, step, clip=clip[1:])
+    norm = torch.empty(2, device="cuda")
+    T.grad_norm(g.cuda(), 1.0, norm)
+    torch.cuda.synchronize()
+    assert _rel(p, ref.detach()) < 1e-6
+    assert abs(norm[0].item() - g.norm().item()) < 1e-4 * g.norm().item()
+    assert abs(norm[1].item() - min(1.0, 1.0 / (g.norm().item() + 1e-6))) < 1e-6
+
+
+# ------------------------------------------------------------------------------ whole model
+SMALL = dict(img_size=64, patch_size=16, encoder_embed_dim=64, encoder_depth=2, encoder_num_heads=2,
+             decoder_embed_dim=64, decoder_depth=2, decoder_num_heads=2, latent_depth=192, hyperprior_depth=96,
+             num_slices=12, num_keep_patches=16)
+
+
+def _model_and_oracle(cfgd, seed, B, dt):
+    import textmae_amd
+    from oracle.mcm_oracle import MCMConfig, make_state_dict
+
+    cfg = MCMConfig(**cfgd)
+    sd = make_state_dict(cfg, seed)
+    m = textmae_amd.MCM(**cfg.kwargs())
+    full = m.state_dict()
+    full.update(sd)
+    m.load_state_dict(full)
+    m = m.cuda().train()
+    m.compute_dtype = dt
+    m.distortion = "none"
+    rng = np.random.default_rng(seed + 1)
+    L = (cfg.img_size // cfg.patch_size) ** 2
+    g = int(cfg.num_keep_patches ** 0.5)
+    hz = g // 4
+    imgs = torch.from_numpy(rng.random((B, 3, cfg.img_size, cfg.img_size), dtype=np.float32))
+    scores = torch.from_numpy(rng.random((B, L), dtype=np.float32))
+    zn = torch.from_numpy(rng.uniform(-0.5, 0.5, (B, cfg.hyperprior_depth, hz, hz)).astype(np.float32))
+    yn = torch.from_numpy(rng.uniform(-0.5, 0.5, (B, cfg.latent_depth, g, g)).astype(np.float32))
+    R = torch.from_numpy(rng.standard_normal((B, 3, cfg.img_size, cfg.img_size)).astype(np.float32)) * 1e-2
+    return m, cfg, sd, imgs, scores, zn, yn, R
+
+
+def _hip_grads(m, imgs, scores, zn, yn, R):
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    m.zero_grad(set_to_none=True)
+    out = m(imgs.cuda(), scores.cuda(), noise=(zn.cuda(), yn.cuda()))
+    crit = RateDistortionLoss(lmbda=1e-2)
+    loss = crit(out, imgs.cuda())["bpp_loss"] + (out["x_hat"] * R.cuda()).sum()
+    loss.backward()
+    aux = m.aux_loss()
+    aux.backward()
+    torch.cuda.synchronize()
+    return {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters() if p.requires_grad}, out, loss, aux
+
+
+def _oracle_grads(cfg, sd, imgs, scores, zn, yn, R):
+    from oracle.train_oracle import aux_loss, mcm_forward_train, rate_bpp
+
+    leaf = {k: (v.clone().double().requires_grad_(True) if torch.is_floating_point(v) and not k.endswith("pos_embed")
+                and k != "entropy_bottleneck.target" else (v.double() if torch.is_floating_point(v) else v))
+            for k, v in sd.items()}
+    x_hat, ylik, zlik = mcm_forward_train(leaf, cfg, imgs.double(), scores, zn.double(), yn.double())
+    n, _, H, W = imgs.shape
+    loss = rate_bpp(ylik, zlik, n * H * W) + (x_hat * R.double()).sum()
+    loss.backward()
+    aux = aux_loss(leaf, "entropy_bottleneck.")
+    aux.backward()
+    return {k: v.grad for k, v in leaf.items() if isinstance(v, torch.Tensor) and v.requires_grad}, x_hat, loss, aux
+
+
+def test_mcm_train_grads_f32_vs_oracle():
+    m, cfg, sd, imgs, scores, zn, yn, R = _model_and_oracle(SMALL, 3, 2, torch.float32)
+    hip, out, loss, aux = _hip_grads(m, imgs, scores, zn, yn, R)
+    ref, x_ref, loss_ref, aux_ref = _oracle_grads(cfg, sd, imgs, scores, zn, yn, R)
+    assert _rel(out["x_hat"], x_ref) < 1e-4
+    assert abs(loss.item() - loss_ref.item()) < 1e-4 * max(1.0, abs(loss_ref.item()))
+    assert abs(aux.item() - aux_ref.item()) < 1e-4 * abs(aux_ref.item())
+    bad = []
+    for name, g in hip.items():
+        r = ref[name].float()
+        if r.abs().max() == 0:
+            if g.abs().max() > 1e-6:
+                bad.append((name, "nonzero", g.abs().max().item()))
+            continue
+        e = _rel(g, r)
+        if e > 2e-3:
+            bad.append((name, e))
+    assert not bad, bad[:20]
+
+
+def test_mcm_train_bf16_close_to_f32():
+    m, cfg, sd, imgs, scores, zn, yn, R = _model_and_oracle(SMALL, 4, 2, torch.float32)
+    g32, *_ = _hip_grads(m, imgs, scores, zn, yn, R)
+    m.compute_dtype = torch.bfloat16
+    g16, *_ = _hip_grads(m, imgs, scores, zn, yn, R)
+    flat32 = torch.cat([g32[k].reshape(-1) for k in g32])
+    flat16 = torch.cat([g16[k].reshape(-1) for k in g32])
+    assert torch.isfinite(flat16).all()
+    assert _rel2(flat16, flat32) < 5e-2
+
+
+def test_mcm_train_vitb_step_runs():
+    """north-star geometry (ViT-B/16 256^2, K=144) at a small batch: fwd + bwd + 2 Adam steps, bf16"""
+    import textmae_amd
+    from textmae_amd.optim import FusedAdam
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    torch.manual_seed(0)
+    m = textmae_amd.MCM(img_size=256, num_keep_patches=144).cuda().train()
+    m.compute_dtype = torch.bfloat16
+    opt = FusedAdam([p for n, p in m.named_parameters() if not n.endswith(".quantiles")], lr=1e-4)
+    imgs = torch.rand(2, 3, 256, 256, device="cuda")
+    scores = torch.rand(2, 256, device="cuda")
+    crit = RateDistortionLoss(lmbda=1e-2)
+    losses = []
+    for _ in range(2):
+        out = m(imgs, scores)
+        loss = crit(out, imgs)["loss"]
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+        opt.step()
+        losses.append(loss.item())
+    assert all(math.isfinite(v) for v in losses)
+    assert all(torch.isfinite(p).all() for p in m.parameters())

@@ -35,6 +35,30 @@ class ConvArgs(ctypes.Structure):
         ("lrp_src", P), ("ld_src", I), ("src_s1", LL), ("src_s2", LL),
         ("y2", P), ("ldy2", I), ("y2_s1", LL), ("y2_s2", LL),
         ("nb1", I), ("nb2", I),
+        ("pre", P), ("ldp", I), ("pre_s1", LL), ("pre_s2", LL),
+    ]
+
+
+class WgradArgs(ctypes.Structure):
+    """mirror of tmae_wgrad_args"""
+    _fields_ = [
+        ("a", P), ("lda", I), ("a_G", I), ("a_Gs", I), ("a_off", I),
+        ("b", P), ("ldb", I), ("b_G", I), ("b_Gs", I), ("b_off", I),
+        ("b_conv", I), ("b2", P), ("b_c1", I), ("b_ld2", I), ("b_H", I), ("b_W", I), ("b_stride", I), ("b_Cin", I),
+        ("M", I), ("N", I), ("K", I),
+        ("work", P), ("work_elems", LL),
+        ("out", P), ("o_base", LL), ("o_sm", LL), ("o_sc", LL), ("o_st", LL), ("o_cp", I), ("accumulate", I),
+    ]
+
+
+class ConvDgradArgs(ctypes.Structure):
+    """mirror of tmae_conv_dgrad_args"""
+    _fields_ = [
+        ("dy", P), ("ldy", I),
+        ("n", I), ("H", I), ("W", I), ("stride", I), ("cout", I), ("cin", I),
+        ("wd", P),
+        ("out", P), ("out_f32", I), ("ldo", I), ("pre", P), ("ldp", I),
+        ("acc", P * 3), ("ld_acc", I * 3), ("lim", I * 3),
     ]
 
 
@@ -83,7 +107,37 @@ SIGNATURES = {
     "tmae_rans_decoder_create": [P, LL, ctypes.POINTER(ctypes.c_void_p)],
     "tmae_rans_decode_with_indexes": [P, P, LL, P, I, P, P, I, P],
     "tmae_rans_decoder_destroy": [P],
+    # training
+    "tmae_linear_fwd_pre": [P, I, I, I, I, I, P, P, P, I, I, P, I, I, I, I, I, I, P],
+    "tmae_linear_residual_out": [P, I, P, P, P, P, I, I, I, I, I, P],
+    "tmae_mha_fwd_lse": [P, P, P, I, I, I, I, F, I, P],
+    "tmae_mha_bwd": [P, P, P, P, P, I, I, I, I, F, I, P],
+    "tmae_patch_gather": [P, P, P, I, I, I, I, I, I, I, I, P],
+    "tmae_wgrad": [ctypes.POINTER(WgradArgs), I, P],
+    "tmae_dgrad_linear": [P, I, I, I, I, P, I, I, I, P, I, I, P, I, P, I, I, P],
+    "tmae_conv_dgrad": [ctypes.POINTER(ConvDgradArgs), I, P],
+    "tmae_relayout": [P, P, I, I, I, I, I, LL, LL, LL, LL, P],
+    "tmae_colsum": [P, I, I, I, I, I, I, I, P, LL, P, I, P],
+    "tmae_layernorm_bwd": [P, P, P, P, P, P, I, I, I, I, I, I, F, P, LL, P, P, I, P],
+    "tmae_unshuffle_bwd": [P, I, I, P, I, P, I, I, I, I, I, P],
+    "tmae_gelu_bwd": [P, I, P, P, LL, I, P],
+    "tmae_lrp_bwd": [P, I, P, I, P, I, P, I, P, I, I, I, I, P],
+    "tmae_copy2d": [P, I, P, I, I, I, I, P],
+    "tmae_gc_bwd": [P, I, I, P, P, I, P, I, P, P, I, P, I, P, P, I, I, I, I, I, P],
+    "tmae_eb_bwd": [ctypes.POINTER(EBParams), P, P, P, P, P, I, I, I, ctypes.POINTER(EBParams), I, P],
+    "tmae_eb_aux_bwd": [ctypes.POINTER(EBParams), P, P, P, I, I, P],
+    "tmae_bpp_bwd": [P, P, P, LL, ctypes.c_double, P],
+    "tmae_patchify": [P, P, I, I, I, I, I, I, P],
+    "tmae_decoder_embed_bwd_gather": [P, P, P, I, I, I, I, I, P, P, I, P],
+    "tmae_add": [P, P, P, LL, P],
+    "tmae_adam": [P, P, P, P, LL, F, F, F, F, F, I, P, P],
+    "tmae_adam_multi": [P, I, LL, F, F, F, F, F, I, P, P],
+    "tmae_grad_norm": [P, LL, P, F, P, P],
+    "tmae_scale": [P, LL, P, P],
 }
+
+# entry points that return a value rather than a status
+VALUE_FUNCS = {"tmae_wgrad_workspace": ([I, I, I, I], ctypes.c_longlong)}
 
 _lib = None
 
@@ -103,10 +157,19 @@ def load():
             fn = getattr(lib, name)
             fn.argtypes = args
             fn.restype = ctypes.c_int
+        for name, (args, res) in VALUE_FUNCS.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = res
         lib.tmae_last_error_string.argtypes = []
         lib.tmae_last_error_string.restype = ctypes.c_char_p
         _lib = lib
     return _lib
+
+
+def value(name: str, *args):
+    """call an entry point of VALUE_FUNCS and return its result"""
+    return getattr(load(), name)(*args)
 
 
 def call(name: str, *args):

@@ -18,7 +18,8 @@ template <> struct AttnCfg<float> { static constexpr int KPAD = 4, VPAD = 1, EPC
 
 template <typename T, int DH>
 __global__ void __launch_bounds__(1024)
-mha_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, int Tn, int H, int Tpad, float scale_log2e) {
+mha_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, float* __restrict__ lse, int Tn, int H, int Tpad,
+               float scale_log2e) {
   constexpr int KPAD = AttnCfg<T>::KPAD, VPAD = AttnCfg<T>::VPAD, EPC = AttnCfg<T>::EPC;
   constexpr int NDT = DH / 32;  // 32-wide output tiles along the head dim
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -161,6 +162,7 @@ mha_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, int Tn, int H, in
   }
 
   if (q >= Tn) return;
+  if (lse && hh == 0) lse[(size_t)bh * Tn + q] = m_run + log2f(l_run);  // base-2 log-sum-exp of the scaled scores
   const float inv_l = 1.0f / l_run;
   T* orow = out + ((size_t)b * Tn + q) * D + h * DH;
 #pragma unroll
@@ -174,14 +176,15 @@ mha_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, int Tn, int H, in
 }
 
 template <typename T, int DH>
-static int mha_launch(const void* qkv, void* out, int B, int Tn, int H, float scale, hipStream_t st) {
+static int mha_launch(const void* qkv, void* out, int B, int Tn, int H, float scale, hipStream_t st,
+                      float* lse = nullptr) {
   const int Tpad = (Tn + 31) / 32 * 32;
   const int nthr = 64 * (Tpad / 32);
   const size_t lds = ((size_t)Tpad * (DH + AttnCfg<T>::KPAD) + (size_t)DH * (Tpad + AttnCfg<T>::VPAD)) * sizeof(T);
   TMAE_REQUIRE(nthr <= 1024 && lds <= 160 * 1024, "tmae_mha_fwd: sequence length %d too long", Tn);
   if (B * H == 0 || Tn == 0) return TMAE_OK;
-  hipLaunchKernelGGL((mha_fwd_kernel<T, DH>), dim3(B * H), dim3(nthr), lds, st, (const T*)qkv, (T*)out, Tn, H, Tpad,
-                     scale * 1.4426950408889634f);
+  hipLaunchKernelGGL((mha_fwd_kernel<T, DH>), dim3(B * H), dim3(nthr), lds, st, (const T*)qkv, (T*)out, lse, Tn, H,
+                     Tpad, scale * 1.4426950408889634f);
   TMAE_LAUNCH_CHECK("tmae_mha_fwd");
 }
 
@@ -193,4 +196,368 @@ extern "C" int tmae_mha_fwd(const void* qkv, void* out, int B, int T, int H, int
                                           : mha_launch<bf16, 32>(qkv, out, B, T, H, scale, st);
   return dh == 64 ? mha_launch<float, 64>(qkv, out, B, T, H, scale, st)
                   : mha_launch<float, 32>(qkv, out, B, T, H, scale, st);
+}
+
+extern "C" int tmae_mha_fwd_lse(const void* qkv, void* out, float* lse, int B, int T, int H, int dh, float scale,
+                                int dtype, void* stream) {
+  TMAE_REQUIRE(dh == 32 || dh == 64, "tmae_mha_fwd_lse: head dim %d unsupported (32 or 64)", dh);
+  TMAE_REQUIRE(lse != nullptr, "tmae_mha_fwd_lse: lse is NULL");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMAE_BF16) return dh == 64 ? mha_launch<bf16, 64>(qkv, out, B, T, H, scale, st, lse)
+                                          : mha_launch<bf16, 32>(qkv, out, B, T, H, scale, st, lse);
+  return dh == 64 ? mha_launch<float, 64>(qkv, out, B, T, H, scale, st, lse)
+                  : mha_launch<float, 32>(qkv, out, B, T, H, scale, st, lse);
+}
+
+// ====================================================================================== backward
+// Flash-style attention backward (timm Attention, MCM.py:629-630, 678-679): P is recomputed from Q, K and
+// the forward's base-2 log-sum-exp; one workgroup owns one (image, head) and holds Q, K, V, dO (row-major)
+// plus Q^T, K^T, dO^T in LDS for the whole sequence.
+//   phase 1 (wave = 32 keys, loop over query tiles):  S = Q K^T, dP = dO V^T with the key on the lane, so
+//            P and dS = P (dP - delta) are already the A operands of dV += P^T dO and dK += scale dS^T Q
+//            (cdna_hip_programming.md §3, "accumulator tile as the next operand");
+//   phase 2 (wave = 32 queries, loop over key tiles): S^T, dP^T with the query on the lane -> dQ += scale dS K.
+// Both phases own their outputs: no atomics, bitwise reproducible.  delta = rowsum(dO * O).
+template <int DH>
+__global__ void __launch_bounds__(1024)
+mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+                    const float* __restrict__ lse, bf16* __restrict__ dqkv, int Tn, int H, int Tpad, float scale) {
+  constexpr int LDR = DH + 8;
+  constexpr int NDT = DH / 32;
+  constexpr int CPR = DH / 8;
+  const int LDT = Tpad + 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  bf16* Qs = reinterpret_cast<bf16*>(smem);
+  bf16* Ks = Qs + (size_t)Tpad * LDR;
+  bf16* Vs = Ks + (size_t)Tpad * LDR;
+  bf16* dOs = Vs + (size_t)Tpad * LDR;
+  bf16* Qt = dOs + (size_t)Tpad * LDR;
+  bf16* Kt = Qt + (size_t)DH * LDT;
+  bf16* dOt = Kt + (size_t)DH * LDT;
+  float* lse_s = reinterpret_cast<float*>(dOt + (size_t)DH * LDT);
+  float* dl_s = lse_s + Tpad;
+
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * DH, ld = 3 * D;
+  const bf16* base = qkv + (size_t)b * Tn * ld + h * DH;
+  const bf16* obase = o + (size_t)b * Tn * D + h * DH;
+  const bf16* gbase = dout + (size_t)b * Tn * D + h * DH;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+
+  for (int i = tid; i < Tpad * CPR; i += nthr) {
+    const int r = i / CPR, c = i - r * CPR;
+    uint4 qv = uint4{0, 0, 0, 0}, kv = qv, vv = qv, gv = qv;
+    if (r < Tn) {
+      qv = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + c * 8);
+      kv = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + D + c * 8);
+      vv = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + 2 * D + c * 8);
+      gv = *reinterpret_cast<const uint4*>(gbase + (size_t)r * D + c * 8);
+    }
+    *reinterpret_cast<uint4*>(Qs + (size_t)r * LDR + c * 8) = qv;
+    *reinterpret_cast<uint4*>(Ks + (size_t)r * LDR + c * 8) = kv;
+    *reinterpret_cast<uint4*>(Vs + (size_t)r * LDR + c * 8) = vv;
+    *reinterpret_cast<uint4*>(dOs + (size_t)r * LDR + c * 8) = gv;
+    const bf16* qe = reinterpret_cast<const bf16*>(&qv);
+    const bf16* ke = reinterpret_cast<const bf16*>(&kv);
+    const bf16* ge = reinterpret_cast<const bf16*>(&gv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      Qt[(size_t)(c * 8 + e) * LDT + r] = qe[e];
+      Kt[(size_t)(c * 8 + e) * LDT + r] = ke[e];
+      dOt[(size_t)(c * 8 + e) * LDT + r] = ge[e];
+    }
+  }
+  for (int r = tid; r < Tpad; r += nthr) {
+    float d = 0.0f, l = 0.0f;
+    if (r < Tn) {
+      const bf16* orow = obase + (size_t)r * D;
+      const bf16* grow = gbase + (size_t)r * D;
+#pragma unroll 8
+      for (int k = 0; k < DH; ++k) d += (float)orow[k] * (float)grow[k];
+      l = lse[(size_t)bh * Tn + r];
+    }
+    dl_s[r] = d;
+    lse_s[r] = l;
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6, nw = Tpad / 32;
+  const int col = lane & 31, hh = lane >> 5;
+  const float c2 = scale * 1.4426950408889634f;
+  if (wave >= nw) return;
+
+  // ---------------- phase 1: this wave's 32 keys
+  {
+    const int kb = 32 * wave;
+    bf16x8 kf[DH / 16], vf[DH / 16];
+#pragma unroll
+    for (int s = 0; s < DH / 16; ++s) {
+      kf[s] = *reinterpret_cast<const bf16x8*>(Ks + (size_t)(kb + col) * LDR + 16 * s + 8 * hh);
+      vf[s] = *reinterpret_cast<const bf16x8*>(Vs + (size_t)(kb + col) * LDR + 16 * s + 8 * hh);
+    }
+    f32x16 dV[NDT], dK[NDT];
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dV[t][r] = dK[t][r] = 0.0f;
+    const bool kok = kb + col < Tn;
+    for (int qt = 0; qt < nw; ++qt) {
+      f32x16 S, G;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S[r] = G[r] = 0.0f;
+#pragma unroll
+      for (int s = 0; s < DH / 16; ++s) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Qs + (size_t)(qt * 32 + col) * LDR + 16 * s + 8 * hh);
+        S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, kf[s], S, 0, 0, 0);
+        const bf16x8 g = *reinterpret_cast<const bf16x8*>(dOs + (size_t)(qt * 32 + col) * LDR + 16 * s + 8 * hh);
+        G = __builtin_amdgcn_mfma_f32_32x32x16_bf16(g, vf[s], G, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float p = (kok && q < Tn) ? exp2f(S[r] * c2 - lse_s[q]) : 0.0f;
+        S[r] = p;
+        G[r] = p * (G[r] - dl_s[q]) * scale;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 pa, da;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { pa[j] = (bf16)S[8 * s + j]; da[j] = (bf16)G[8 * s + j]; }
+        const int k0 = qt * 32 + 16 * s + 4 * hh;
+#pragma unroll
+        for (int t = 0; t < NDT; ++t) {
+          const bf16* grow = dOt + (size_t)(32 * t + col) * LDT + k0;
+          const bf16* qrow = Qt + (size_t)(32 * t + col) * LDT + k0;
+          const bf16x4 g0 = *reinterpret_cast<const bf16x4*>(grow), g1 = *reinterpret_cast<const bf16x4*>(grow + 8);
+          const bf16x4 q0 = *reinterpret_cast<const bf16x4*>(qrow), q1 = *reinterpret_cast<const bf16x4*>(qrow + 8);
+          bf16x8 gb, qb8;
+          gb[0] = g0[0]; gb[1] = g0[1]; gb[2] = g0[2]; gb[3] = g0[3]; gb[4] = g1[0]; gb[5] = g1[1]; gb[6] = g1[2]; gb[7] = g1[3];
+          qb8[0] = q0[0]; qb8[1] = q0[1]; qb8[2] = q0[2]; qb8[3] = q0[3]; qb8[4] = q1[0]; qb8[5] = q1[1]; qb8[6] = q1[2]; qb8[7] = q1[3];
+          dV[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, gb, dV[t], 0, 0, 0);
+          dK[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, qb8, dK[t], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (key < Tn) {
+          bf16* row = dqkv + ((size_t)b * Tn + key) * ld + h * DH + 32 * t + col;
+          row[D] = (bf16)dK[t][r];
+          row[2 * D] = (bf16)dV[t][r];
+        }
+      }
+  }
+
+  // ---------------- phase 2: this wave's 32 queries
+  {
+    const int qb = 32 * wave;
+    bf16x8 qf[DH / 16], gf[DH / 16];
+#pragma unroll
+    for (int s = 0; s < DH / 16; ++s) {
+      qf[s] = *reinterpret_cast<const bf16x8*>(Qs + (size_t)(qb + col) * LDR + 16 * s + 8 * hh);
+      gf[s] = *reinterpret_cast<const bf16x8*>(dOs + (size_t)(qb + col) * LDR + 16 * s + 8 * hh);
+    }
+    const bool qok = qb + col < Tn;
+    const float lq = lse_s[qb + col], dq = dl_s[qb + col];
+    f32x16 dQ[NDT];
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dQ[t][r] = 0.0f;
+    for (int kt = 0; kt < nw; ++kt) {
+      f32x16 S, G;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S[r] = G[r] = 0.0f;
+#pragma unroll
+      for (int s = 0; s < DH / 16; ++s) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Ks + (size_t)(kt * 32 + col) * LDR + 16 * s + 8 * hh);
+        S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], S, 0, 0, 0);
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(Vs + (size_t)(kt * 32 + col) * LDR + 16 * s + 8 * hh);
+        G = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v, gf[s], G, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float p = (qok && key < Tn) ? exp2f(S[r] * c2 - lq) : 0.0f;
+        G[r] = p * (G[r] - dq) * scale;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 da;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) da[j] = (bf16)G[8 * s + j];
+        const int k0 = kt * 32 + 16 * s + 4 * hh;
+#pragma unroll
+        for (int t = 0; t < NDT; ++t) {
+          const bf16* krow = Kt + (size_t)(32 * t + col) * LDT + k0;
+          const bf16x4 k0v = *reinterpret_cast<const bf16x4*>(krow), k1v = *reinterpret_cast<const bf16x4*>(krow + 8);
+          bf16x8 kb8;
+          kb8[0] = k0v[0]; kb8[1] = k0v[1]; kb8[2] = k0v[2]; kb8[3] = k0v[3];
+          kb8[4] = k1v[0]; kb8[5] = k1v[1]; kb8[6] = k1v[2]; kb8[7] = k1v[3];
+          dQ[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, kb8, dQ[t], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = qb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (q < Tn) dqkv[((size_t)b * Tn + q) * ld + h * DH + 32 * t + col] = (bf16)dQ[t][r];
+      }
+  }
+}
+
+// f32 (parity) form: same two phases on v_mfma_f32_32x32x2_f32, operands read straight from global memory
+// (L2-resident per head); exact f32 products.
+template <int DH>
+__global__ void __launch_bounds__(1024)
+mha_bwd_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ o, const float* __restrict__ dout,
+                   const float* __restrict__ lse, float* __restrict__ dqkv, int Tn, int H, int Tpad, float scale) {
+  constexpr int NDT = DH / 32;
+  __shared__ float lse_s[1024], dl_s[1024];
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * DH, ld = 3 * D;
+  const float* Q = qkv + (size_t)b * Tn * ld + h * DH;
+  const float* K = Q + D;
+  const float* V = Q + 2 * D;
+  const float* Og = o + (size_t)b * Tn * D + h * DH;
+  const float* G = dout + (size_t)b * Tn * D + h * DH;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  for (int r = tid; r < Tpad; r += nthr) {
+    float d = 0.0f, l = 0.0f;
+    if (r < Tn) {
+      for (int k = 0; k < DH; ++k) d += Og[(size_t)r * D + k] * G[(size_t)r * D + k];
+      l = lse[(size_t)bh * Tn + r];
+    }
+    dl_s[r] = d;
+    lse_s[r] = l;
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6, nw = Tpad / 32;
+  const int col = lane & 31, hh = lane >> 5;
+  const float c2 = scale * 1.4426950408889634f;
+  if (wave >= nw) return;
+  auto ld_row = [&](const float* m, int row, int stride, int k) -> float {
+    return row < Tn ? m[(size_t)row * stride + k] : 0.0f;
+  };
+  {  // phase 1
+    const int kb = 32 * wave;
+    f32x16 dV[NDT], dK[NDT];
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dV[t][r] = dK[t][r] = 0.0f;
+    const bool kok = kb + col < Tn;
+    for (int qt = 0; qt < nw; ++qt) {
+      f32x16 S, P;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S[r] = P[r] = 0.0f;
+      for (int kk = 0; kk < DH / 2; ++kk) {
+        const int d = 2 * kk + hh;
+        S = __builtin_amdgcn_mfma_f32_32x32x2f32(ld_row(Q, qt * 32 + col, ld, d), ld_row(K, kb + col, ld, d), S, 0, 0, 0);
+        P = __builtin_amdgcn_mfma_f32_32x32x2f32(ld_row(G, qt * 32 + col, D, d), ld_row(V, kb + col, ld, d), P, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float p = (kok && q < Tn) ? exp2f(S[r] * c2 - lse_s[q]) : 0.0f;
+        S[r] = p;
+        P[r] = p * (P[r] - dl_s[q]) * scale;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = qt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+#pragma unroll
+        for (int t = 0; t < NDT; ++t) {
+          const int d = 32 * t + col;
+          dV[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(S[r], ld_row(G, q, D, d), dV[t], 0, 0, 0);
+          dK[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(P[r], ld_row(Q, q, ld, d), dK[t], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (key < Tn) {
+          float* row = dqkv + ((size_t)b * Tn + key) * ld + h * DH + 32 * t + col;
+          row[D] = dK[t][r];
+          row[2 * D] = dV[t][r];
+        }
+      }
+  }
+  {  // phase 2
+    const int qb = 32 * wave;
+    const bool qok = qb + col < Tn;
+    const float lq = lse_s[qb + col], dq = dl_s[qb + col];
+    f32x16 dQ[NDT];
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dQ[t][r] = 0.0f;
+    for (int kt = 0; kt < nw; ++kt) {
+      f32x16 S, P;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) S[r] = P[r] = 0.0f;
+      for (int kk = 0; kk < DH / 2; ++kk) {
+        const int d = 2 * kk + hh;
+        S = __builtin_amdgcn_mfma_f32_32x32x2f32(ld_row(K, kt * 32 + col, ld, d), ld_row(Q, qb + col, ld, d), S, 0, 0, 0);
+        P = __builtin_amdgcn_mfma_f32_32x32x2f32(ld_row(V, kt * 32 + col, ld, d), ld_row(G, qb + col, D, d), P, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        const float p = (qok && key < Tn) ? exp2f(S[r] * c2 - lq) : 0.0f;
+        P[r] = p * (P[r] - dq) * scale;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+#pragma unroll
+        for (int t = 0; t < NDT; ++t)
+          dQ[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(P[r], ld_row(K, key, ld, 32 * t + col), dQ[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int q = qb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (q < Tn) dqkv[((size_t)b * Tn + q) * ld + h * DH + 32 * t + col] = dQ[t][r];
+      }
+  }
+}
+
+template <int DH>
+static int mha_bwd_launch(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv, int B, int Tn,
+                          int H, float scale, int dtype, hipStream_t st) {
+  const int Tpad = (Tn + 31) / 32 * 32;
+  const int nthr = 64 * (Tpad / 32);
+  TMAE_REQUIRE(nthr <= 1024, "tmae_mha_bwd: sequence length %d too long", Tn);
+  if (B * H == 0 || Tn == 0) return TMAE_OK;
+  if (dtype == TMAE_BF16) {
+    const size_t lds = ((size_t)4 * Tpad * (DH + 8) + (size_t)3 * DH * (Tpad + 4)) * 2 + (size_t)2 * Tpad * 4;
+    TMAE_REQUIRE(lds <= 160 * 1024, "tmae_mha_bwd: sequence length %d needs %zu B of LDS", Tn, lds);
+    hipLaunchKernelGGL((mha_bwd_bf16_kernel<DH>), dim3(B * H), dim3(nthr), lds, st, (const bf16*)qkv, (const bf16*)o,
+                       (const bf16*)dout, lse, (bf16*)dqkv, Tn, H, Tpad, scale);
+  } else {
+    hipLaunchKernelGGL((mha_bwd_f32_kernel<DH>), dim3(B * H), dim3(nthr), 0, st, (const float*)qkv, (const float*)o,
+                       (const float*)dout, lse, (float*)dqkv, Tn, H, Tpad, scale);
+  }
+  TMAE_LAUNCH_CHECK("tmae_mha_bwd");
+}
+
+extern "C" int tmae_mha_bwd(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv, int B,
+                            int T, int H, int dh, float scale, int dtype, void* stream) {
+  TMAE_REQUIRE(dh == 32 || dh == 64, "tmae_mha_bwd: head dim %d unsupported (32 or 64)", dh);
+  TMAE_REQUIRE(qkv && o && dout && lse && dqkv, "tmae_mha_bwd: null argument");
+  hipStream_t st = (hipStream_t)stream;
+  return dh == 64 ? mha_bwd_launch<64>(qkv, o, dout, lse, dqkv, B, T, H, scale, dtype, st)
+                  : mha_bwd_launch<32>(qkv, o, dout, lse, dqkv, B, T, H, scale, dtype, st);
 }

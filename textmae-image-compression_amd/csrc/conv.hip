@@ -10,7 +10,13 @@ template <typename OT, int ACT> struct EpiPixelShuffle2 {
   const float* bias;
   int H, W, ldo;
   BStride so, sb;
-  __device__ void batch(int b1, int b2) { out += so.at(b1, b2); bias += sb.at(b1, b2); }
+  OT* pre = nullptr;  // optional pre-activation copy, same (shuffled) layout as out
+  BStride sp = {0, 0};
+  __device__ void batch(int b1, int b2) {
+    out += so.at(b1, b2);
+    bias += sb.at(b1, b2);
+    if (pre) pre += sp.at(b1, b2);
+  }
   __device__ void operator()(int m, int n, f32x4 v) const {
     const int hw = H * W;
     const int b = m / hw, rem = m - b * hw;
@@ -20,9 +26,11 @@ template <typename OT, int ACT> struct EpiPixelShuffle2 {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float o = v[j];
-      if (ACT == TMAE_ACT_GELU) o = gelu_erf(o);
       const int oy = 2 * y + (j >> 1), ox = 2 * x + (j & 1);
-      out[(((size_t)b * 2 * H + oy) * 2 * W + ox) * ldo + c] = to_out<OT>(o);
+      const size_t at = (((size_t)b * 2 * H + oy) * 2 * W + ox) * ldo + c;
+      if (pre) pre[at] = to_out<OT>(o);
+      if (ACT == TMAE_ACT_GELU) o = gelu_erf(o);
+      out[at] = to_out<OT>(o);
     }
   }
   // 8 columns = output channels c, c+1 of the 4 sub-pixels: four 2-channel stores
@@ -37,9 +45,11 @@ template <typename OT, int ACT> struct EpiPixelShuffle2 {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float o0 = lo[j], o1 = hi[j];
-      if (ACT == TMAE_ACT_GELU) { o0 = gelu_erf(o0); o1 = gelu_erf(o1); }
       const int oy = 2 * y + (j >> 1), ox = 2 * x + (j & 1);
-      OT* p = out + (((size_t)b * 2 * H + oy) * 2 * W + ox) * ldo + c;
+      const size_t at = (((size_t)b * 2 * H + oy) * 2 * W + ox) * ldo + c;
+      if (pre) { pre[at] = to_out<OT>(o0); pre[at + 1] = to_out<OT>(o1); }
+      if (ACT == TMAE_ACT_GELU) { o0 = gelu_erf(o0); o1 = gelu_erf(o1); }
+      OT* p = out + at;
       p[0] = to_out<OT>(o0);
       p[1] = to_out<OT>(o1);
     }
@@ -56,14 +66,19 @@ template <typename OT> struct EpiLRP {
   int ldo2;
   const float* bias;
   BStride ssrc, so, so2, sb;
+  float* pre = nullptr;  // optional pre-tanh value (training: tanh' in the backward)
+  int ldp = 0;
+  BStride sp = {0, 0};
   __device__ void batch(int b1, int b2) {
     src += ssrc.at(b1, b2);
     out += so.at(b1, b2);
     if (out2) out2 += so2.at(b1, b2);
     bias += sb.at(b1, b2);
+    if (pre) pre += sp.at(b1, b2);
   }
   __device__ void operator()(int m, int n, f32x4 v) const {
     v += load4f(bias + n);
+    if (pre) store4(pre + (size_t)m * ldp + n, v);
     f32x4 o = load4f(src + (size_t)m * lds + n);
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = o[j] + 0.5f * tanhf(v[j]);
@@ -75,6 +90,7 @@ template <typename OT> struct EpiLRP {
     load8f(bias + n, b0, b1);
     load8f(src + (size_t)m * lds + n, o0, o1);
     lo += b0; hi += b1;
+    if (pre) store8(pre + (size_t)m * ldp + n, lo, hi);
 #pragma unroll
     for (int j = 0; j < 4; ++j) { o0[j] += 0.5f * tanhf(lo[j]); o1[j] += 0.5f * tanhf(hi[j]); }
     store8(out + (size_t)m * ldo + n, o0, o1);
@@ -103,20 +119,24 @@ static int conv_t(const tmae_conv_args& a, hipStream_t st) {
   if (a.pixel_shuffle) {
     TMAE_REQUIRE(a.stride == 1, "tmae_conv3x3: pixel shuffle needs stride 1");
     if (a.y_f32) {
-      EpiPixelShuffle2<float, 1> g{(float*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2}};
-      EpiPixelShuffle2<float, 0> l{(float*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2}};
+      EpiPixelShuffle2<float, 1> g{(float*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2},
+                                   (float*)a.pre, {a.pre_s1, a.pre_s2}};
+      EpiPixelShuffle2<float, 0> l{(float*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2},
+                                   (float*)a.pre, {a.pre_s1, a.pre_s2}};
       if (a.act == TMAE_ACT_GELU) TMAE_GO(g);
       TMAE_GO(l);
     }
-    EpiPixelShuffle2<T, 1> g{(T*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2}};
-    EpiPixelShuffle2<T, 0> l{(T*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2}};
+    EpiPixelShuffle2<T, 1> g{(T*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2},
+                             (T*)a.pre, {a.pre_s1, a.pre_s2}};
+    EpiPixelShuffle2<T, 0> l{(T*)a.y, a.bias, a.H, a.W, a.ldy, {a.y_s1, a.y_s2}, {a.b_s1, a.b_s2},
+                             (T*)a.pre, {a.pre_s1, a.pre_s2}};
     if (a.act == TMAE_ACT_GELU) TMAE_GO(g);
     TMAE_GO(l);
   }
   if (a.lrp_src) {
     TMAE_REQUIRE(!a.y_f32 || sizeof(T) == 4, "tmae_conv3x3: lrp output must be in the operand dtype");
     EpiLRP<T> r{a.lrp_src, a.ld_src, (T*)a.y, a.ldy, (T*)a.y2, a.ldy2, a.bias, {a.src_s1, a.src_s2},
-                {a.y_s1, a.y_s2}, {a.y2_s1, a.y2_s2}, {a.b_s1, a.b_s2}};
+                {a.y_s1, a.y_s2}, {a.y2_s1, a.y2_s2}, {a.b_s1, a.b_s2}, (float*)a.pre, a.ldp, {a.pre_s1, a.pre_s2}};
     TMAE_GO(r);
   }
   if (a.y_f32) {
@@ -127,6 +147,9 @@ static int conv_t(const tmae_conv_args& a, hipStream_t st) {
     g.addend = l.addend = a.addend;
     g.ld_add = l.ld_add = a.ld_add;
     g.sa = l.sa = BStride{a.a_s1, a.a_s2};
+    g.pre = l.pre = (float*)a.pre;
+    g.ldp = l.ldp = a.ldp;
+    g.sp = l.sp = BStride{a.pre_s1, a.pre_s2};
     if (a.act == TMAE_ACT_GELU) TMAE_GO(g);
     TMAE_GO(l);
   }
@@ -140,6 +163,9 @@ static int conv_t(const tmae_conv_args& a, hipStream_t st) {
   g.out32 = l.out32 = a.y32;
   g.ld32 = l.ld32 = a.ld32;
   g.s32 = l.s32 = BStride{a.y32_s1, a.y32_s2};
+  g.pre = l.pre = (T*)a.pre;
+  g.ldp = l.ldp = a.ldp;
+  g.sp = l.sp = BStride{a.pre_s1, a.pre_s2};
   if (a.act == TMAE_ACT_GELU) TMAE_GO(g);
   TMAE_GO(l);
 #undef TMAE_GO

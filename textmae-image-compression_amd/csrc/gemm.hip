@@ -117,16 +117,41 @@ struct EpiUnpatchify {
   }
 };
 
+// out = resid + W·a + b, out-of-place (training keeps the block input for the LayerNorm backward)
+struct EpiResidualOut {
+  const float* resid;
+  float* out;
+  int ld;
+  const float* bias;
+  __device__ void batch(int, int) {}
+  __device__ void operator()(int m, int n, f32x4 v) const {
+    if (bias) v += load4f(bias + n);
+    store4(out + (size_t)m * ld + n, load4f(resid + (size_t)m * ld + n) + v);
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
+    f32x4 r0, r1;
+    load8f(resid + (size_t)m * ld + n, r0, r1);
+    if (bias) {
+      f32x4 b0, b1;
+      load8f(bias + n, b0, b1);
+      lo += b0; hi += b1;
+    }
+    store8(out + (size_t)m * ld + n, r0 + lo, r1 + hi);
+  }
+};
+
 template <typename T> static int check_k(int K) { return (K % Elt<T>::EPC) == 0; }
 
 // ------------------------------------------------------------------ linear
 template <typename T, class XS, bool GLDS>
 static int linear_epi(const T* W, int N, int K, const XS& xs, void* y, int y_f32, int ldy, float* y32, int ld32,
-                      const float* bias, int M, int act, hipStream_t st) {
+                      const float* bias, int M, int act, hipStream_t st, void* pre = nullptr, int ldp = 0) {
   const char* nm = "tmae_linear_fwd";
   if (y_f32) {
     auto e0 = make_store<float, 0>((float*)y, ldy, bias);
     auto e1 = make_store<float, 1>((float*)y, ldy, bias);
+    e0.pre = e1.pre = (float*)pre;
+    e0.ldp = e1.ldp = ldp;
     return act == TMAE_ACT_GELU ? launch_gemm<GLDS, T>(nm, W, 0, 0, N, K, xs, e1, M, 1, 1, st)
                                 : launch_gemm<GLDS, T>(nm, W, 0, 0, N, K, xs, e0, M, 1, 1, st);
   }
@@ -134,13 +159,16 @@ static int linear_epi(const T* W, int N, int K, const XS& xs, void* y, int y_f32
   auto e1 = make_store<T, 1>((T*)y, ldy, bias);
   e0.out32 = e1.out32 = y32;
   e0.ld32 = e1.ld32 = ld32;
+  e0.pre = e1.pre = (T*)pre;
+  e0.ldp = e1.ldp = ldp;
   return act == TMAE_ACT_GELU ? launch_gemm<GLDS, T>(nm, W, 0, 0, N, K, xs, e1, M, 1, 1, st)
                               : launch_gemm<GLDS, T>(nm, W, 0, 0, N, K, xs, e0, M, 1, 1, st);
 }
 
 template <typename T>
 static int linear_t(const void* x, int x_f32, int ldx, int G, int Gs, int off, const void* w, const float* bias,
-                    void* y, int y_f32, int ldy, float* y32, int ld32, int M, int N, int K, int act, hipStream_t st) {
+                    void* y, int y_f32, int ldy, float* y32, int ld32, int M, int N, int K, int act, hipStream_t st,
+                    void* pre = nullptr, int ldp = 0) {
   TMAE_REQUIRE(check_k<T>(K) && N % 4 == 0, "tmae_linear_fwd: K=%d must be a multiple of %d and N=%d of 4", K,
                Elt<T>::EPC, N);
   TMAE_REQUIRE(G > 0, "tmae_linear_fwd: row_group must be > 0");
@@ -148,10 +176,36 @@ static int linear_t(const void* x, int x_f32, int ldx, int G, int Gs, int off, c
   const T* W = (const T*)w;
   if (x_f32 && sizeof(T) != 4) {
     DenseSrcF32<T> xs{(const float*)x, ldx, M, K, G, Gs, off};
-    return linear_epi<T, DenseSrcF32<T>, false>(W, N, K, xs, y, y_f32, ldy, y32, ld32, bias, M, act, st);
+    return linear_epi<T, DenseSrcF32<T>, false>(W, N, K, xs, y, y_f32, ldy, y32, ld32, bias, M, act, st, pre, ldp);
   }
   DenseSrc<T> xs{(const T*)x, ldx, M, K, G, Gs, off, BStride{0, 0}};
-  return linear_epi<T, DenseSrc<T>, true>(W, N, K, xs, y, y_f32, ldy, y32, ld32, bias, M, act, st);
+  return linear_epi<T, DenseSrc<T>, true>(W, N, K, xs, y, y_f32, ldy, y32, ld32, bias, M, act, st, pre, ldp);
+}
+
+extern "C" int tmae_linear_fwd_pre(const void* x, int x_f32, int ldx, int row_group, int group_stride, int row_offset,
+                                   const void* w, const float* bias, void* y, int y_f32, int ldy, void* pre, int ldp,
+                                   int M, int N, int K, int act, int dtype, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMAE_BF16)
+    return linear_t<bf16>(x, x_f32, ldx, row_group, group_stride, row_offset, w, bias, y, y_f32, ldy, nullptr, 0, M,
+                          N, K, act, st, pre, ldp);
+  return linear_t<float>(x, 1, ldx, row_group, group_stride, row_offset, w, bias, y, 1, ldy, nullptr, 0, M, N, K, act,
+                         st, pre, ldp);
+}
+
+template <typename T>
+static int resid_out_t(const void* x, int ldx, const void* w, const float* bias, const float* r, float* out, int ld,
+                       int M, int N, int K, hipStream_t st) {
+  TMAE_REQUIRE(check_k<T>(K) && N % 4 == 0, "tmae_linear_residual_out: bad K=%d / N=%d", K, N);
+  DenseSrc<T> xs{(const T*)x, ldx, M, K, 1 << 30, 0, 0, BStride{0, 0}};
+  return launch_gemm<true, T>("tmae_linear_residual_out", (const T*)w, 0, 0, N, K, xs, EpiResidualOut{r, out, ld, bias},
+                              M, 1, 1, st);
+}
+
+extern "C" int tmae_linear_residual_out(const void* x, int ldx, const void* w, const float* bias, const float* resid,
+                                        float* out, int ld, int M, int N, int K, int dtype, void* stream) {
+  if (dtype == TMAE_BF16) return resid_out_t<bf16>(x, ldx, w, bias, resid, out, ld, M, N, K, (hipStream_t)stream);
+  return resid_out_t<float>(x, ldx, w, bias, resid, out, ld, M, N, K, (hipStream_t)stream);
 }
 
 extern "C" int tmae_linear_fwd(const void* x, int x_f32, int ldx, int row_group, int group_stride, int row_offset,

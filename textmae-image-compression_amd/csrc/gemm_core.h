@@ -669,16 +669,20 @@ template <typename OT, int ACT> struct EpiStore {
   int ld_add;
   float* out32;         // optional f32 copy
   int ld32;
-  BStride so, sb, sa, s32;
+  OT* pre;              // optional pre-activation copy (training keeps GELU inputs for the backward)
+  int ldp;
+  BStride so, sb, sa, s32, sp;
   __device__ void batch(int b1, int b2) {
     out += so.at(b1, b2);
     if (bias) bias += sb.at(b1, b2);
     if (addend) addend += sa.at(b1, b2);
     if (out32) out32 += s32.at(b1, b2);
+    if (pre) pre += sp.at(b1, b2);
   }
   __device__ void operator()(int m, int n, f32x4 v) const {
     if (bias) v += load4f(bias + n);
     if (addend) v += load4f(addend + (size_t)m * ld_add + n);
+    if (pre) store4(pre + (size_t)m * ldp + n, v);
     if (ACT == TMAE_ACT_GELU) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = gelu_erf(v[j]);
@@ -697,6 +701,7 @@ template <typename OT, int ACT> struct EpiStore {
       load8f(addend + (size_t)m * ld_add + n, a0, a1);
       lo += a0; hi += a1;
     }
+    if (pre) store8(pre + (size_t)m * ldp + n, lo, hi);
     if (ACT == TMAE_ACT_GELU) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) { lo[j] = gelu_erf(lo[j]); hi[j] = gelu_erf(hi[j]); }
@@ -710,6 +715,7 @@ template <typename OT, int ACT>
 static inline EpiStore<OT, ACT> make_store(OT* out, int ldo, const float* bias) {
   EpiStore<OT, ACT> e;
   e.out = out; e.ldo = ldo; e.bias = bias; e.addend = nullptr; e.ld_add = 0; e.out32 = nullptr; e.ld32 = 0;
-  e.so = e.sb = e.sa = e.s32 = BStride{0, 0};
+  e.pre = nullptr; e.ldp = 0;
+  e.so = e.sb = e.sa = e.s32 = e.sp = BStride{0, 0};
   return e;
 }

@@ -1,0 +1,1195 @@
+// Training-step kernels of the MCM hot path (reference MCM.forward + RateDistortionLoss backward, driven by
+// utils/engine.py:75-91): weight/data-gradient GEMMs, LayerNorm / GELU / entropy-model backward, layout
+// glue of the encoder/decoder, and the optimizer (Adam over flat buffers, clip_grad_norm_).
+// Entry points and the reference computation each differentiates: include/tmae.h ("training").
+#include "gemm_tn.h"
+
+static int tmae_wgrad_reduce(const float* ws, int splits, int M, int N, float* out, long long base, long long sm,
+                             long long sc, long long st, int cp, int accumulate, hipStream_t s);
+static int tmae_ln_fold(const float* part, int waves, int D, float* dg, float* db, int accumulate, hipStream_t st);
+
+// ================================================================== helpers
+__device__ __forceinline__ float gelu_grad(float x) {
+  // d/dx [0.5 x (1 + erf(x / sqrt2))] = Phi(x) + x phi(x); erf by Abramowitz-Stegun 7.1.26 like gelu_erf
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.44269504088896341f);  // exp(-x^2 / 2)
+  const float erf_abs = fmaf(-p, e, 1.0f);
+  const float cdf = x >= 0.0f ? 0.5f + 0.5f * erf_abs : 0.5f * p * e;
+  return cdf + x * e * 0.39894228040143267794f;
+}
+
+// ================================================================== weight gradients (split-K TN GEMM)
+template <typename T>
+static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
+  const int e = Elt<T>::EPC;
+  TMAE_REQUIRE(a.M % e == 0 && a.N % e == 0 && a.lda % e == 0, "tmae_wgrad: M=%d / N=%d / lda must be multiples of %d",
+               a.M, a.N, e);
+  TMAE_REQUIRE(a.a_G > 0 && a.o_cp > 0, "tmae_wgrad: bad row group / column period");
+  const bool bf = sizeof(T) == 2;
+  const TnPlan p = tn_plan(a.M, a.N, a.K, bf);
+  TMAE_REQUIRE((long long)p.splits * a.M * a.N <= a.work_elems, "tmae_wgrad: workspace too small (%lld < %lld)",
+               a.work_elems, (long long)p.splits * a.M * a.N);
+  KDenseSrc<T> as{(const T*)a.a, a.lda, a.M, a.a_G, a.a_Gs, a.a_off};
+  int rc;
+  if (a.b_conv) {
+    TMAE_REQUIRE(a.b_Cin % e == 0 && a.b_c1 % e == 0 && a.ldb % e == 0, "tmae_wgrad: conv channels");
+    TMAE_REQUIRE(a.N == 9 * a.b_Cin, "tmae_wgrad: N must be 9 * Cin for a 3x3 conv");
+    TMAE_REQUIRE(a.b_stride == 1 || a.b_stride == 2, "tmae_wgrad: stride %d", a.b_stride);
+    KConvSrc<T> bs;
+    bs.x1 = (const T*)a.b; bs.x2 = (const T*)a.b2; bs.c1 = a.b_c1; bs.ld1 = a.ldb; bs.ld2 = a.b_ld2; bs.Cin = a.b_Cin;
+    bs.H = a.b_H; bs.W = a.b_W; bs.stride = a.b_stride;
+    bs.Ho = (a.b_H + 2 - 3) / a.b_stride + 1; bs.Wo = (a.b_W + 2 - 3) / a.b_stride + 1; bs.cols = a.N;
+    rc = bf ? launch_tn_bf16(p, as, bs, a.work, a.M, a.N, a.K, st) : launch_tn_f32(p, as, bs, a.work, a.M, a.N, a.K, st);
+  } else {
+    TMAE_REQUIRE(a.ldb % e == 0 && a.b_G > 0, "tmae_wgrad: ldb");
+    KDenseSrc<T> bs{(const T*)a.b, a.ldb, a.N, a.b_G, a.b_Gs, a.b_off};
+    rc = bf ? launch_tn_bf16(p, as, bs, a.work, a.M, a.N, a.K, st) : launch_tn_f32(p, as, bs, a.work, a.M, a.N, a.K, st);
+  }
+  if (rc != TMAE_OK) return rc;
+  return tmae_wgrad_reduce(a.work, p.splits, a.M, a.N, a.out, a.o_base, a.o_sm, a.o_sc, a.o_st, a.o_cp, a.accumulate, st);
+}
+
+// fixed-order sum over the split slabs, scattered into the parameter's layout:
+// dst = base + m*sm + (n % cp)*sc + (n / cp)*st   (dense [M][N]: sm=N, sc=1, cp=N; conv [co][ci][3][3]
+// from columns tap*Cin + ci: sm=cin_total*9, sc=9, st=1, cp=Cin, base=ci_off*9; transposed: sm=1, sc=M)
+__global__ void __launch_bounds__(256)
+tn_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N, float* __restrict__ out, long long base,
+                 long long sm, long long sc, long long st, int cp, int accumulate) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long tot = (long long)M * N;
+  if (i >= tot) return;
+  const int m = (int)(i / N), n = (int)(i - (long long)m * N);
+  float s = 0.0f;
+  for (int k = 0; k < splits; ++k) s += ws[(size_t)k * tot + i];
+  const long long d = base + m * sm + (long long)(n % cp) * sc + (long long)(n / cp) * st;
+  out[d] = accumulate ? out[d] + s : s;
+}
+
+static int tmae_wgrad_reduce(const float* ws, int splits, int M, int N, float* out, long long base, long long sm,
+                             long long sc, long long st, int cp, int accumulate, hipStream_t s) {
+  const long long tot = (long long)M * N;
+  if (tot == 0) return TMAE_OK;
+  hipLaunchKernelGGL(tn_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, ws, splits, M, N, out,
+                     base, sm, sc, st, cp, accumulate);
+  TMAE_LAUNCH_CHECK("tmae_wgrad");
+}
+
+extern "C" int tmae_wgrad(const tmae_wgrad_args* a, int dtype, void* stream) {
+  TMAE_REQUIRE(a != nullptr && a->a && a->b && a->work && a->out, "tmae_wgrad: null argument");
+  if (a->M == 0 || a->N == 0) return TMAE_OK;
+  if (dtype == TMAE_BF16) return wgrad_t<bf16>(*a, (hipStream_t)stream);
+  return wgrad_t<float>(*a, (hipStream_t)stream);
+}
+
+extern "C" long long tmae_wgrad_workspace(int M, int N, int K, int dtype) {
+  const TnPlan p = tn_plan(M, N, K, dtype == TMAE_BF16);
+  return (long long)p.splits * M * N;
+}
+
+// ================================================================== data gradients (NT core on transposed weights)
+// out = acc * (pre ? gelu'(pre) : 1) in OT; acc32 (optional) += the same value in f32
+template <typename OT, typename PT> struct EpiDgrad {
+  OT* out;
+  int ldo;
+  const PT* pre;
+  int ldp;
+  float* acc;
+  int lda;
+  __device__ void batch(int, int) {}
+  __device__ void operator()(int m, int n, f32x4 v) const {
+    if (pre) {
+      const f32x4 p = load4f(pre + (size_t)m * ldp + n);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] *= gelu_grad(p[j]);
+    }
+    if (out) store4(out + (size_t)m * ldo + n, v);
+    if (acc) {
+      float* q = acc + (size_t)m * lda + n;
+      store4(q, load4f(q) + v);
+    }
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
+    if (pre) {
+      f32x4 p0, p1;
+      load8f(pre + (size_t)m * ldp + n, p0, p1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { lo[j] *= gelu_grad(p0[j]); hi[j] *= gelu_grad(p1[j]); }
+    }
+    if (out) store8(out + (size_t)m * ldo + n, lo, hi);
+    if (acc) {
+      float* q = acc + (size_t)m * lda + n;
+      f32x4 a0, a1;
+      load8f(q, a0, a1);
+      store8(q, a0 + lo, a1 + hi);
+    }
+  }
+};
+
+// columns [0, lim0) -> d0, [lim0, lim1) -> d1, [lim1, lim2) -> d2; each f32 +=  (conv input = channel concat)
+struct EpiRoute3 {
+  float* d[3];
+  int ld[3];
+  int lim[3];
+  __device__ void batch(int, int) {}
+  __device__ __forceinline__ float* at(int m, int n) const {
+    if (n < lim[0]) return d[0] + (size_t)m * ld[0] + n;
+    if (n < lim[1]) return d[1] + (size_t)m * ld[1] + (n - lim[0]);
+    return d[2] + (size_t)m * ld[2] + (n - lim[1]);
+  }
+  __device__ void operator()(int m, int n, f32x4 v) const {
+    float* q = at(m, n);
+    store4(q, load4f(q) + v);
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
+    operator()(m, n, lo);
+    operator()(m, n + 4, hi);
+  }
+};
+
+template <typename T>
+static int dgrad_linear_t(const void* dy, int ldy, int G, int Gs, int off, const void* wt, int M, int N, int K, void* out,
+                          int out_f32, int ldo, const void* pre, int ldp, float* acc, int lda, hipStream_t st) {
+  TMAE_REQUIRE(N % Elt<T>::EPC == 0 && K % 4 == 0 && ldy % Elt<T>::EPC == 0 && G > 0,
+               "tmae_dgrad_linear: N=%d / K=%d / ldy unsupported", N, K);
+  DenseSrc<T> xs{(const T*)dy, ldy, M, N, G, Gs, off, BStride{0, 0}};
+  const char* nm = "tmae_dgrad_linear";
+  if (out_f32 || !out) {
+    EpiDgrad<float, T> e{(float*)out, ldo, (const T*)pre, ldp, acc, lda};
+    return launch_gemm<true, T>(nm, (const T*)wt, 0, 0, K, N, xs, e, M, 1, 1, st);
+  }
+  EpiDgrad<T, T> e{(T*)out, ldo, (const T*)pre, ldp, acc, lda};
+  return launch_gemm<true, T>(nm, (const T*)wt, 0, 0, K, N, xs, e, M, 1, 1, st);
+}
+
+extern "C" int tmae_dgrad_linear(const void* dy, int ldy, int row_group, int group_stride, int row_offset,
+                                 const void* wt, int M, int N, int K, void* out, int out_f32, int ldo, const void* pre,
+                                 int ldp, float* acc32, int ld32, int dtype, void* stream) {
+  TMAE_REQUIRE(dy && wt && (out || acc32), "tmae_dgrad_linear: null argument");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMAE_BF16)
+    return dgrad_linear_t<bf16>(dy, ldy, row_group, group_stride, row_offset, wt, M, N, K, out, out_f32, ldo, pre, ldp,
+                                acc32, ld32, st);
+  return dgrad_linear_t<float>(dy, ldy, row_group, group_stride, row_offset, wt, M, N, K, out, 1, ldo, pre, ldp, acc32,
+                               ld32, st);
+}
+
+// ---------------------------------------------------------------- conv dgrad: transposed-conv row source
+// row m = input pixel (b, iy, ix); k = tap * Cout + co reads dY at the output pixel that saw (iy, ix)
+// through tap (ky, kx): oy = (iy + 1 - ky) / stride when integral and in range, else zero.
+template <typename T> struct ConvTSrc {
+  const T* dy;
+  int ldy, Cout, H, W, Ho, Wo, stride, rows, K;
+  float inv_cout;
+  struct Row { int b; int iy; int ix; bool ok; };
+  __device__ void batch(int, int) {}
+  __device__ Row row(int m) const {
+    if (m >= rows) return {0, 0, 0, false};
+    const int hw = H * W;
+    const int b = m / hw, rem = m - b * hw;
+    const int iy = rem / W;
+    return {b, iy, rem - iy * W, true};
+  }
+  __device__ const void* addr_k(const Row& r, int k) const {
+    if (!r.ok || k >= K) return g_tmae_zero_page;
+    int tap = (int)((float)k * inv_cout);
+    if (tap * Cout > k) --tap;
+    if ((tap + 1) * Cout <= k) ++tap;
+    const int co = k - tap * Cout;
+    const int ky = (tap * 11) >> 5;
+    int ty = r.iy + 1 - ky, tx = r.ix + 1 - (tap - 3 * ky);
+    if (ty < 0 || tx < 0) return g_tmae_zero_page;
+    if (stride == 2) {
+      if ((ty | tx) & 1) return g_tmae_zero_page;
+      ty >>= 1;
+      tx >>= 1;
+    }
+    if (ty >= Ho || tx >= Wo) return g_tmae_zero_page;
+    return dy + ((size_t)(r.b * Ho + ty) * Wo + tx) * ldy + co;
+  }
+  __device__ const void* addr(const Row& r, int kt, int c) const {
+    return addr_k(r, kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC);
+  }
+  __device__ uint4 load(const Row& r, int kt, int c) const { return *reinterpret_cast<const uint4*>(addr(r, kt, c)); }
+};
+
+template <typename T>
+static int conv_dgrad_t(const tmae_conv_dgrad_args& a, hipStream_t st) {
+  const int e = Elt<T>::EPC;
+  TMAE_REQUIRE(a.cout % e == 0 && a.ldy % e == 0 && a.cin % 4 == 0, "tmae_conv_dgrad: channels %d -> %d", a.cout,
+               a.cin);
+  TMAE_REQUIRE(a.stride == 1 || a.stride == 2, "tmae_conv_dgrad: stride %d", a.stride);
+  ConvTSrc<T> xs;
+  xs.dy = (const T*)a.dy; xs.ldy = a.ldy; xs.Cout = a.cout; xs.H = a.H; xs.W = a.W; xs.stride = a.stride;
+  xs.Ho = (a.H + 2 - 3) / a.stride + 1; xs.Wo = (a.W + 2 - 3) / a.stride + 1;
+  xs.rows = a.n * a.H * a.W; xs.K = 9 * a.cout; xs.inv_cout = 1.0f / (float)a.cout;
+  const int M = xs.rows, K = xs.K, N = a.cin;
+  const char* nm = "tmae_conv_dgrad";
+  if (a.acc[0]) {
+    TMAE_REQUIRE(a.lim[0] % 8 == 0 && a.lim[1] % 8 == 0 && a.lim[2] == a.cin && a.lim[0] <= a.lim[1] &&
+                     a.lim[1] <= a.lim[2],
+                 "tmae_conv_dgrad: route limits");
+    TMAE_REQUIRE((a.lim[1] == a.lim[0] || a.acc[1]) && (a.lim[2] == a.lim[1] || a.acc[2]),
+                 "tmae_conv_dgrad: route destination missing");
+    EpiRoute3 r;
+    for (int i = 0; i < 3; ++i) { r.d[i] = a.acc[i]; r.ld[i] = a.ld_acc[i]; r.lim[i] = a.lim[i]; }
+    return launch_gemm<true, T>(nm, (const T*)a.wd, 0, 0, N, K, xs, r, M, 1, 1, st);
+  }
+  if (a.out_f32) {
+    EpiDgrad<float, T> g{(float*)a.out, a.ldo, (const T*)a.pre, a.ldp, nullptr, 0};
+    return launch_gemm<true, T>(nm, (const T*)a.wd, 0, 0, N, K, xs, g, M, 1, 1, st);
+  }
+  EpiDgrad<T, T> g{(T*)a.out, a.ldo, (const T*)a.pre, a.ldp, nullptr, 0};
+  return launch_gemm<true, T>(nm, (const T*)a.wd, 0, 0, N, K, xs, g, M, 1, 1, st);
+}
+
+extern "C" int tmae_conv_dgrad(const tmae_conv_dgrad_args* a, int dtype, void* stream) {
+  TMAE_REQUIRE(a && a->dy && a->wd && (a->out || a->acc[0]), "tmae_conv_dgrad: null argument");
+  if (dtype == TMAE_BF16) return conv_dgrad_t<bf16>(*a, (hipStream_t)stream);
+  TMAE_REQUIRE(a->out_f32 || a->acc[0], "tmae_conv_dgrad: the f32 path writes f32 outputs");
+  return conv_dgrad_t<float>(*a, (hipStream_t)stream);
+}
+
+// ================================================================== weight re-layout + cast
+// dst (contiguous, dims d0..d3) = cast(src[i0*s0 + i1*s1 + i2*s2 + i3*s3]); src f32
+template <typename OT>
+__global__ void __launch_bounds__(256)
+relayout_kernel(const float* __restrict__ src, OT* __restrict__ dst, int d1, int d2, int d3, long long s0, long long s1,
+                long long s2, long long s3, long long total) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  long long r = i;
+  const int i3 = (int)(r % d3); r /= d3;
+  const int i2 = (int)(r % d2); r /= d2;
+  const int i1 = (int)(r % d1);
+  const long long i0 = r / d1;
+  dst[i] = to_out<OT>(src[i0 * s0 + i1 * s1 + i2 * s2 + i3 * s3]);
+}
+
+// 2-D transpose-cast through LDS: dst[c][r] = src[r][c] (src rows of ld_src floats), R rows, C columns
+template <typename OT>
+__global__ void __launch_bounds__(256)
+transpose_kernel(const float* __restrict__ src, int ld_src, OT* __restrict__ dst, int R, int C) {
+  __shared__ float t[32][33];
+  const int c0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, c = c0 + tx;
+    t[k][tx] = (r < R && c < C) ? src[(size_t)r * ld_src + c] : 0.0f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, r = r0 + tx;
+    if (c < C && r < R) dst[(size_t)c * R + r] = to_out<OT>(t[tx][k]);
+  }
+}
+
+extern "C" int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0, int d1, int d2, int d3, long long s0,
+                             long long s1, long long s2, long long s3, void* stream) {
+  TMAE_REQUIRE(src && dst && d0 >= 0 && d1 > 0 && d2 > 0 && d3 > 0, "tmae_relayout: bad arguments");
+  const long long total = (long long)d0 * d1 * d2 * d3;
+  if (total == 0) return TMAE_OK;
+  hipStream_t st = (hipStream_t)stream;
+  // a plain 2-D transpose (dst[i0][i3] = src[i3 * ld + i0]) goes through the LDS tile: coalesced both ways
+  if (d1 == 1 && d2 == 1 && s0 == 1 && s3 >= d0) {
+    const dim3 grid(ceil_div(d0, 32), ceil_div(d3, 32));
+    if (dst_dtype == TMAE_BF16)
+      hipLaunchKernelGGL(transpose_kernel<bf16>, grid, dim3(256), 0, st, src, (int)s3, (bf16*)dst, d3, d0);
+    else
+      hipLaunchKernelGGL(transpose_kernel<float>, grid, dim3(256), 0, st, src, (int)s3, (float*)dst, d3, d0);
+    TMAE_LAUNCH_CHECK("tmae_relayout");
+  }
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (dst_dtype == TMAE_BF16)
+    hipLaunchKernelGGL(relayout_kernel<bf16>, grid, dim3(256), 0, st, src, (bf16*)dst, d1, d2, d3, s0, s1, s2, s3, total);
+  else
+    hipLaunchKernelGGL(relayout_kernel<float>, grid, dim3(256), 0, st, src, (float*)dst, d1, d2, d3, s0, s1, s2, s3,
+                       total);
+  TMAE_LAUNCH_CHECK("tmae_relayout");
+}
+
+// ================================================================== column sums (bias gradients)
+// part[split][c] = sum over this split's rows r of x[src_row(r)][c]; src_row = (r / G) * Gs + off + r % G
+template <typename T>
+__global__ void __launch_bounds__(256)
+colsum_partial_kernel(const T* __restrict__ x, int ld, int rows, int C, int G, int Gs, int off, int rows_per_split,
+                      float* __restrict__ part) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  const int r0 = blockIdx.y * rows_per_split, r1 = min(rows, r0 + rows_per_split);
+  float s = 0.0f;
+  for (int r = r0; r < r1; ++r) {
+    const int sr = (r / G) * Gs + off + (r % G);
+    s += (float)x[(size_t)sr * ld + c];
+  }
+  part[(size_t)blockIdx.y * C + c] = s;
+}
+
+__global__ void __launch_bounds__(256)
+colsum_final_kernel(const float* __restrict__ part, int splits, int C, float* __restrict__ out, int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.0f;
+  for (int k = 0; k < splits; ++k) s += part[(size_t)k * C + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+extern "C" int tmae_colsum(const void* x, int x_dtype, int ld, int rows, int C, int row_group, int group_stride,
+                           int row_offset, float* work, long long work_elems, float* out, int accumulate, void* stream) {
+  TMAE_REQUIRE(x && out && work && row_group > 0, "tmae_colsum: bad arguments");
+  if (C == 0) return TMAE_OK;
+  hipStream_t st = (hipStream_t)stream;
+  int splits = std::max(1, std::min(256, rows / 32));
+  while ((long long)splits * C > work_elems && splits > 1) splits /= 2;
+  TMAE_REQUIRE((long long)splits * C <= work_elems, "tmae_colsum: workspace too small");
+  const int rps = ceil_div(std::max(rows, 1), splits);
+  const dim3 grid(ceil_div(C, 256), splits);
+  if (x_dtype == TMAE_BF16)
+    hipLaunchKernelGGL(colsum_partial_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ld, rows, C, row_group,
+                       group_stride, row_offset, rps, work);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<float>, grid, dim3(256), 0, st, (const float*)x, ld, rows, C, row_group,
+                       group_stride, row_offset, rps, work);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, work, splits, C, out, accumulate);
+  TMAE_LAUNCH_CHECK("tmae_colsum");
+}
+
+// ================================================================== LayerNorm backward
+// x rows remapped like the forward (source row sr = (r / G) * Gs + off + r % G); dy dense [rows][D] f32.
+// dx lands at row sr of dx32 (f32; + dres[sr] when given) and of dxop (operand dtype copy, optional).
+// Each wave walks a contiguous run of rows and keeps its dgamma / dbeta partial in registers -> part.
+template <typename OT, int VPL>
+__global__ void __launch_bounds__(256)
+layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ dy,
+                     const float* __restrict__ dres, float* __restrict__ dx32, OT* __restrict__ dxop, int rows, int D,
+                     int G, int Gs, int off, float eps, int rows_per_wave, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63;
+  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nch = D >> 2;
+  f32x4 dg[VPL], db[VPL], gm[VPL];
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    dg[i] = db[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int c = lane + 64 * i;
+    gm[i] = c < nch ? load4f(gamma + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int r0 = wave * rows_per_wave, r1 = min(rows, r0 + rows_per_wave);
+  for (int r = r0; r < r1; ++r) {
+    const int sr = (r / G) * Gs + off + (r % G);
+    const float* xr = x + (size_t)sr * D;
+    const float* gr = dy + (size_t)r * D;
+    f32x4 v[VPL], g[VPL];
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + 64 * i;
+      v[i] = c < nch ? load4f(xr + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      g[i] = c < nch ? load4f(gr + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s / (float)D;
+    float q = 0.0f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = v[i][j] - mean;
+          q += d * d;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    const float rstd = 1.0f / sqrtf(q / (float)D + eps);
+    float sa = 0.0f, sb = 0.0f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xh = (v[i][j] - mean) * rstd;
+          v[i][j] = xh;
+          const float gg = g[i][j] * gm[i][j];
+          sa += gg;
+          sb += gg * xh;
+          dg[i][j] += g[i][j] * xh;
+          db[i][j] += g[i][j];
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      sa += __shfl_xor(sa, o);
+      sb += __shfl_xor(sb, o);
+    }
+    sa /= (float)D;
+    sb /= (float)D;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = rstd * (g[i][j] * gm[i][j] - sa - v[i][j] * sb);
+        if (dres) o += load4f(dres + (size_t)sr * D + 4 * c);
+        store4(dx32 + (size_t)sr * D + 4 * c, o);
+        if (dxop) store4(dxop + (size_t)sr * D + 4 * c, o);
+      }
+    }
+  }
+  float* pw = part + (size_t)wave * 2 * D;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      store4(pw + 4 * c, dg[i]);
+      store4(pw + D + 4 * c, db[i]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+ln_fold_kernel(const float* __restrict__ part, int waves, int D, float* __restrict__ dg, float* __restrict__ db,
+               int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= 2 * D) return;
+  float s = 0.0f;
+  for (int k = 0; k < waves; ++k) s += part[(size_t)k * 2 * D + c];
+  float* o = c < D ? dg + c : db + (c - D);
+  *o = accumulate ? *o + s : s;
+}
+
+static int tmae_ln_fold(const float* part, int waves, int D, float* dg, float* db, int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(ln_fold_kernel, dim3(ceil_div(2 * D, 256)), dim3(256), 0, st, part, waves, D, dg, db, accumulate);
+  TMAE_LAUNCH_CHECK("tmae_layernorm_bwd");
+}
+
+extern "C" int tmae_layernorm_bwd(const float* x, const float* gamma, const float* dy, const float* dres, float* dx32,
+                                  void* dxop, int op_dtype, int rows, int D, int row_group, int group_stride,
+                                  int row_offset, float eps, float* work, long long work_elems, float* dgamma,
+                                  float* dbeta, int accumulate, void* stream) {
+  TMAE_REQUIRE(D % 4 == 0 && D <= 2048 && row_group > 0, "tmae_layernorm_bwd: D=%d", D);
+  TMAE_REQUIRE(x && gamma && dy && dx32 && work && dgamma && dbeta, "tmae_layernorm_bwd: null argument");
+  hipStream_t st = (hipStream_t)stream;
+  int waves = std::min(1024, std::max(4, rows / 8));
+  while ((long long)(waves + 4) * 2 * D > work_elems && waves > 4) waves /= 2;
+  const int rpw = ceil_div(std::max(rows, 1), waves);
+  waves = ceil_div(ceil_div(std::max(rows, 1), rpw), 4) * 4;
+  TMAE_REQUIRE((long long)waves * 2 * D <= work_elems, "tmae_layernorm_bwd: workspace too small");
+  const int vpl = ceil_div(D / 4, 64);
+  const dim3 grid(waves / 4);
+#define TMAE_LNB(OT, V)                                                                                              \
+  hipLaunchKernelGGL((layernorm_bwd_kernel<OT, V>), grid, dim3(256), 0, st, x, gamma, dy, dres, dx32, (OT*)dxop, rows, \
+                     D, row_group, group_stride, row_offset, eps, rpw, work)
+#define TMAE_LNB_V(OT)          \
+  if (vpl <= 1) TMAE_LNB(OT, 1);  \
+  else if (vpl <= 2) TMAE_LNB(OT, 2); \
+  else if (vpl <= 3) TMAE_LNB(OT, 3); \
+  else if (vpl <= 4) TMAE_LNB(OT, 4); \
+  else TMAE_LNB(OT, 8)
+  if (op_dtype == TMAE_BF16) {
+    TMAE_LNB_V(bf16);
+  } else {
+    TMAE_LNB_V(float);
+  }
+#undef TMAE_LNB_V
+#undef TMAE_LNB
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    tmae_set_error(TMAE_EHIP, "tmae_layernorm_bwd: launch failed: %s", hipGetErrorString(e));
+    return TMAE_EHIP;
+  }
+  return tmae_ln_fold(work, waves, D, dgamma, dbeta, accumulate, st);
+}
+
+// ================================================================== elementwise backward pieces
+// subpel_conv3x3 backward (compressai PixelShuffle(2) after the conv, then GELU): dpre [n*H*W][4c] (conv
+// channel co = c*4 + i*2 + j of pixel (y, x)) = dy_ps[(2y+i, 2x+j)][c] * gelu'(pre_ps) (pre optional)
+template <typename GT, typename T>
+__global__ void __launch_bounds__(256)
+unshuffle_bwd_kernel(const GT* __restrict__ dy, int ldy, const T* __restrict__ pre, int ldp, T* __restrict__ out,
+                     int n, int H, int W, int C4) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long total = (long long)n * H * W * C4;
+  if (i >= total) return;
+  const int co = (int)(i % C4);
+  const long long m = i / C4;
+  const int hw = H * W;
+  const int b = (int)(m / hw), rem = (int)(m - (long long)b * hw);
+  const int y = rem / W, x = rem - y * W;
+  const int c = co >> 2, si = (co >> 1) & 1, sj = co & 1;
+  const size_t at = ((size_t)(b * 2 * H + 2 * y + si) * 2 * W + 2 * x + sj);
+  float g = (float)dy[at * ldy + c];
+  if (pre) g *= gelu_grad((float)pre[at * ldp + c]);
+  out[i] = to_out<T>(g);
+}
+
+extern "C" int tmae_unshuffle_bwd(const void* dy, int dy_f32, int ldy, const void* pre, int ldp, void* out, int n,
+                                  int H, int W, int C4, int dtype, void* stream) {
+  TMAE_REQUIRE(C4 % 4 == 0, "tmae_unshuffle_bwd: channels %d", C4);
+  const long long total = (long long)n * H * W * C4;
+  if (total == 0) return TMAE_OK;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+#define TMAE_UB(GT, T)                                                                                             \
+  hipLaunchKernelGGL((unshuffle_bwd_kernel<GT, T>), grid, dim3(256), 0, st, (const GT*)dy, ldy, (const T*)pre, ldp, \
+                     (T*)out, n, H, W, C4)
+  if (dtype == TMAE_BF16) {
+    if (dy_f32) TMAE_UB(float, bf16);
+    else TMAE_UB(bf16, bf16);
+  } else {
+    TMAE_UB(float, float);
+  }
+#undef TMAE_UB
+  TMAE_LAUNCH_CHECK("tmae_unshuffle_bwd");
+}
+
+// y = gelu(pre) elementwise backward: out = dy * gelu'(pre)  (layers whose dgrad epilogue cannot fuse it)
+template <typename GT, typename T>
+__global__ void __launch_bounds__(256)
+gelu_bwd_kernel(const GT* __restrict__ dy, const T* __restrict__ pre, T* __restrict__ out, long long total) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  out[i] = to_out<T>((float)dy[i] * gelu_grad((float)pre[i]));
+}
+
+extern "C" int tmae_gelu_bwd(const void* dy, int dy_f32, const void* pre, void* out, long long total, int dtype,
+                             void* stream) {
+  if (total <= 0) return TMAE_OK;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == TMAE_BF16) {
+    if (dy_f32)
+      hipLaunchKernelGGL((gelu_bwd_kernel<float, bf16>), grid, dim3(256), 0, st, (const float*)dy, (const bf16*)pre,
+                         (bf16*)out, total);
+    else
+      hipLaunchKernelGGL((gelu_bwd_kernel<bf16, bf16>), grid, dim3(256), 0, st, (const bf16*)dy, (const bf16*)pre,
+                         (bf16*)out, total);
+  } else {
+    hipLaunchKernelGGL((gelu_bwd_kernel<float, float>), grid, dim3(256), 0, st, (const float*)dy, (const float*)pre,
+                       (float*)out, total);
+  }
+  TMAE_LAUNCH_CHECK("tmae_gelu_bwd");
+}
+
+// last lrp_transform conv (MCM.py:779-783): y_hat = y_hat_pre + 0.5 tanh(t).  g = g32 (f32, optional) + g16
+// (operand dtype, optional) is the y_hat gradient; dt = g * 0.5 (1 - tanh(t)^2) (operand dtype) and
+// gsum = g (f32, optional: the y_hat_pre gradient the GaussianConditional backward continues with)
+template <typename T>
+__global__ void __launch_bounds__(256)
+lrp_bwd_kernel(const float* __restrict__ g32, int ld32, const T* __restrict__ g16, int ld16, const float* __restrict__ t,
+               int ldt, T* __restrict__ dt, int lddt, float* __restrict__ gsum, int ldgs, int rows, int C) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * C) return;
+  const int m = i / C, c = i - m * C;
+  float g = g32 ? g32[(size_t)m * ld32 + c] : 0.0f;
+  if (g16) g += (float)g16[(size_t)m * ld16 + c];
+  const float th = tanhf(t[(size_t)m * ldt + c]);
+  dt[(size_t)m * lddt + c] = to_out<T>(g * 0.5f * (1.0f - th * th));
+  if (gsum) gsum[(size_t)m * ldgs + c] = g;
+}
+
+extern "C" int tmae_lrp_bwd(const float* g32, int ld32, const void* g16, int ld16, const float* t, int ldt, void* dt,
+                            int lddt, float* gsum, int ldgs, int rows, int C, int dtype, void* stream) {
+  if (rows * C == 0) return TMAE_OK;
+  const dim3 grid(ceil_div(rows * C, 256));
+  if (dtype == TMAE_BF16)
+    hipLaunchKernelGGL(lrp_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, g32, ld32, (const bf16*)g16, ld16,
+                       t, ldt, (bf16*)dt, lddt, gsum, ldgs, rows, C);
+  else
+    hipLaunchKernelGGL(lrp_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, g32, ld32, (const float*)g16,
+                       ld16, t, ldt, (float*)dt, lddt, gsum, ldgs, rows, C);
+  TMAE_LAUNCH_CHECK("tmae_lrp_bwd");
+}
+
+// strided 2-D copy of rows x cols elements (esz = 2 or 4 bytes)
+template <typename E>
+__global__ void __launch_bounds__(256)
+copy2d_kernel(const E* __restrict__ src, int lds, E* __restrict__ dst, int ldd, int rows, int cols) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)rows * cols) return;
+  const int r = (int)(i / cols), c = (int)(i - (long long)r * cols);
+  dst[(size_t)r * ldd + c] = src[(size_t)r * lds + c];
+}
+
+extern "C" int tmae_copy2d(const void* src, int lds, void* dst, int ldd, int rows, int cols, int esz, void* stream) {
+  TMAE_REQUIRE(esz == 2 || esz == 4, "tmae_copy2d: element size %d", esz);
+  const long long total = (long long)rows * cols;
+  if (total <= 0) return TMAE_OK;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (esz == 2)
+    hipLaunchKernelGGL(copy2d_kernel<uint16_t>, grid, dim3(256), 0, (hipStream_t)stream, (const uint16_t*)src, lds,
+                       (uint16_t*)dst, ldd, rows, cols);
+  else
+    hipLaunchKernelGGL(copy2d_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, (const float*)src, lds,
+                       (float*)dst, ldd, rows, cols);
+  TMAE_LAUNCH_CHECK("tmae_copy2d");
+}
+
+// GaussianConditional backward for one slice (compressai 1.2.4 _likelihood + LowerBound semantics,
+// MCM.py:771-776).  Element (pixel m, channel c) of slice channel ch = yoff + c.
+//   lik = LB_1e-9( Phi((1/2 - v)/s) - Phi((-1/2 - v)/s) ),  v = |x~ - mu|,  s = LB_0.11(sigma)
+//   x~ = y + noise (train) | round(y - mu) + mu (eval);  y_hat_pre = STE(y - mu) + mu
+// LowerBound backward passes the gradient where x >= bound or grad < 0.
+// Outputs: dy (f32, +=), dmu / dsigma (operand dtype, [m][ldd]).
+template <typename T>
+__global__ void __launch_bounds__(256)
+gc_bwd_kernel(const float* __restrict__ y, int ldy, int yoff, const float* __restrict__ mu,
+              const float* __restrict__ sigma, int ld_ms, const float* __restrict__ noise, int Mtot,
+              const float* __restrict__ glik, const float* __restrict__ gyp, int ldg, float* __restrict__ dy, int lddy,
+              T* __restrict__ dmu, T* __restrict__ dsig, int ldd, int n, int HW, int sw) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * HW * sw) return;
+  const int m = i / sw, c = i - m * sw;
+  const int ch = yoff + c;
+  const int b = m / HW, pix = m - b * HW;
+  const size_t nchw = ((size_t)b * Mtot + ch) * HW + pix;
+  const float yv = y[(size_t)m * ldy + ch];
+  const float mv = mu[(size_t)m * ld_ms + c];
+  const float sr = sigma[(size_t)m * ld_ms + c];
+  const float xt = noise ? yv + noise[nchw] : rintf(yv - mv) + mv;
+  const float s = fmaxf(sr, 0.11f);
+  const float dd = xt - mv;
+  const float v = fabsf(dd);
+  const float a = (0.5f - v) / s, bb = (-0.5f - v) / s;
+  const float k = -0.70710678118654752440f;
+  const float lik = 0.5f * erfcf(k * a) - 0.5f * erfcf(k * bb);
+  float g = glik ? glik[nchw] : 0.0f;
+  if (!(lik >= 1e-9f || g < 0.0f)) g = 0.0f;
+  const float inv_sqrt2pi = 0.39894228040143267794f;
+  const float pa = inv_sqrt2pi * expf(-0.5f * a * a), pb = inv_sqrt2pi * expf(-0.5f * bb * bb);
+  const float dv = g * (pb - pa) / s;
+  float ds = g * (bb * pb - a * pa) / s;
+  if (!(sr >= 0.11f || ds < 0.0f)) ds = 0.0f;
+  const float sg = dd > 0.0f ? 1.0f : (dd < 0.0f ? -1.0f : 0.0f);
+  const float ddd = dv * sg;  // d lik / d (x~ - mu)
+  float dyv = gyp ? gyp[(size_t)m * ldg + ch] : 0.0f;  // STE path of y_hat_pre
+  float dmv = -ddd;
+  if (noise) dyv += ddd;
+  else dmv += ddd;  // eval: x~ = round(y - mu) + mu moves with mu, round has no gradient
+  dy[(size_t)m * lddy + ch] += dyv;
+  dmu[(size_t)m * ldd + c] = to_out<T>(dmv);
+  dsig[(size_t)m * ldd + c] = to_out<T>(ds);
+}
+
+extern "C" int tmae_gc_bwd(const float* y, int ldy, int yoff, const float* mu, const float* sigma, int ld_ms,
+                           const float* noise, int Mtot, const float* glik, const float* gyp, int ldg, float* dy,
+                           int lddy, void* dmu, void* dsigma, int ldd, int n, int HW, int sw, int dtype, void* stream) {
+  const int total = n * HW * sw;
+  if (total == 0) return TMAE_OK;
+  const dim3 grid(ceil_div(total, 256));
+  if (dtype == TMAE_BF16)
+    hipLaunchKernelGGL(gc_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, y, ldy, yoff, mu, sigma, ld_ms,
+                       noise, Mtot, glik, gyp, ldg, dy, lddy, (bf16*)dmu, (bf16*)dsigma, ldd, n, HW, sw);
+  else
+    hipLaunchKernelGGL(gc_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, y, ldy, yoff, mu, sigma, ld_ms,
+                       noise, Mtot, glik, gyp, ldg, dy, lddy, (float*)dmu, (float*)dsigma, ldd, n, HW, sw);
+  TMAE_LAUNCH_CHECK("tmae_gc_bwd");
+}
+
+// ================================================================== EntropyBottleneck backward
+// compressai 1.2.4 _logits_cumulative / _likelihood (MCM.py:741), per channel c (one workgroup):
+//   h = softplus(M0) v + b0; h += tanh(F0) tanh(h); [h = softplus(Ml) h + bl; h += tanh(Fl) tanh(h)] x3;
+//   f = softplus(M4) h + b4;  lik = LB_1e-9 |sigmoid(s f(x+1/2)) - sigmoid(s f(x-1/2))|, s = -sign(sum) detached
+// Gradients: dz (x = z + noise in training; the STE z_hat adds its own pass-through gz) and every density
+// parameter of the channel (softplus' = sigmoid below the threshold 20, tanh' = 1 - tanh^2).
+struct EbCh {
+  float sp0[3], b0[3], tf0[3];
+  float sp[3][9], bl[3][3], tf[3][3];
+  float sp4[3], b4;
+};
+typedef EbCh EbGrad;  // gradient w.r.t. the same packed (transformed) quantities
+
+__device__ __forceinline__ float eb_softplus(float x) { return x > 20.0f ? x : log1pf(expf(x)); }
+__device__ __forceinline__ float eb_softplus_grad(float x) { return x > 20.0f ? 1.0f : 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float eb_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ void eb_load(const tmae_eb_params& p, int c, EbCh& w) {
+  for (int j = 0; j < 3; ++j) {
+    w.sp0[j] = eb_softplus(p.matrix[0][c * 3 + j]);
+    w.b0[j] = p.bias[0][c * 3 + j];
+    w.tf0[j] = tanhf(p.factor[0][c * 3 + j]);
+  }
+  for (int l = 0; l < 3; ++l) {
+    for (int e = 0; e < 9; ++e) w.sp[l][e] = eb_softplus(p.matrix[l + 1][c * 9 + e]);
+    for (int j = 0; j < 3; ++j) {
+      w.bl[l][j] = p.bias[l + 1][c * 3 + j];
+      w.tf[l][j] = tanhf(p.factor[l + 1][c * 3 + j]);
+    }
+  }
+  for (int k = 0; k < 3; ++k) w.sp4[k] = eb_softplus(p.matrix[4][c * 3 + k]);
+  w.b4 = p.bias[4][c];
+}
+
+// f(v); for upstream gradient go also accumulates the packed-parameter gradients (gr != null) and df/dv
+__device__ float eb_fwd_bwd(const EbCh& w, float v, float go, EbGrad* gr, float* dv) {
+  float u[4][3], th[4][3], h[4][3];
+  for (int j = 0; j < 3; ++j) {
+    u[0][j] = w.sp0[j] * v + w.b0[j];
+    th[0][j] = tanhf(u[0][j]);
+    h[0][j] = u[0][j] + w.tf0[j] * th[0][j];
+  }
+  for (int l = 0; l < 3; ++l) {
+    for (int i = 0; i < 3; ++i) {
+      u[l + 1][i] = (w.sp[l][3 * i] * h[l][0] + w.sp[l][3 * i + 1] * h[l][1] + w.sp[l][3 * i + 2] * h[l][2]) + w.bl[l][i];
+      th[l + 1][i] = tanhf(u[l + 1][i]);
+      h[l + 1][i] = u[l + 1][i] + w.tf[l][i] * th[l + 1][i];
+    }
+  }
+  const float f = (w.sp4[0] * h[3][0] + w.sp4[1] * h[3][1] + w.sp4[2] * h[3][2]) + w.b4;
+  if (!gr && !dv) return f;
+  float dh[3];
+  for (int k = 0; k < 3; ++k) {
+    dh[k] = go * w.sp4[k];
+    if (gr) gr->sp4[k] += go * h[3][k];
+  }
+  if (gr) gr->b4 += go;
+  for (int l = 2; l >= 0; --l) {
+    float du[3], dprev[3] = {0.f, 0.f, 0.f};
+    for (int i = 0; i < 3; ++i) {
+      du[i] = dh[i] * (1.0f + w.tf[l][i] * (1.0f - th[l + 1][i] * th[l + 1][i]));
+      if (gr) {
+        gr->tf[l][i] += dh[i] * th[l + 1][i];
+        gr->bl[l][i] += du[i];
+      }
+      for (int j = 0; j < 3; ++j) {
+        if (gr) gr->sp[l][3 * i + j] += du[i] * h[l][j];
+        dprev[j] += w.sp[l][3 * i + j] * du[i];
+      }
+    }
+    for (int j = 0; j < 3; ++j) dh[j] = dprev[j];
+  }
+  float d = 0.0f;
+  for (int j = 0; j < 3; ++j) {
+    const float du = dh[j] * (1.0f + w.tf0[j] * (1.0f - th[0][j] * th[0][j]));
+    if (gr) {
+      gr->tf0[j] += dh[j] * th[0][j];
+      gr->b0[j] += du;
+      gr->sp0[j] += du * v;
+    }
+    d += w.sp0[j] * du;
+  }
+  if (dv) *dv = d;
+  return f;
+}
+
+#define EB_NG 58
+
+__global__ void __launch_bounds__(256)
+eb_bwd_kernel(tmae_eb_params p, const float* __restrict__ z, const float* __restrict__ noise,
+              const float* __restrict__ glik, const float* __restrict__ gzhat, float* __restrict__ dz, int C, int HW,
+              int n, tmae_eb_params g, int accumulate) {
+  const int c = blockIdx.x;
+  EbCh w;
+  eb_load(p, c, w);
+  const float med = p.quantiles[c * 3 + 1];
+  EbGrad gr;
+  float* gf = reinterpret_cast<float*>(&gr);
+  for (int k = 0; k < EB_NG; ++k) gf[k] = 0.0f;
+  const int total = n * HW;
+  for (int e = threadIdx.x; e < total; e += 256) {
+    const int b = e / HW, pix = e - b * HW;
+    const size_t nhwc = ((size_t)b * HW + pix) * C + c;
+    const size_t nchw = ((size_t)b * C + c) * HW + pix;
+    const float zv = z[nhwc];
+    const float x = noise ? zv + noise[nchw] : rintf(zv - med) + med;
+    const float lower = eb_fwd_bwd(w, x - 0.5f, 0.0f, nullptr, nullptr);
+    const float upper = eb_fwd_bwd(w, x + 0.5f, 0.0f, nullptr, nullptr);
+    const float sum = lower + upper;
+    const float s = sum > 0.0f ? -1.0f : (sum < 0.0f ? 1.0f : 0.0f);
+    const float su = eb_sigmoid(s * upper), sl = eb_sigmoid(s * lower);
+    const float raw = fabsf(su - sl);
+    float gl = glik ? glik[nchw] : 0.0f;
+    if (!(raw >= 1e-9f || gl < 0.0f)) gl = 0.0f;
+    const float sg = su > sl ? 1.0f : (su < sl ? -1.0f : 0.0f);
+    const float gu = gl * sg * s * su * (1.0f - su);
+    const float glo = -gl * sg * s * sl * (1.0f - sl);
+    float dvu = 0.0f, dvl = 0.0f;
+    if (gu != 0.0f) eb_fwd_bwd(w, x + 0.5f, gu, &gr, &dvu);
+    if (glo != 0.0f) eb_fwd_bwd(w, x - 0.5f, glo, &gr, &dvl);
+    float d = gzhat ? gzhat[nhwc] : 0.0f;  // quantize_ste pass-through (MCM.py:742-744)
+    if (noise) d += dvu + dvl;             // eval: x = round(z - med) + med, no gradient to z
+    dz[nhwc] = d;
+  }
+  // workgroup reduction of the 58 parameter gradients
+  __shared__ float red[EB_NG][4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int k = 0; k < EB_NG; ++k) {
+    float v = gf[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) red[k][wv] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < EB_NG) {
+    const int k = threadIdx.x;
+    const float v = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+    // packed index -> (tensor element, chain rule of softplus / tanh back to the raw parameter)
+    float* dst;
+    float dval;
+    if (k < 3) {
+      dst = (float*)g.matrix[0] + c * 3 + k;
+      dval = v * eb_softplus_grad(p.matrix[0][c * 3 + k]);
+    } else if (k < 6) {
+      dst = (float*)g.bias[0] + c * 3 + (k - 3);
+      dval = v;
+    } else if (k < 9) {
+      const float t = tanhf(p.factor[0][c * 3 + k - 6]);
+      dst = (float*)g.factor[0] + c * 3 + (k - 6);
+      dval = v * (1.0f - t * t);
+    } else if (k < 36) {
+      const int l = (k - 9) / 9, e = (k - 9) % 9;
+      dst = (float*)g.matrix[l + 1] + c * 9 + e;
+      dval = v * eb_softplus_grad(p.matrix[l + 1][c * 9 + e]);
+    } else if (k < 45) {
+      const int l = (k - 36) / 3, j = (k - 36) % 3;
+      dst = (float*)g.bias[l + 1] + c * 3 + j;
+      dval = v;
+    } else if (k < 54) {
+      const int l = (k - 45) / 3, j = (k - 45) % 3;
+      const float t = tanhf(p.factor[l + 1][c * 3 + j]);
+      dst = (float*)g.factor[l + 1] + c * 3 + j;
+      dval = v * (1.0f - t * t);
+    } else if (k < 57) {
+      dst = (float*)g.matrix[4] + c * 3 + (k - 54);
+      dval = v * eb_softplus_grad(p.matrix[4][c * 3 + k - 54]);
+    } else {
+      dst = (float*)g.bias[4] + c;
+      dval = v;
+    }
+    *dst = accumulate ? *dst + dval : dval;
+  }
+}
+
+extern "C" int tmae_eb_bwd(const tmae_eb_params* params, const float* z, const float* noise, const float* glik,
+                           const float* gzhat, float* dz, int n, int C, int HW, const tmae_eb_params* grads,
+                           int accumulate, void* stream) {
+  TMAE_REQUIRE(params && grads && z && dz, "tmae_eb_bwd: null argument");
+  static_assert(sizeof(EbGrad) == EB_NG * sizeof(float), "EbGrad packing");
+  if (C == 0) return TMAE_OK;
+  hipLaunchKernelGGL(eb_bwd_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, *params, z, noise, glik, gzhat, dz, C,
+                     HW, n, *grads, accumulate);
+  TMAE_LAUNCH_CHECK("tmae_eb_bwd");
+}
+
+// aux_loss backward (compressai EntropyBottleneck.loss, stop_gradient=True on the density parameters):
+// d/dq[c][j] = g * sign(f_c(q[c][j]) - target[j]) * f_c'(q[c][j])
+__global__ void __launch_bounds__(256)
+eb_aux_bwd_kernel(tmae_eb_params p, const float* __restrict__ target, const float* __restrict__ gout,
+                  float* __restrict__ dq, int C, int accumulate) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= C * 3) return;
+  const int c = i / 3, j = i - 3 * c;
+  EbCh w;
+  eb_load(p, c, w);
+  float d = 0.0f;
+  const float f = eb_fwd_bwd(w, p.quantiles[i], 1.0f, nullptr, &d);
+  const float r = f - target[j];
+  const float sg = r > 0.0f ? 1.0f : (r < 0.0f ? -1.0f : 0.0f);
+  const float v = (gout ? gout[0] : 1.0f) * sg * d;
+  dq[i] = accumulate ? dq[i] + v : v;
+}
+
+extern "C" int tmae_eb_aux_bwd(const tmae_eb_params* params, const float* target, const float* gout, float* dquantiles,
+                               int C, int accumulate, void* stream) {
+  TMAE_REQUIRE(params && target && dquantiles, "tmae_eb_aux_bwd: null argument");
+  if (C == 0) return TMAE_OK;
+  hipLaunchKernelGGL(eb_aux_bwd_kernel, dim3(ceil_div(3 * C, 256)), dim3(256), 0, (hipStream_t)stream, *params, target,
+                     gout, dquantiles, C, accumulate);
+  TMAE_LAUNCH_CHECK("tmae_eb_aux_bwd");
+}
+
+// ================================================================== rate term backward
+// bpp = (sum log y + sum log z) / (-ln2 * num_pixels) (rd_loss.py:19-20): dlik = g / (lik * -ln2 * num_pixels)
+__global__ void __launch_bounds__(256)
+bpp_bwd_kernel(const float* __restrict__ lik, const float* __restrict__ g, float* __restrict__ out, long long n,
+               float scale) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  out[i] = g[0] * scale / lik[i];
+}
+
+extern "C" int tmae_bpp_bwd(const float* lik, const float* gout, float* dlik, long long n, double num_pixels,
+                            void* stream) {
+  if (n <= 0) return TMAE_OK;
+  hipLaunchKernelGGL(bpp_bwd_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, lik, gout,
+                     dlik, n, (float)(1.0 / (-0.69314718055994530942 * num_pixels)));
+  TMAE_LAUNCH_CHECK("tmae_bpp_bwd");
+}
+
+// ================================================================== encoder / decoder glue
+// kept-patch im2col (timm PatchEmbed conv16/s16 over the kept patches, MCM.py:615 + gather 585-586):
+// out[b*keep + k][(c*P + py)*P + px] = img[b][c][hy*P + py][hx*P + px], patch ids_shuffle[b][k]
+template <typename T>
+__global__ void __launch_bounds__(256)
+patch_gather_kernel(const float* __restrict__ img, const int64_t* __restrict__ ids, T* __restrict__ out, int n, int C,
+                    int H, int W, int P, int L, int keep) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int KP = C * P * P;
+  if (i >= (long long)n * keep * KP) return;
+  const int col = (int)(i % KP);
+  const int row = (int)(i / KP);
+  const int b = row / keep, k = row - b * keep;
+  const int p = (int)ids[(size_t)b * L + k];
+  const int G = W / P;
+  const int hy = p / G, hx = p - hy * G;
+  const int c = col / (P * P), rem = col - c * P * P;
+  const int py = rem / P, px = rem - py * P;
+  out[i] = to_out<T>(img[(((size_t)b * C + c) * H + hy * P + py) * W + hx * P + px]);
+}
+
+extern "C" int tmae_patch_gather(const float* imgs, const int64_t* ids_shuffle, void* out, int n, int C, int H, int W,
+                                 int patch, int L, int keep, int dtype, void* stream) {
+  const long long total = (long long)n * keep * C * patch * patch;
+  if (total == 0) return TMAE_OK;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (dtype == TMAE_BF16)
+    hipLaunchKernelGGL(patch_gather_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, imgs, ids_shuffle, (bf16*)out,
+                       n, C, H, W, patch, L, keep);
+  else
+    hipLaunchKernelGGL(patch_gather_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, imgs, ids_shuffle,
+                       (float*)out, n, C, H, W, patch, L, keep);
+  TMAE_LAUNCH_CHECK("tmae_patch_gather");
+}
+
+// patchify of the reconstruction gradient ("nchpwq -> nhwpqc", MCM.py:497-522): out[b*L + p][(py*P + px)*C + c]
+template <typename T>
+__global__ void __launch_bounds__(256)
+patchify_kernel(const float* __restrict__ img, T* __restrict__ out, int n, int C, int H, int W, int P) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const int G = W / P, L = (H / P) * G, KP = P * P * C;
+  if (i >= (long long)n * L * KP) return;
+  const int col = (int)(i % KP);
+  const int row = (int)(i / KP);
+  const int b = row / L, p = row - b * L;
+  const int hy = p / G, hx = p - hy * G;
+  const int q = col / C, c = col - q * C;
+  const int py = q / P, px = q - py * P;
+  out[i] = to_out<T>(img[(((size_t)b * C + c) * H + hy * P + py) * W + hx * P + px]);
+}
+
+extern "C" int tmae_patchify(const float* imgs, void* out, int n, int C, int H, int W, int patch, int dtype,
+                             void* stream) {
+  TMAE_REQUIRE(H % patch == 0 && W % patch == 0, "tmae_patchify: image %dx%d, patch %d", H, W, patch);
+  const long long total = (long long)n * C * H * W;
+  if (total == 0) return TMAE_OK;
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (dtype == TMAE_BF16)
+    hipLaunchKernelGGL(patchify_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, imgs, (bf16*)out, n, C, H, W,
+                       patch);
+  else
+    hipLaunchKernelGGL(patchify_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, imgs, (float*)out, n, C, H, W,
+                       patch);
+  TMAE_LAUNCH_CHECK("tmae_patchify");
+}
+
+// decoder_embed backward gather (MCM.py:657-675): token k of image b sat at decoder row
+// 0 (k == 0) or 1 + ids_shuffle[b][k-1]; out[b*ntok + k] = dec_grad[b*(L+1) + row] (cast to the operand dtype)
+template <typename T>
+__global__ void __launch_bounds__(256)
+dec_gather_kernel(const float* __restrict__ g, const int64_t* __restrict__ ids, T* __restrict__ out, int n, int ntok,
+                  int L, int D) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)n * ntok * D) return;
+  const int d = (int)(i % D);
+  const int r = (int)(i / D);
+  const int b = r / ntok, k = r - b * ntok;
+  const int row = k == 0 ? 0 : 1 + (int)ids[(size_t)b * L + k - 1];
+  out[i] = to_out<T>(g[((size_t)b * (L + 1) + row) * D + d]);
+}
+
+// mask_token gradient: sum over every decoder row the mask token filled (MCM.py:660-664)
+__global__ void __launch_bounds__(256)
+mask_token_bwd_kernel(const float* __restrict__ g, const int64_t* __restrict__ ids, float* __restrict__ part, int n,
+                      int ntok, int L, int D) {
+  const int b = blockIdx.y;
+  const int d = blockIdx.x * 256 + threadIdx.x;
+  if (d >= D) return;
+  float s = 0.0f;
+  for (int mi = ntok - 1; mi < L; ++mi) {
+    const int row = 1 + (int)ids[(size_t)b * L + mi];
+    s += g[((size_t)b * (L + 1) + row) * D + d];
+  }
+  part[(size_t)b * D + d] = s;
+}
+
+extern "C" int tmae_decoder_embed_bwd_gather(const float* dec_grad, const int64_t* ids_shuffle, void* tok_grad, int n,
+                                             int ntok, int L, int D, int dtype, float* mask_part, float* dmask,
+                                             int accumulate, void* stream) {
+  TMAE_REQUIRE(dec_grad && ids_shuffle && tok_grad && ntok >= 1 && ntok <= L + 1, "tmae_decoder_embed_bwd_gather: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)n * ntok * D;
+  if (total > 0) {
+    const dim3 grid((unsigned)((total + 255) / 256));
+    if (dtype == TMAE_BF16)
+      hipLaunchKernelGGL(dec_gather_kernel<bf16>, grid, dim3(256), 0, st, dec_grad, ids_shuffle, (bf16*)tok_grad, n,
+                         ntok, L, D);
+    else
+      hipLaunchKernelGGL(dec_gather_kernel<float>, grid, dim3(256), 0, st, dec_grad, ids_shuffle, (float*)tok_grad, n,
+                         ntok, L, D);
+  }
+  if (dmask) {
+    TMAE_REQUIRE(mask_part != nullptr, "tmae_decoder_embed_bwd_gather: mask_part workspace required");
+    hipLaunchKernelGGL(mask_token_bwd_kernel, dim3(ceil_div(D, 256), n), dim3(256), 0, st, dec_grad, ids_shuffle,
+                       mask_part, n, ntok, L, D);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(D, 256)), dim3(256), 0, st, mask_part, n, D, dmask,
+                       accumulate);
+  }
+  TMAE_LAUNCH_CHECK("tmae_decoder_embed_bwd_gather");
+}
+
+// out = a + b (f32), the out-of-place residual add where autograd keeps the block input
+__global__ void __launch_bounds__(256)
+add_kernel(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ out, long long n) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = a[i] + b[i];
+}
+
+extern "C" int tmae_add(const float* a, const float* b, float* out, long long n, void* stream) {
+  if (n <= 0) return TMAE_OK;
+  hipLaunchKernelGGL(add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a, b, out, n);
+  TMAE_LAUNCH_CHECK("tmae_add");
+}
+
+// ================================================================== optimizer
+// torch.optim.Adam (amsgrad=False) over one flat f32 buffer: g' = g * clip (+ wd * p); m, v moments;
+// p -= (lr / bc1) * m / (sqrt(v) / sqrt(bc2) + eps)
+__global__ void __launch_bounds__(256)
+adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
+            long long n, float lr, float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt,
+            const float* __restrict__ clip) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float gg = g[i];
+  if (clip) gg *= clip[0];
+  const float pv = p[i];
+  if (wd != 0.0f) gg += wd * pv;
+  const float mm = b1 * m[i] + (1.0f - b1) * gg;
+  const float vv = b2 * v[i] + (1.0f - b2) * gg * gg;
+  m[i] = mm;
+  v[i] = vv;
+  p[i] = pv - (lr / bc1) * mm / (sqrtf(vv) / bc2_sqrt + eps);
+}
+
+extern "C" int tmae_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2,
+                         float eps, float weight_decay, int step, const float* clip, void* stream) {
+  TMAE_REQUIRE(p && g && m && v && step >= 1, "tmae_adam: bad arguments");
+  if (n <= 0) return TMAE_OK;
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n,
+                     lr, beta1, beta2, eps, weight_decay, (float)bc1, (float)sqrt(bc2), clip);
+  TMAE_LAUNCH_CHECK("tmae_adam");
+}
+
+// multi-tensor form: table[t] = {p, g, m, v, n, first_chunk} (int64), chunks of 1024 elements; a block
+// finds its tensor by binary search over first_chunk.  One launch updates every parameter of a group.
+__global__ void __launch_bounds__(256)
+adam_multi_kernel(const long long* __restrict__ tab, int nt, float lr, float b1, float b2, float eps, float wd,
+                  float bc1, float bc2_sqrt, const float* __restrict__ clip) {
+  const long long b = blockIdx.x;
+  int lo = 0, hi = nt - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[6 * mid + 5] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const long long* e = tab + 6 * lo;
+  float* p = (float*)e[0];
+  const float* g = (const float*)e[1];
+  float* m = (float*)e[2];
+  float* v = (float*)e[3];
+  const long long n = e[4];
+  const long long base = (b - e[5]) * 1024;
+  const float cs = clip ? clip[0] : 1.0f;
+  for (int k = threadIdx.x; k < 1024; k += 256) {
+    const long long i = base + k;
+    if (i >= n) break;
+    float gg = g[i] * cs;
+    const float pv = p[i];
+    if (wd != 0.0f) gg += wd * pv;
+    const float mm = b1 * m[i] + (1.0f - b1) * gg;
+    const float vv = b2 * v[i] + (1.0f - b2) * gg * gg;
+    m[i] = mm;
+    v[i] = vv;
+    p[i] = pv - (lr / bc1) * mm / (sqrtf(vv) / bc2_sqrt + eps);
+  }
+}
+
+extern "C" int tmae_adam_multi(const long long* table, int ntensors, long long nchunks, float lr, float beta1,
+                               float beta2, float eps, float weight_decay, int step, const float* clip, void* stream) {
+  TMAE_REQUIRE(table && ntensors > 0 && step >= 1, "tmae_adam_multi: bad arguments");
+  if (nchunks <= 0) return TMAE_OK;
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, table, ntensors,
+                     lr, beta1, beta2, eps, weight_decay, (float)bc1, (float)sqrt(bc2), clip);
+  TMAE_LAUNCH_CHECK("tmae_adam_multi");
+}
+
+// clip_grad_norm_(params, max_norm) over a flat gradient buffer: out[0] = ||g||_2 (f64 partials, fixed
+// order), out[1] = min(1, max_norm / (norm + 1e-6)) -- the factor applied to the gradients (no host sync)
+__global__ void __launch_bounds__(256)
+sumsq_partial_kernel(const float* __restrict__ g, long long n, double* __restrict__ part) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double x = g[i];
+    s += x * x;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256)
+clip_final_kernel(const double* __restrict__ part, int np, float max_norm, float* __restrict__ out) {
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < np; i += 256) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float norm = (float)sqrt(red[0]);
+    out[0] = norm;
+    out[1] = fminf(1.0f, max_norm / (norm + 1e-6f));
+  }
+}
+
+extern "C" int tmae_grad_norm(const float* g, long long n, double* work, float max_norm, float* out, void* stream) {
+  TMAE_REQUIRE(g && work && out, "tmae_grad_norm: null argument");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(512), dim3(256), 0, st, g, n, work);
+  hipLaunchKernelGGL(clip_final_kernel, dim3(1), dim3(256), 0, st, work, 512, max_norm, out);
+  TMAE_LAUNCH_CHECK("tmae_grad_norm");
+}
+
+// grads *= scale[0] (clip_grad_norm_ applies its factor to the stored gradients)
+__global__ void __launch_bounds__(256) scale_kernel(float* __restrict__ g, long long n, const float* __restrict__ s) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) g[i] *= s[0];
+}
+
+extern "C" int tmae_scale(float* g, long long n, const float* scale, void* stream) {
+  if (n <= 0) return TMAE_OK;
+  hipLaunchKernelGGL(scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, g, n, scale);
+  TMAE_LAUNCH_CHECK("tmae_scale");
+}

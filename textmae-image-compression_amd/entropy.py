@@ -156,9 +156,14 @@ class EntropyBottleneck(EntropyModel):
         outputs = (x.float() + noise) if training else zhat.view(n, h, w, c).permute(0, 3, 1, 2).contiguous()
         return outputs, lik.view(n, c, h, w)
 
-    @torch.no_grad()
     def loss(self):
-        return ops.eb_aux_loss(self)
+        """aux loss sum |f(quantiles) - target| (utils/engine.py:79); differentiable w.r.t. quantiles"""
+        if torch.is_grad_enabled() and self.quantiles.requires_grad:
+            from .mcm_train import AuxLossFn
+
+            return AuxLossFn.apply(self, self.quantiles)
+        with torch.no_grad():
+            return ops.eb_aux_loss(self)
 
     @torch.no_grad()
     def update(self, force=False):

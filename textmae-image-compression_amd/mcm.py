@@ -139,6 +139,7 @@ class MCM(CompressionModel):
         # the reference override drops `strict` (MCM.py:445-446); keep the compressai buffer resizing
         r = super().load_state_dict(state_dict, strict=strict)
         self._exec = None
+        self._train_exec = None
         return r
 
     @classmethod
@@ -193,8 +194,7 @@ class MCM(CompressionModel):
         if not imgs.is_cuda:
             raise ValueError("MCM.forward runs on the MI355X kernels: move the model and inputs to the GPU")
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError(
-                "training-mode autograd is not available in this build: run forward under torch.no_grad()")
+            return self._forward_train(imgs, total_scores, noise)
         with torch.no_grad():
             ex = self._executor(imgs.shape[0], imgs.device)
             out = ex.run(imgs, total_scores, self.training, noise)
@@ -202,6 +202,23 @@ class MCM(CompressionModel):
             loss = self.forward_loss(imgs, x_hat) if self.distortion != "none" else (
                 torch.zeros((), device=imgs.device),) * 3
         return {"loss": loss, "likelihoods": {"y": out["y"], "z": out["z"]}, "x_hat": x_hat}
+
+    def _forward_train(self, imgs, total_scores, noise):
+        """MCM.forward under autograd (utils/engine.py:75): one autograd node whose forward keeps the
+        activations and whose backward is the HIP reverse pass (mcm_train.py)."""
+        from .mcm_train import TrainExec, _MCMTrainFn
+
+        dt = self.compute_dtype
+        if torch.is_autocast_enabled() and dt == torch.float32:
+            dt = torch.bfloat16
+        B = imgs.shape[0]
+        ex = getattr(self, "_train_exec", None)
+        if ex is None or ex.batch != B or ex.dtype != dt or ex.device != imgs.device:
+            ex = self._train_exec = TrainExec(self, B, dt, imgs.device)
+        x_hat, ylik, zlik = _MCMTrainFn.apply(ex, noise, imgs, total_scores, *self.parameters())
+        loss = self.forward_loss(imgs, x_hat) if self.distortion != "none" else (
+            torch.zeros((), device=imgs.device),) * 3
+        return {"loss": loss, "likelihoods": {"y": ylik, "z": zlik}, "x_hat": x_hat}
 
     def forward_loss(self, imgs, x_hat):
         """MCM.forward_loss (MCM.py:690-712): (1 - SSIM, L1, VGG feature loss).  The VGG term needs

@@ -1,0 +1,781 @@
+"""Training path of the MCM drop-in: MCM.forward under autograd (utils/engine.py:75-91 calls
+``model(samples, total_scores)``, ``criterion(out_net, samples)``, ``loss.backward()``).
+
+One ``torch.autograd.Function`` covers the whole model: its forward enqueues the same gfx950 kernels
+as inference but keeps every activation the backward needs (GELU inputs, attention log-sum-exp,
+per-slice stack activations, ...); its backward is the full reverse pass on HIP kernels (split-K
+TN weight gradients, transposed-weight data gradients, LayerNorm / attention / entropy-model
+backward) writing every parameter gradient into one flat f32 buffer, whose views are returned to
+autograd (AccumulateGrad adopts them as ``p.grad``).  A ``GradSync`` attached to the model all-reduces
+that buffer in buckets over RCCL while the backward is still running (data parallel).
+
+Reference semantics reproduced (compressai 1.2.4 / timm 0.4.5 restated):
+  * training mode: EntropyBottleneck / GaussianConditional likelihoods of x + U(-1/2, 1/2);
+    z_hat, y_hat through quantize_ste (pass-through gradient, MCM.py:742-744, 776);
+  * LowerBound backward (gradient passes where x >= bound or grad < 0);
+  * the main loss's gradient on ``*.quantiles`` is exactly zero (d z_hat / d median = -1 + 1) and is
+    returned as zeros, so clip_grad_norm_ / aux_loss.backward() see what they see in the reference.
+The slice loop runs slice by slice (no batching of slices 6-11 in training).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import ops
+from . import train_ops as T
+from .ops import ACT_GELU, ACT_NONE
+
+
+def _convs(seq):
+    return [l for l in seq if isinstance(l, nn.Conv2d)]
+
+
+class _Weights:
+    """Kernel-layout copies of the f32 parameters, rebuilt when a parameter's version changes
+    (once per optimizer step)."""
+
+    def __init__(self, dtype):
+        self.dtype = dtype
+        self.cache = {}
+
+    def _get(self, p, kind, build):
+        key = (id(p), kind)
+        sig = (p.data_ptr(), p._version)
+        hit = self.cache.get(key)
+        if hit is not None and hit[0] == sig:
+            return hit[1]
+        t = build(p.detach())
+        self.cache[key] = (sig, t)
+        return t
+
+    def nt(self, p, rows=None):
+        """nn.Linear / 1x1 conv weight as [N][K] in the operand dtype"""
+        def b(w):
+            w2 = w.reshape(w.shape[0], -1) if rows is None else w.reshape(rows, -1)
+            if self.dtype == torch.float32:
+                return w2.contiguous()
+            return T.relayout(w2, torch.empty(w2.shape, dtype=self.dtype, device=w.device), (w2.numel(),), (1,))
+        return self._get(p, "nt", b)
+
+    def t(self, p, rows=None):
+        """transposed [K][N] (the data-gradient operand of y = x W^T)"""
+        def b(w):
+            w2 = w.reshape(w.shape[0], -1) if rows is None else w.reshape(rows, -1)
+            N, K = w2.shape
+            return T.relayout(w2, torch.empty((K, N), dtype=self.dtype, device=w.device), (K, 1, 1, N), (1, 0, 0, K))
+        return self._get(p, "t", b)
+
+    def raw(self, p):
+        """the weight as stored ([cin][cout] for ConvTranspose2d 1x1), cast"""
+        def b(w):
+            w2 = w.reshape(w.shape[0], -1)
+            if self.dtype == torch.float32:
+                return w2.contiguous()
+            return T.relayout(w2, torch.empty(w2.shape, dtype=self.dtype, device=w.device), (w2.numel(),), (1,))
+        return self._get(p, "raw", b)
+
+    def conv(self, p):
+        """Conv2d 3x3 weight [Cout][Cin][3][3] -> [Cout][3][3][Cin] (forward implicit GEMM)"""
+        def b(w):
+            co, ci = w.shape[:2]
+            return T.relayout(w, torch.empty((co, 9 * ci), dtype=self.dtype, device=w.device), (co, 3, 3, ci),
+                              (ci * 9, 3, 1, 9))
+        return self._get(p, "conv", b)
+
+    def conv_dg(self, p):
+        """-> [Cin][3][3][Cout] (transposed-conv data gradient)"""
+        def b(w):
+            co, ci = w.shape[:2]
+            return T.relayout(w, torch.empty((ci, 9 * co), dtype=self.dtype, device=w.device), (ci, 3, 3, co),
+                              (9, 3, 1, ci * 9))
+        return self._get(p, "conv_dg", b)
+
+
+class _BlockSaved:
+    __slots__ = ("x", "a1", "qkv", "att", "lse", "xmid", "a2", "hpre", "h")
+
+
+class TrainExec:
+    """Workspaces + saved activations of one training forward for (batch, dtype, device)."""
+
+    def __init__(self, m, batch, dtype, device):
+        self.m, self.batch, self.dtype, self.device = m, batch, dtype, device
+        self.w = _Weights(dtype)
+        K = m.num_keep_patches
+        self.P = m.encoder_embed.patch_size[0]
+        self.img = m.encoder_embed.img_size[0]
+        self.L = m.encoder_embed.num_patches
+        self.g = int(round(K ** 0.5))
+        if self.g * self.g != K:
+            raise ValueError(f"num_keep_patches={K} must be a perfect square (MCM.py:729-732)")
+        self.hz = ((self.g + 1) // 2 + 1) // 2
+        if self.hz * 4 != self.g:
+            raise ValueError(f"sqrt(num_keep_patches)={self.g} must be a multiple of 4 so h_s returns to the y grid")
+        self.Mp = batch * K
+        self.sw = m.latent_depth // m.num_slices
+        self.ms = m.num_slices // 2
+        self.mid = [l.out_channels for l in _convs(m.cc_transform_mean[0])]
+        # parameter gradient layout: the order in which the backward finishes them (DP buckets)
+        self.params = [p for p in self._grad_order() if p.requires_grad]
+        self.offsets = {}
+        off = 0
+        for p in self.params:
+            self.offsets[id(p)] = off
+            off += p.numel()
+        self.numel = off
+        self._gflat = None
+
+    # ------------------------------------------------------------------ helpers
+    def _e(self, *shape, dtype=None):
+        return torch.empty(shape, dtype=dtype or self.dtype, device=self.device)
+
+    def _z(self, *shape, dtype=torch.float32):
+        return torch.zeros(shape, dtype=dtype, device=self.device)
+
+    def _cast(self, src):
+        """f32 -> operand dtype (identity for the f32 path)"""
+        if self.dtype == torch.float32:
+            return src
+        return T.relayout(src, torch.empty(src.shape, dtype=self.dtype, device=self.device), (src.numel(),), (1,))
+
+    def _grad_order(self):
+        m = self.m
+        out = [m.decoder_pred.weight, m.decoder_pred.bias, m.decoder_norm.weight, m.decoder_norm.bias]
+        for blk in reversed(m.decoder_blocks):
+            out += _block_params(blk)
+        out += [m.decoder_embed.weight, m.decoder_embed.bias, m.mask_token]
+        for l in reversed([l for l in m.g_s if isinstance(l, nn.ConvTranspose2d)]):
+            out += [l.weight, l.bias]
+        for i in reversed(range(m.num_slices)):
+            for seq in (m.lrp_transform[i], m.cc_transform_mean[i], m.cc_transform_scale[i]):
+                for c in reversed(_convs(seq)):
+                    out += [c.weight, c.bias]
+        for seq in (m.h_s_mean, m.h_s_scale):
+            for c in reversed(_hs_convs(seq)):
+                out += [c.weight, c.bias]
+        eb = m.entropy_bottleneck
+        out += [getattr(eb, f"_matrix{i}") for i in range(5)] + [getattr(eb, f"_bias{i}") for i in range(5)]
+        out += [getattr(eb, f"_factor{i}") for i in range(4)] + [eb.quantiles]
+        for c in reversed(_convs(m.h_a)):
+            out += [c.weight, c.bias]
+        for l in reversed([l for l in m.g_a if isinstance(l, nn.Conv2d)]):
+            out += [l.weight, l.bias]
+        out += [m.encoder_norm.weight, m.encoder_norm.bias]
+        for blk in reversed(m.encoder_blocks):
+            out += _block_params(blk)
+        out += [m.encoder_embed.proj.weight, m.encoder_embed.proj.bias, m.cls_token]
+        seen, uniq = set(), []
+        for p in out:
+            if id(p) not in seen:
+                seen.add(id(p))
+                uniq.append(p)
+        missing = [n for n, p in m.named_parameters() if p.requires_grad and id(p) not in seen]
+        if missing:
+            raise RuntimeError(f"training executor does not cover parameters {missing}")
+        return uniq
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, imgs, scores, noise):
+        m, dt, B = self.m, self.dtype, self.batch
+        E, K, P, g = m.encoder_embed_dim, m.num_keep_patches, self.P, self.g
+        M, N, S, hz = m.latent_depth, m.hyperprior_depth, m.num_slices, self.hz
+        Te, Td = K + 1, self.L + 1
+        imgs = imgs.float().contiguous()
+        if imgs.shape[1:] != (m.encoder_embed.proj.in_channels, self.img, self.img):
+            raise ValueError(f"Input image size {tuple(imgs.shape[2:])} doesn't match model ({self.img})")
+        self.imgs = imgs
+        if noise is not None:
+            self.z_noise, self.y_noise = (t.float().contiguous() for t in noise)
+        elif not m.training:  # eval semantics: round(x - median) + median / round(y - mu) + mu
+            self.z_noise = self.y_noise = None
+        else:
+            self.z_noise = torch.empty((B, N, hz, hz), device=self.device).uniform_(-0.5, 0.5)
+            self.y_noise = torch.empty((B, M, g, g), device=self.device).uniform_(-0.5, 0.5)
+        W = self.w
+
+        # ---- encoder (MCM.py:590-634): masking ids, kept-patch embedding, cls, blocks, norm
+        shuf, rest = ops.ids_shuffle(scores, K, m.sum_lanes)
+        self.shuf, self.rest = shuf, rest
+        pos_e = m.encoder_pos_embed.detach()
+        tok = torch.empty((B * Te, E), dtype=torch.float32, device=self.device)
+        ops.patch_embed(imgs, shuf, W.nt(m.encoder_embed.proj.weight), m.encoder_embed.proj.bias.detach(), pos_e, tok,
+                        K, P, dt)
+        ops.cls_rows(tok, m.cls_token.detach(), pos_e, B, Te, E)
+        self.patches = T.patch_gather(imgs, shuf, self._e(B * K, m.encoder_embed.proj.weight[0].numel()), K, P, dt)
+        self.enc = []
+        for blk in m.encoder_blocks:
+            tok = self._block_fwd(blk, tok, B, Te)
+        self.tok_last = tok
+        enc_out = ops.layernorm(tok, m.encoder_norm.weight, m.encoder_norm.bias, m.encoder_norm.eps, dt, rows=B * K,
+                                row_group=K, group_stride=Te, row_offset=1)
+        self.enc_out = enc_out
+
+        # ---- g_a (MCM.py:735)
+        x = enc_out
+        self.ga = []  # (input, pre) per GELU layer
+        ga = [l for l in m.g_a if isinstance(l, nn.Conv2d)]
+        for j, l in enumerate(ga):
+            if j < len(ga) - 1:
+                h, pre = self._e(self.Mp, l.out_channels), self._e(self.Mp, l.out_channels)
+                T.linear_pre(x, W.nt(l.weight), l.bias.detach(), dt, ACT_GELU, h, pre)
+                self.ga.append((x, pre))
+                x = h
+            else:
+                self.ga.append((x, None))
+                self.Y32 = torch.empty((self.Mp, M), dtype=torch.float32, device=self.device)
+                if dt == torch.float32:
+                    ops.linear(x, W.nt(l.weight), l.bias.detach(), dt, out=self.Y32)
+                    self.YT = self.Y32
+                else:
+                    self.YT = self._e(self.Mp, M)
+                    ops.linear(x, W.nt(l.weight), l.bias.detach(), dt, out=self.YT, out32=self.Y32)
+
+        # ---- h_a (MCM.py:739)
+        self.ha = []
+        x, cin, H = self.YT, M, g
+        convs = _convs(m.h_a)
+        for j, c in enumerate(convs):
+            last = j == len(convs) - 1
+            s = c.stride[0]
+            Ho = (H + 2 - 3) // s + 1
+            if last:
+                out, pre = torch.empty((B * Ho * Ho, c.out_channels), dtype=torch.float32, device=self.device), None
+            else:
+                out, pre = self._e(B * Ho * Ho, c.out_channels), self._e(B * Ho * Ho, c.out_channels)
+            ops.conv3x3(x, cin, cin, B, H, H, W.conv(c.weight), c.bias.detach(), out, c.out_channels, c.out_channels,
+                        dt, stride=s, act=ACT_NONE if last else ACT_GELU, pre=pre, ldp=c.out_channels,
+                        y_f32=last)
+            self.ha.append((x, cin, H, s, pre))
+            x, cin, H = out, c.out_channels, Ho
+        self.Z = x
+
+        # ---- entropy bottleneck + z_hat (MCM.py:741-744)
+        eb = m.entropy_bottleneck
+        self.ZLIK = torch.empty((B, N, hz, hz), dtype=torch.float32, device=self.device)
+        self.ZHAT = self._e(B * hz * hz, N)
+        ops.eb_likelihood(eb, self.Z, B, N, hz * hz, noise=self.z_noise, lik=self.ZLIK, zhat=self.ZHAT,
+                          table=torch.empty((N, 59), dtype=torch.float32, device=self.device))
+
+        # ---- h_s (MCM.py:747-748): mean straight into the first M columns of LMS = [latent_means | y_hat slots]
+        self.LMS = self._z(self.Mp, 2 * M, dtype=dt)
+        self.LS = self._e(self.Mp, M)
+        self.hs_mean = self._h_s_fwd(m.h_s_mean, self.LMS, 2 * M)
+        self.hs_scale = self._h_s_fwd(m.h_s_scale, self.LS, M)
+
+        # ---- slice loop (MCM.py:751-787)
+        self._slices_fwd()
+
+        # ---- g_s (MCM.py:790-792)
+        x = self.YH
+        self.gs = []
+        gs = [l for l in m.g_s if isinstance(l, nn.ConvTranspose2d)]
+        for j, l in enumerate(gs):
+            cout = l.out_channels
+            h = self._e(self.Mp, cout)
+            if j < len(gs) - 1:
+                pre = self._e(self.Mp, cout)
+                T.linear_pre(x, W.t(l.weight), l.bias.detach(), dt, ACT_GELU, h, pre)
+            else:
+                pre = None
+                ops.linear(x, W.t(l.weight), l.bias.detach(), dt, out=h)
+            self.gs.append((x, pre))
+            x = h
+        self.gs_out = x
+
+        # ---- decoder (MCM.py:636-688)
+        Dd, L = m.decoder_embed_dim, self.L
+        pos_d = m.decoder_pos_embed.detach()
+        dec = torch.empty((B * Td, Dd), dtype=torch.float32, device=self.device)
+        ops.decoder_embed(x, W.nt(m.decoder_embed.weight), m.decoder_embed.bias.detach(), pos_d, shuf, dec, B, K, L,
+                          dt)
+        ops.mask_rows(dec, m.mask_token.detach(), pos_d, shuf, B, L, K, Dd)
+        self.dec = []
+        for blk in m.decoder_blocks:
+            dec = self._block_fwd(blk, dec, B, Td, store=self.dec)
+        self.dec_last = dec
+        self.dn = ops.layernorm(dec, m.decoder_norm.weight, m.decoder_norm.bias, m.decoder_norm.eps, dt, rows=B * L,
+                                row_group=L, group_stride=Td, row_offset=1)
+        x_hat = torch.empty((B, imgs.shape[1], self.img, self.img), dtype=torch.float32, device=self.device)
+        ops.decoder_pred(self.dn, W.nt(m.decoder_pred.weight), m.decoder_pred.bias.detach(), x_hat, B, L, P, dt)
+        return x_hat, self.YLIK, self.ZLIK
+
+    def _block_fwd(self, blk, x, B, Tn, store=None):
+        dt, W = self.dtype, self.w
+        rows, D = x.shape
+        s = _BlockSaved()
+        s.x = x
+        s.a1 = ops.layernorm(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, dt)
+        s.qkv = ops.linear(s.a1, W.nt(blk.attn.qkv.weight), _bias(blk.attn.qkv.bias), dt)
+        H = blk.attn.num_heads
+        s.att = self._e(rows, D)
+        s.lse = torch.empty((B * H * Tn,), dtype=torch.float32, device=self.device)
+        T.mha_lse(s.qkv, B, Tn, H, D // H, blk.attn.scale, dt, s.att, s.lse)
+        s.xmid = torch.empty_like(x)
+        T.linear_residual_out(s.att, W.nt(blk.attn.proj.weight), _bias(blk.attn.proj.bias), x, s.xmid, dt)
+        s.a2 = ops.layernorm(s.xmid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, dt)
+        hid = blk.mlp.fc1.out_features
+        s.h, s.hpre = self._e(rows, hid), self._e(rows, hid)
+        T.linear_pre(s.a2, W.nt(blk.mlp.fc1.weight), _bias(blk.mlp.fc1.bias), dt, ACT_GELU, s.h, s.hpre)
+        out = torch.empty_like(x)
+        T.linear_residual_out(s.h, W.nt(blk.mlp.fc2.weight), _bias(blk.mlp.fc2.bias), s.xmid, out, dt)
+        (self.enc if store is None else store).append(s)
+        return out
+
+    def _h_s_fwd(self, seq, out_final, ld_final):
+        dt, W, B = self.dtype, self.w, self.batch
+        x, cin, H = self.ZHAT, self.m.hyperprior_depth, self.hz
+        saved = []
+        layers = _hs_layers(seq)
+        for j, (c, pshuf) in enumerate(layers):
+            last = j == len(layers) - 1
+            cout = c.out_channels
+            if last:
+                out, pre, ldo = out_final, None, ld_final
+            else:
+                Ho = 2 * H if pshuf else H
+                co = cout // 4 if pshuf else cout
+                out, pre, ldo = self._e(B * Ho * Ho, co), self._e(B * Ho * Ho, co), co
+            ops.conv3x3(x, cin, cin, B, H, H, W.conv(c.weight), c.bias.detach(), out, ldo, cout, dt,
+                        act=ACT_NONE if last else ACT_GELU, pixel_shuffle=pshuf, pre=pre, ldp=ldo)
+            saved.append((x, cin, H, pshuf, pre))
+            if pshuf:
+                H, cin = 2 * H, cout // 4
+            else:
+                cin = cout
+            x = out
+        return saved
+
+    def _slices_fwd(self):
+        m, dt, W, B, g = self.m, self.dtype, self.w, self.batch, self.g
+        M, S, sw, ms, Mp, HW = m.latent_depth, m.num_slices, self.sw, self.ms, self.Mp, self.g * self.g
+        esz = self.LMS.element_size()
+        lms = self.LMS.data_ptr()
+        self.YPT = self._e(Mp, M)
+        self.YPRE = torch.empty((Mp, M), dtype=torch.float32, device=self.device)
+        self.YH = self._e(Mp, M)
+        self.YLIK = torch.empty((B, M, g, g), dtype=torch.float32, device=self.device)
+        self.sl = []
+        for i in range(S):
+            k = min(i, ms)
+            cin_m = M + sw * k
+            rec = {}
+            rec["mean"] = self._stack_fwd(_convs(m.cc_transform_mean[i]), (self.LMS, cin_m, 2 * M, None, 0, 0))
+            rec["scale"] = self._stack_fwd(_convs(m.cc_transform_scale[i]),
+                                           (self.LS, M, M, lms + M * esz if k else None, sw * k, 2 * M))
+            mu, sig = rec["mean"][-1], rec["scale"][-1]
+            ops.gc_slices(self.Y32, M, i * sw, mu, sig, 0, sw, self.y_noise, self.YLIK, M, self.YPT, dt, M,
+                          self.YPRE, M, B, HW, 1, sw)
+            ypt = self.YPT.data_ptr() + i * sw * esz
+            rec["lrp"] = self._stack_fwd(_convs(m.lrp_transform[i]), (self.LMS, cin_m, 2 * M, ypt, sw, M), lrp=i)
+            self.sl.append(rec)
+
+    def _stack_fwd(self, convs, first, lrp=None):
+        """5-conv stack (cc_transform / lrp_transform): returns [(act_l, pre_l) for l < 4] + [out]"""
+        dt, W, B, g, Mp = self.dtype, self.w, self.batch, self.g, self.Mp
+        m = self.m
+        M, sw = m.latent_depth, self.sw
+        x1, c1, ld1, x2, c2, ld2 = first
+        saved = []
+        for l, c in enumerate(convs):
+            cout = c.out_channels
+            if l < 4:
+                act, pre = self._e(Mp, cout), self._e(Mp, cout)
+                ops.conv3x3(x1, c1, ld1, B, g, g, W.conv(c.weight), c.bias.detach(), act, cout, cout, dt, act=ACT_GELU,
+                            x2=x2, c2=c2, ld2=ld2, pre=pre, ldp=cout)
+                saved.append((act, pre))
+                x1, c1, ld1, x2, c2, ld2 = act, cout, cout, None, 0, 0
+            elif lrp is None:
+                out = torch.empty((Mp, cout), dtype=torch.float32, device=self.device)
+                ops.conv3x3(x1, c1, ld1, B, g, g, W.conv(c.weight), c.bias.detach(), out, cout, cout, dt, y_f32=True)
+                saved.append(out)
+            else:
+                i = lrp
+                esz = self.YH.element_size()
+                t = torch.empty((Mp, cout), dtype=torch.float32, device=self.device)
+                ops.conv3x3(x1, c1, ld1, B, g, g, W.conv(c.weight), c.bias.detach(), self.YH.data_ptr() + i * sw * esz,
+                            M, cout, dt, y_f32=(dt == torch.float32), lrp_src=self.YPRE.data_ptr() + i * sw * 4,
+                            ld_src=M, y2=(self.LMS.data_ptr() + (M + i * sw) * esz) if i < self.ms else None,
+                            ldy2=2 * M, pre=t, ldp=cout)
+                saved.append(t)
+        return saved
+
+    # ------------------------------------------------------------------ backward
+    def grads_buffer(self, fresh):
+        if fresh or self._gflat is None:
+            buf = torch.empty(self.numel, dtype=torch.float32, device=self.device)
+            if fresh:
+                return buf
+            self._gflat = buf
+        return self._gflat
+
+    def backward(self, dxhat, dylik, dzlik, gflat, sync=None):
+        """full reverse pass; every parameter's gradient lands in gflat (views per self.offsets)"""
+        m, dt, W, B = self.m, self.dtype, self.w, self.batch
+        E, K, P, g = m.encoder_embed_dim, m.num_keep_patches, self.P, self.g
+        M, N, S, hz, L = m.latent_depth, m.hyperprior_depth, m.num_slices, self.hz, self.L
+        Dd = m.decoder_embed_dim
+        Te, Td = K + 1, L + 1
+        Mp = self.Mp
+        self.gflat = gflat
+        self.sync = sync
+        G = self.grad
+        dxhat = dxhat.float().contiguous() if dxhat is not None else torch.zeros_like(self.imgs)
+        dylik = dylik.float().contiguous() if dylik is not None else None
+        dzlik = dzlik.float().contiguous() if dzlik is not None else None
+
+        # ---- decoder_pred + unpatchify (MCM.py:683-686, 797)
+        dP = T.patchify(dxhat, self._e(B * L, dxhat.shape[1] * P * P), P, dt)
+        npred = dP.shape[1]
+        T.wgrad(dP, self.dn, npred, Dd, B * L, G(m.decoder_pred.weight), dt)
+        T.colsum(dP, B * L, npred, G(m.decoder_pred.bias))
+        ddn = torch.empty((B * L, Dd), dtype=torch.float32, device=self.device)
+        T.dgrad_linear(dP, W.t(m.decoder_pred.weight), B * L, npred, Dd, dt, out=ddn)
+        ddec = self._z(B * Td, Dd)
+        ddec_op = ddec if dt == torch.float32 else self._z(B * Td, Dd, dtype=dt)
+        T.layernorm_bwd(self.dec_last, m.decoder_norm.weight, ddn, ddec, B * L, Dd, m.decoder_norm.eps,
+                        G(m.decoder_norm.weight), G(m.decoder_norm.bias), dxop=None if dt == torch.float32 else ddec_op,
+                        row_group=L, group_stride=Td, row_offset=1)
+        self._ready(m.decoder_norm.bias)
+        for blk, s in zip(reversed(m.decoder_blocks), reversed(self.dec)):
+            ddec, ddec_op = self._block_bwd(blk, s, ddec, ddec_op, B, Td)
+            self._ready(_block_params(blk)[-1])
+
+        # ---- decoder_embed + mask tokens (MCM.py:657-675)
+        dtok = self._e(Mp, Dd)
+        T.decoder_embed_bwd_gather(ddec, self.shuf, dtok, B, K, L, Dd, dt, dmask=G(m.mask_token).view(-1))
+        T.wgrad(dtok, self.gs_out, Dd, E, Mp, G(m.decoder_embed.weight), dt)
+        T.colsum(dtok, Mp, Dd, G(m.decoder_embed.bias))
+        d = self._e(Mp, E)
+        T.dgrad_linear(dtok, W.t(m.decoder_embed.weight), Mp, Dd, E, dt, out=d)
+        self._ready(m.mask_token)
+
+        # ---- g_s
+        gs = [l for l in m.g_s if isinstance(l, nn.ConvTranspose2d)]
+        for j in reversed(range(len(gs))):
+            l = gs[j]
+            x, _ = self.gs[j]
+            pre_prev = self.gs[j - 1][1] if j > 0 else None
+            cin, cout = l.in_channels, l.out_channels
+            T.wgrad(d, x, cout, cin, Mp, G(l.weight), dt, layout="dense_t")
+            T.colsum(d, Mp, cout, G(l.bias))
+            dx = self._e(Mp, cin)
+            T.dgrad_linear(d, W.raw(l.weight), Mp, cout, cin, dt, out=dx, pre=pre_prev)
+            d = dx
+        dYH = d
+        self._ready(gs[0].bias)
+
+        # ---- slice loop
+        DY, dLM, dLS = self._slices_bwd(dYH, dylik)
+
+        # ---- h_s
+        dZH = self._z(B * hz * hz, N)
+        self._h_s_bwd(m.h_s_mean, self.hs_mean, dLM, dZH)
+        self._h_s_bwd(m.h_s_scale, self.hs_scale, dLS, dZH)
+        self._ready(_hs_convs(m.h_s_scale)[0].bias)
+
+        # ---- entropy bottleneck (MCM.py:741-744)
+        eb = m.entropy_bottleneck
+        dZ = torch.empty((B * hz * hz, N), dtype=torch.float32, device=self.device)
+        T.eb_bwd(ops._eb_params(eb), self.Z, self.z_noise, dzlik, dZH, dZ, B, N, hz * hz, self._eb_grads(eb))
+        G(eb.quantiles).zero_()
+        self._ready(eb.quantiles)
+
+        # ---- h_a (MCM.py:739): dZ -> DY (accumulated with the slice loop's y gradient)
+        d = self._cast(dZ)
+        convs = _convs(m.h_a)
+        for j in reversed(range(len(convs))):
+            c = convs[j]
+            x, cin, H, s, _ = self.ha[j]
+            pre_prev = self.ha[j - 1][4] if j > 0 else None
+            cout = c.out_channels
+            Ho = (H + 2 - 3) // s + 1
+            T.wgrad(d, x, cout, 9 * cin, B * Ho * Ho, G(c.weight), dt,
+                    conv=dict(c1=cin, H=H, W=H, stride=s, cin=cin), layout="conv")
+            T.colsum(d, B * Ho * Ho, cout, G(c.bias))
+            if j > 0:
+                dx = self._e(B * H * H, cin)
+                T.conv_dgrad(d, W.conv_dg(c.weight), B, H, H, s, cout, cin, dt, out=dx, pre=pre_prev)
+                d = dx
+            else:
+                T.conv_dgrad(d, W.conv_dg(c.weight), B, H, H, s, cout, cin, dt, routes=[(DY, M, M)])
+        self._ready(convs[0].bias)
+
+        # ---- g_a (MCM.py:735)
+        d = self._cast(DY)
+        ga = [l for l in m.g_a if isinstance(l, nn.Conv2d)]
+        for j in reversed(range(len(ga))):
+            l = ga[j]
+            x, _ = self.ga[j]
+            pre_prev = self.ga[j - 1][1] if j > 0 else None
+            cin, cout = l.in_channels, l.out_channels
+            T.wgrad(d, x, cout, cin, Mp, G(l.weight), dt)
+            T.colsum(d, Mp, cout, G(l.bias))
+            if j > 0:
+                dx = self._e(Mp, cin)
+                T.dgrad_linear(d, W.t(l.weight), Mp, cout, cin, dt, out=dx, pre=pre_prev)
+            else:
+                dx = torch.empty((Mp, cin), dtype=torch.float32, device=self.device)
+                T.dgrad_linear(d, W.t(l.weight), Mp, cout, cin, dt, out=dx)
+            d = dx
+        denc = d
+        self._ready(ga[0].bias)
+
+        # ---- encoder norm (drops cls, MCM.py:631-632) + blocks
+        dt_tok = self._z(B * Te, E)
+        dt_op = dt_tok if dt == torch.float32 else self._z(B * Te, E, dtype=dt)
+        T.layernorm_bwd(self.tok_last, m.encoder_norm.weight, denc, dt_tok, B * K, E, m.encoder_norm.eps,
+                        G(m.encoder_norm.weight), G(m.encoder_norm.bias), dxop=None if dt == torch.float32 else dt_op,
+                        row_group=K, group_stride=Te, row_offset=1)
+        self._ready(m.encoder_norm.bias)
+        for blk, s in zip(reversed(m.encoder_blocks), reversed(self.enc)):
+            dt_tok, dt_op = self._block_bwd(blk, s, dt_tok, dt_op, B, Te)
+            self._ready(_block_params(blk)[-1])
+
+        # ---- patch embed + cls token (MCM.py:615-626)
+        pw = m.encoder_embed.proj.weight
+        T.wgrad(dt_op, self.patches, E, pw[0].numel(), B * K, G(pw), dt, lda=E, a_remap=(K, Te, 1))
+        T.colsum(dt_tok, B * K, E, G(m.encoder_embed.proj.bias), row_group=K, group_stride=Te, row_offset=1)
+        T.colsum(dt_tok, B, E, G(m.cls_token).view(-1), row_group=1, group_stride=Te, row_offset=0)
+        self._ready(m.cls_token)
+
+    def grad(self, p):
+        off = self.offsets[id(p)]
+        return self.gflat[off:off + p.numel()].view(p.shape)
+
+    def _ready(self, p):
+        """every gradient up to and including p's is final (DP bucket hand-off)"""
+        if self.sync is not None:
+            self.sync.ready(self.offsets[id(p)] + p.numel())
+
+    def _eb_grads(self, eb):
+        from ._lib import EBParams
+
+        g = EBParams()
+        for i in range(5):
+            g.matrix[i] = self.grad(getattr(eb, f"_matrix{i}")).data_ptr()
+            g.bias[i] = self.grad(getattr(eb, f"_bias{i}")).data_ptr()
+            if i < 4:
+                g.factor[i] = self.grad(getattr(eb, f"_factor{i}")).data_ptr()
+        g.quantiles = self.grad(eb.quantiles).data_ptr()
+        return g
+
+    def _block_bwd(self, blk, s, dres, dres_op, B, Tn):
+        """timm Block backward: (dres f32, dres in the operand dtype) -> the same for the block input"""
+        dt, W, G = self.dtype, self.w, self.grad
+        rows, D = dres.shape
+        hid = blk.mlp.fc1.out_features
+        H = blk.attn.num_heads
+        f32 = dt == torch.float32
+        # fc2 (+ GELU of fc1 in the data-gradient epilogue)
+        T.wgrad(dres_op, s.h, D, hid, rows, G(blk.mlp.fc2.weight), dt)
+        T.colsum(dres, rows, D, G(blk.mlp.fc2.bias))
+        dh = self._e(rows, hid)
+        T.dgrad_linear(dres_op, W.t(blk.mlp.fc2.weight), rows, D, hid, dt, out=dh, pre=s.hpre)
+        # fc1
+        T.wgrad(dh, s.a2, hid, D, rows, G(blk.mlp.fc1.weight), dt)
+        T.colsum(dh, rows, hid, G(blk.mlp.fc1.bias))
+        da2 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
+        T.dgrad_linear(dh, W.t(blk.mlp.fc1.weight), rows, hid, D, dt, out=da2)
+        # norm2 + residual
+        dmid = torch.empty((rows, D), dtype=torch.float32, device=self.device)
+        dmid_op = dmid if f32 else self._e(rows, D)
+        T.layernorm_bwd(s.xmid, blk.norm2.weight, da2, dmid, rows, D, blk.norm2.eps, G(blk.norm2.weight),
+                        G(blk.norm2.bias), dres=dres, dxop=None if f32 else dmid_op)
+        # proj
+        T.wgrad(dmid_op, s.att, D, D, rows, G(blk.attn.proj.weight), dt)
+        T.colsum(dmid, rows, D, G(blk.attn.proj.bias))
+        datt = self._e(rows, D)
+        T.dgrad_linear(dmid_op, W.t(blk.attn.proj.weight), rows, D, D, dt, out=datt)
+        # attention core
+        dqkv = self._e(rows, 3 * D)
+        T.mha_bwd(s.qkv, s.att, datt, s.lse, dqkv, B, Tn, H, D // H, blk.attn.scale, dt)
+        # qkv
+        T.wgrad(dqkv, s.a1, 3 * D, D, rows, G(blk.attn.qkv.weight), dt)
+        if blk.attn.qkv.bias is not None:
+            T.colsum(dqkv, rows, 3 * D, G(blk.attn.qkv.bias))
+        da1 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
+        T.dgrad_linear(dqkv, W.t(blk.attn.qkv.weight), rows, 3 * D, D, dt, out=da1)
+        # norm1 + residual
+        dx = torch.empty((rows, D), dtype=torch.float32, device=self.device)
+        dx_op = dx if f32 else self._e(rows, D)
+        T.layernorm_bwd(s.x, blk.norm1.weight, da1, dx, rows, D, blk.norm1.eps, G(blk.norm1.weight),
+                        G(blk.norm1.bias), dres=dmid, dxop=None if f32 else dx_op)
+        return dx, dx_op
+
+    def _h_s_bwd(self, seq, saved, dout32, dZH):
+        dt, W, G, B = self.dtype, self.w, self.grad, self.batch
+        layers = _hs_layers(seq)
+        d = self._cast(dout32)
+        for j in reversed(range(len(layers))):
+            c, pshuf = layers[j]
+            x, cin, H, _, _ = saved[j]
+            cout = c.out_channels
+            T.wgrad(d, x, cout, 9 * cin, B * H * H, G(c.weight), dt, conv=dict(c1=cin, H=H, W=H, cin=cin),
+                    layout="conv")
+            T.colsum(d, B * H * H, cout, G(c.bias))
+            if j == 0:
+                T.conv_dgrad(d, W.conv_dg(c.weight), B, H, H, 1, cout, cin, dt, routes=[(dZH, cin, cin)])
+                break
+            _, _, Hp, pshuf_prev, pre_prev = saved[j - 1]
+            dx = self._e(B * H * H, cin)
+            if pshuf_prev:
+                # input of this conv = GELU(PixelShuffle(conv_{j-1})): plain data gradient, then unshuffle * gelu'
+                T.conv_dgrad(d, W.conv_dg(c.weight), B, H, H, 1, cout, cin, dt, out=dx)
+                c4 = cin * 4
+                dpre = self._e(B * Hp * Hp, c4)
+                T.unshuffle_bwd(dx, cin, pre_prev, cin, dpre, B, Hp, Hp, c4, dt, dy_f32=(dt == torch.float32))
+                d = dpre
+            else:
+                T.conv_dgrad(d, W.conv_dg(c.weight), B, H, H, 1, cout, cin, dt, out=dx, pre=pre_prev)
+                d = dx
+
+    def _slices_bwd(self, dYH, dylik):
+        m, dt, W, G, B, g = self.m, self.dtype, self.w, self.grad, self.batch, self.g
+        M, S, sw, ms, Mp, HW = m.latent_depth, m.num_slices, self.sw, self.ms, self.Mp, g * g
+        esz = self.LMS.element_size()
+        lms = self.LMS.data_ptr()
+        DY = self._z(Mp, M)
+        dLM = self._z(Mp, M)
+        dLS = self._z(Mp, M)
+        dSUP = self._z(Mp, M)
+        GS = torch.empty((Mp, M), dtype=torch.float32, device=self.device)
+        dT = self._e(Mp, sw)
+        dMU, dSG = self._e(Mp, sw), self._e(Mp, sw)
+        for i in reversed(range(S)):
+            k = min(i, ms)
+            cin_m = M + sw * k
+            rec = self.sl[i]
+            gs_i = GS.data_ptr() + i * sw * 4
+            # y_hat = y_hat_pre + 0.5 tanh(t)   (MCM.py:782-783)
+            T.lrp_bwd(rec["lrp"][-1], sw, dT, sw, Mp, sw, dt, g32=(dSUP.data_ptr() + i * sw * 4) if i < ms else None,
+                      ld32=M, g16=dYH.data_ptr() + i * sw * esz, ld16=M, gsum=gs_i, ldgs=M)
+            self._stack_bwd(_convs(m.lrp_transform[i]), rec["lrp"], dT,
+                            (self.LMS, cin_m, 2 * M, self.YPT.data_ptr() + i * sw * esz, sw, M),
+                            [(dLM, M, M), (dSUP, M, sw * k), (gs_i, M, sw)])
+            # GaussianConditional + quantize_ste (MCM.py:771-776)
+            T.gc_bwd(self.Y32, M, i * sw, rec["mean"][-1], rec["scale"][-1], sw, self.y_noise, M, dylik, GS, M, DY, M,
+                     dMU, dSG, sw, B, HW, sw, dt)
+            self._stack_bwd(_convs(m.cc_transform_mean[i]), rec["mean"], dMU, (self.LMS, cin_m, 2 * M, None, 0, 0),
+                            [(dLM, M, M), (dSUP, M, sw * k)])
+            self._stack_bwd(_convs(m.cc_transform_scale[i]), rec["scale"], dSG,
+                            (self.LS, M, M, lms + M * esz if k else None, sw * k, 2 * M),
+                            [(dLS, M, M), (dSUP, M, sw * k)])
+            self._ready(_convs(m.cc_transform_scale[i])[0].bias)
+        return DY, dLM, dLS
+
+    def _stack_bwd(self, convs, saved, dtop, first, routes):
+        dt, W, G, B, g, Mp = self.dtype, self.w, self.grad, self.batch, self.g, self.Mp
+        d = dtop
+        for l in range(4, 0, -1):
+            c = convs[l]
+            cin, cout = c.in_channels, c.out_channels
+            act_prev, pre_prev = saved[l - 1]
+            T.wgrad(d, act_prev, cout, 9 * cin, Mp, G(c.weight), dt, conv=dict(c1=cin, H=g, W=g, cin=cin),
+                    layout="conv")
+            T.colsum(d, Mp, cout, G(c.bias))
+            dx = self._e(Mp, cin)
+            T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, out=dx, pre=pre_prev)
+            d = dx
+        c = convs[0]
+        x1, c1, ld1, x2, c2, ld2 = first
+        cin, cout = c1 + c2, c.out_channels
+        T.wgrad(d, x1, cout, 9 * cin, Mp, G(c.weight), dt, ldb=ld1,
+                conv=dict(x2=x2, c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv")
+        T.colsum(d, Mp, cout, G(c.bias))
+        # zero-width routes (no support slices yet) stay in place: their limits still partition the channels
+        T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
+
+
+def _bias(b):
+    return None if b is None else b.detach()
+
+
+def _block_params(blk):
+    ps = [blk.mlp.fc2.weight, blk.mlp.fc2.bias, blk.mlp.fc1.weight, blk.mlp.fc1.bias, blk.norm2.weight, blk.norm2.bias,
+          blk.attn.proj.weight, blk.attn.proj.bias, blk.attn.qkv.weight]
+    if blk.attn.qkv.bias is not None:
+        ps.append(blk.attn.qkv.bias)
+    ps += [blk.norm1.weight, blk.norm1.bias]
+    return ps
+
+
+def _hs_layers(seq):
+    """h_s layers as (conv, followed_by_pixel_shuffle)"""
+    out = []
+    for l in seq:
+        if isinstance(l, nn.Conv2d):
+            out.append((l, False))
+        elif isinstance(l, nn.Sequential):
+            out.append((l[0], True))
+    return out
+
+
+def _hs_convs(seq):
+    return [c for c, _ in _hs_layers(seq)]
+
+
+class _MCMTrainFn(torch.autograd.Function):
+    """MCM.forward as one autograd node: (imgs, scores, *params) -> (x_hat, y likelihood, z likelihood)"""
+
+    @staticmethod
+    def forward(ctx, ex, noise, imgs, scores, *params):
+        x_hat, ylik, zlik = ex.forward(imgs, scores, noise)
+        ctx.ex = ex
+        ctx.params = params
+        return x_hat, ylik, zlik
+
+    @staticmethod
+    def backward(ctx, dxhat, dylik, dzlik):
+        ex = ctx.ex
+        params = ctx.params
+        # a pre-existing .grad (accumulation across calls, zero_grad(set_to_none=False)) is added to by
+        # autograd: write into a fresh buffer then, so the returned views never alias p.grad
+        fresh = any(p.grad is not None for p in params if p.requires_grad)
+        gflat = ex.grads_buffer(fresh)
+        sync = getattr(ex.m, "grad_sync", None)
+        ex.backward(dxhat, dylik, dzlik, gflat, sync=sync)
+        if sync is not None:
+            sync.finish()
+        out = []
+        for p in params:
+            if not p.requires_grad:
+                out.append(None)
+            else:
+                off = ex.offsets[id(p)]
+                out.append(gflat[off:off + p.numel()].view(p.shape))
+        return (None, None, None, None, *out)
+
+
+class BppFn(torch.autograd.Function):
+    """RateDistortionLoss bpp term (rd_loss.py:19-20) with its HIP backward"""
+
+    @staticmethod
+    def forward(ctx, ylik, zlik, num_pixels):
+        ctx.save_for_backward(ylik, zlik)
+        ctx.num_pixels = num_pixels
+        return ops.bpp(ylik, zlik, num_pixels)
+
+    @staticmethod
+    def backward(ctx, g):
+        ylik, zlik = ctx.saved_tensors
+        g = g.float().contiguous().reshape(1)
+        dy = T.bpp_bwd(ylik.contiguous(), g, torch.empty_like(ylik), ctx.num_pixels)
+        dz = T.bpp_bwd(zlik.contiguous(), g, torch.empty_like(zlik), ctx.num_pixels)
+        return dy, dz, None
+
+
+class AuxLossFn(torch.autograd.Function):
+    """EntropyBottleneck.loss (compressai; utils/engine.py:79, 87): gradient only to quantiles"""
+
+    @staticmethod
+    def forward(ctx, eb, quantiles):
+        ctx.eb = eb
+        return ops.eb_aux_loss(eb)
+
+    @staticmethod
+    def backward(ctx, g):
+        eb = ctx.eb
+        dq = torch.empty_like(eb.quantiles)
+        T.eb_aux_bwd(ops._eb_params(eb), eb.target, g.float().contiguous().reshape(1), dq, eb.channels)
+        return None, dq

@@ -154,10 +154,11 @@ def decoder_pred(x, w, b, imgs, n, L, patch, dtype):
 # --------------------------------------------------------------------------------------- LIC
 def conv3x3(x1, c1, ld1, n, H, W, w, b, y, ldy, cout, dtype, stride=1, act=ACT_NONE, pixel_shuffle=False,
             x2=None, c2=0, ld2=0, y_f32=None, y32=None, ld32=0, addend=None, ld_add=0, lrp_src=None, ld_src=0,
-            y2=None, ldy2=0, nb=(1, 1), strides=None):
+            y2=None, ldy2=0, nb=(1, 1), strides=None, pre=None, ldp=0):
     """Batched 3x3 conv (tmae_conv3x3).  Pointer arguments: tensors or raw device addresses.
-    `strides` maps operand name (x1, x2, w, b, y, y32, a, src, y2) -> (s1, s2) element strides for the
-    nb[0] x nb[1] problems."""
+    `strides` maps operand name (x1, x2, w, b, y, y32, a, src, y2, pre) -> (s1, s2) element strides for the
+    nb[0] x nb[1] problems.  `pre` (training): pre-activation copy in the output's dtype / layout (the last
+    lrp conv: f32 pre-tanh rows ldp apart)."""
     a = ConvArgs()
     a.x1, a.c1, a.ld1 = _p(x1), c1, ld1
     a.x2, a.c2, a.ld2 = _p(x2), c2, ld2
@@ -173,6 +174,7 @@ def conv3x3(x1, c1, ld1, n, H, W, w, b, y, ldy, cout, dtype, stride=1, act=ACT_N
     a.addend, a.ld_add = _p(addend), ld_add
     a.lrp_src, a.ld_src = _p(lrp_src), ld_src
     a.y2, a.ldy2 = _p(y2), ldy2
+    a.pre, a.ldp = _p(pre), ldp
     a.nb1, a.nb2 = nb
     for name, (s1, s2) in (strides or {}).items():
         setattr(a, f"{name}_s1", s1)

@@ -4,6 +4,7 @@ Same constructor (`lmbda`), same output keys ("bpp_loss", "ssim_loss", "L1_loss"
 and the same formula: loss = lmbda * (0.25*ssim + 10*L1 + 0.1*vgg) + bpp.  The bpp reduction over
 both likelihood tensors runs on the device (tmae_bpp_sum).
 """
+import torch
 import torch.nn as nn
 
 from . import ops
@@ -18,7 +19,12 @@ class RateDistortionLoss(nn.Module):
         N, _, H, W = target.size()
         out = {}
         lik = output["likelihoods"]
-        out["bpp_loss"] = ops.bpp(lik["y"], lik["z"], N * H * W)
+        if torch.is_grad_enabled() and (lik["y"].requires_grad or lik["z"].requires_grad):
+            from .mcm_train import BppFn
+
+            out["bpp_loss"] = BppFn.apply(lik["y"], lik["z"], N * H * W)
+        else:
+            out["bpp_loss"] = ops.bpp(lik["y"], lik["z"], N * H * W)
         out["ssim_loss"] = output["loss"][0]
         out["L1_loss"] = output["loss"][1]
         out["vgg_loss"] = output["loss"][2]
