@@ -25,6 +25,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "images/sec encode+decode+rate, ViT-B 256×256 batch64, 1/2/4/8 MI355X"
 FWD_GFLOP_PER_IMG = 61.48        # BASELINE.md §2, config 2 (K=144)
+TRAIN_GFLOP_PER_IMG = 184.4      # fwd + bwd = 3x fwd
 PEAK_BF16 = 2.5e15               # MI355X_MICROARCH.md: dense bf16 MFMA
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
@@ -43,6 +44,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--train-steps", type=int, default=10, help="training steps timed after the inference run")
+    ap.add_argument("--train-warmup", type=int, default=3)
+    ap.add_argument("--train-batch", type=int, default=64)
+    ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for a one-GPU rehearsal)")
     return ap.parse_args()
 
 
@@ -97,6 +103,51 @@ def dominant_kernel_roofline(model, batch, reps, dtype):
             "traffic": traffic, "avg_launch_us": round(t * 1e6, 2), "flops_per_launch": flops}
 
 
+def train_bench(model, args, rank, world, dev, barrier):
+    """the reference training step (utils/engine.py:72-91): forward, RateDistortionLoss (SSIM + L1 +
+    bpp; VGG needs a weight download), aux loss, backward (HIP reverse pass; for world > 1 the RCCL
+    gradient all-reduce runs inside it, bucketed), clip_grad_norm_(1.0), Adam, aux backward, aux Adam"""
+    from textmae_amd import engine
+    from textmae_amd.optim import configure_optimizers
+    from textmae_amd.parallel import enable_data_parallel
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    model.train()
+    model.distortion = "ssim+l1"
+    if world > 1:
+        enable_data_parallel(model)
+    opt, aux_opt = configure_optimizers(model, lr=1e-4, aux_lr=1e-4, fused=True)
+    crit = RateDistortionLoss(lmbda=1e-2)
+    L = model.encoder_embed.num_patches
+    imgs, scores = synthetic_inputs(args.train_batch, args.img, L, 2000 + rank, dev)
+
+    def step():
+        return engine.train_step(model, crit, imgs, scores, opt, aux_opt, clip_max_norm=1.0)
+
+    for _ in range(args.train_warmup):
+        out = step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.train_steps):
+        out = step()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    ips = world * args.train_batch * args.train_steps / el
+    return {"metric": "training images/s (fwd + bwd + clip + 2x Adam" + (", RCCL grad all-reduce" if world > 1 else "")
+            + ")", "value": round(ips, 2), "unit": "images/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
+            "steps": args.train_steps, "warmup": args.train_warmup, "per_gpu_batch": args.train_batch,
+            "global_batch": args.train_batch * world, "parallelism": f"dp{world}", "dtype": "bf16",
+            "loss_last": round(float(out["loss"]), 6), "step_mfma_frac": round(ips * TRAIN_GFLOP_PER_IMG * 1e9 /
+                                                                             (world * PEAK_BF16), 4),
+            "hip_graph": False}
+
+
 def cpu_baseline(img, keep, seconds):
     """The oracle (CPU restatement, fp32) on the host cores: a bounded 2-image sample of the workload."""
     from oracle.mcm_oracle import MCMConfig, make_state_dict, mcm_forward
@@ -121,12 +172,16 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     def barrier():
         if world > 1:
@@ -142,6 +197,7 @@ def main():
     L = model.encoder_embed.num_patches
     imgs, scores = synthetic_inputs(args.batch, args.img, L, 1000 + rank, dev)
 
+    graph = None
     with torch.no_grad():
         if args.no_graph:
             def step():
@@ -176,6 +232,11 @@ def main():
             el = float(t.item())
         roof = dominant_kernel_roofline(model, args.batch, args.kernel_reps, dtype) if rank == 0 else None
 
+    train = None
+    if not args.no_train and args.train_steps > 0:
+        graph = None
+        train = train_bench(model, args, rank, world, dev, barrier)
+
     value = world * args.batch * args.steps / el
     rec = {
         "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
@@ -189,6 +250,8 @@ def main():
         "step_mfma_frac": round(value * FWD_GFLOP_PER_IMG * 1e9 / (world * PEAK_BF16), 4),
         "roofline": roof,
     }
+    if train is not None:
+        rec["train"] = train
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             rec["cpu_baseline"] = cpu_baseline(args.img, args.keep, args.cpu_seconds)

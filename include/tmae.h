@@ -352,6 +352,17 @@ int tmae_grad_norm(const float* g, long long n, double* work, float max_norm, fl
 /* g *= scale[0] */
 int tmae_scale(float* g, long long n, const float* scale, void* stream);
 
+/* ---------------------------------------------------------------- distortion (MCM.forward_loss, MCM.py:690-712)
+ * SSIM (pytorch_msssim: 11-tap gaussian, sigma 1.5, valid filtering, K = (0.01, 0.03), data range 1) and L1
+ * over P = N*C planes of H x W (f32 NCHW, H, W >= 11): out[0] = 1 - SSIM, out[1] = mean |x - y|.
+ * hwork >= 5*P*H*(W-10) floats, dmaps (3*P*(H-10)*(W-10) floats; NULL when no backward follows),
+ * part >= 2048 doubles.  Backward: gx = d(g0 * out[0] + g1 * out[1]) / dx with gout = {g0, g1} on the device,
+ * vwork >= 3*P*H*(W-10) floats. */
+int tmae_distortion_fwd(const float* x, const float* y, int P, int H, int W, float* hwork, float* dmaps, double* part,
+                        float* out, void* stream);
+int tmae_distortion_bwd(const float* x, const float* y, int P, int H, int W, const float* dmaps, float* vwork,
+                        const float* gout, float* gx, void* stream);
+
 /* diagnostics (no device work): writes into out[len] the name of the MFMA GEMM variant that
  * tmae_linear_fwd / tmae_conv3x3 launch for an M x N x K problem batched `batch` times (tile shape,
  * waves per workgroup, LDS ring), e.g. "ring<bf16,256x256,8w,BK32x4>". */

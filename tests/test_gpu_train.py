@@ -196,6 +196,25 @@ def test_mha_bwd(T, T_, H, dh, dt):
         assert _rel2(dq.float(), q_.grad) < 2e-2
 
 
+# ------------------------------------------------------------------------------ distortion
+def test_distortion_fwd_bwd_vs_oracle():
+    from oracle.thirdparty import ssim as ssim_ref
+    from textmae_amd.distortion import ssim_l1_loss
+
+    x = torch.rand(2, 3, 40, 37, generator=torch.Generator().manual_seed(30))
+    y = (x + 0.1 * _rnd(2, 3, 40, 37, seed=31)).clamp(0, 1)
+    xr = x.double().requires_grad_(True)
+    s_ref = 1 - ssim_ref(xr, y.double(), data_range=1)
+    l_ref = F.l1_loss(xr, y.double())
+    (0.7 * s_ref + 1.3 * l_ref).backward()
+    xg = x.cuda().requires_grad_(True)
+    s, l = ssim_l1_loss(xg, y.cuda())
+    (0.7 * s + 1.3 * l).backward()
+    torch.cuda.synchronize()
+    assert abs(s.item() - s_ref.item()) < 1e-5 and abs(l.item() - l_ref.item()) < 1e-6
+    assert _rel(xg.grad, xr.grad) < 1e-4
+
+
 # ------------------------------------------------------------------------------ optimizer
 def test_adam_matches_torch(T):
     n = 1000

@@ -134,6 +134,8 @@ SIGNATURES = {
     "tmae_adam_multi": [P, I, LL, F, F, F, F, F, I, P, P],
     "tmae_grad_norm": [P, LL, P, F, P, P],
     "tmae_scale": [P, LL, P, P],
+    "tmae_distortion_fwd": [P, P, I, I, I, P, P, P, P, P],
+    "tmae_distortion_bwd": [P, P, I, I, I, P, P, P, P, P],
 }
 
 # entry points that return a value rather than a status

@@ -330,13 +330,33 @@ colsum_partial_kernel(const T* __restrict__ x, int ld, int rows, int C, int G, i
   part[(size_t)blockIdx.y * C + c] = s;
 }
 
-__global__ void __launch_bounds__(256)
-colsum_final_kernel(const float* __restrict__ part, int splits, int C, float* __restrict__ out, int accumulate) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+// fold [rows][C] partials over rows: 64 columns x 16 row-lanes per block, fixed-order LDS tree
+// (deterministic); columns [0, split) -> out0[c], [split, C) -> out1[c - split]
+__global__ void __launch_bounds__(1024)
+fold_rows_kernel(const float* __restrict__ part, int rows, int C, float* __restrict__ out0, float* __restrict__ out1,
+                 int split, int accumulate) {
+  __shared__ float red[16][65];
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cx;
   float s = 0.0f;
-  for (int k = 0; k < splits; ++k) s += part[(size_t)k * C + c];
-  out[c] = accumulate ? out[c] + s : s;
+  if (c < C)
+    for (int r = ry; r < rows; r += 16) s += part[(size_t)r * C + c];
+  red[ry][cx] = s;
+  __syncthreads();
+  for (int o = 8; o > 0; o >>= 1) {
+    if (ry < o) red[ry][cx] += red[ry + o][cx];
+    __syncthreads();
+  }
+  if (ry == 0 && c < C) {
+    float* dst = c < split ? out0 + c : out1 + (c - split);
+    *dst = accumulate ? *dst + red[0][cx] : red[0][cx];
+  }
+}
+
+static void fold_rows(const float* part, int rows, int C, float* out0, float* out1, int split, int accumulate,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(fold_rows_kernel, dim3(ceil_div(C, 64)), dim3(1024), 0, st, part, rows, C, out0, out1, split,
+                     accumulate);
 }
 
 extern "C" int tmae_colsum(const void* x, int x_dtype, int ld, int rows, int C, int row_group, int group_stride,
@@ -355,7 +375,7 @@ extern "C" int tmae_colsum(const void* x, int x_dtype, int ld, int rows, int C, 
   else
     hipLaunchKernelGGL(colsum_partial_kernel<float>, grid, dim3(256), 0, st, (const float*)x, ld, rows, C, row_group,
                        group_stride, row_offset, rps, work);
-  hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(C, 256)), dim3(256), 0, st, work, splits, C, out, accumulate);
+  fold_rows(work, splits, C, out, out, C, accumulate, st);
   TMAE_LAUNCH_CHECK("tmae_colsum");
 }
 
@@ -458,19 +478,8 @@ layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamm
   }
 }
 
-__global__ void __launch_bounds__(256)
-ln_fold_kernel(const float* __restrict__ part, int waves, int D, float* __restrict__ dg, float* __restrict__ db,
-               int accumulate) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= 2 * D) return;
-  float s = 0.0f;
-  for (int k = 0; k < waves; ++k) s += part[(size_t)k * 2 * D + c];
-  float* o = c < D ? dg + c : db + (c - D);
-  *o = accumulate ? *o + s : s;
-}
-
 static int tmae_ln_fold(const float* part, int waves, int D, float* dg, float* db, int accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(ln_fold_kernel, dim3(ceil_div(2 * D, 256)), dim3(256), 0, st, part, waves, D, dg, db, accumulate);
+  fold_rows(part, waves, 2 * D, dg, db, D, accumulate, st);
   TMAE_LAUNCH_CHECK("tmae_layernorm_bwd");
 }
 
@@ -1042,8 +1051,7 @@ extern "C" int tmae_decoder_embed_bwd_gather(const float* dec_grad, const int64_
     TMAE_REQUIRE(mask_part != nullptr, "tmae_decoder_embed_bwd_gather: mask_part workspace required");
     hipLaunchKernelGGL(mask_token_bwd_kernel, dim3(ceil_div(D, 256), n), dim3(256), 0, st, dec_grad, ids_shuffle,
                        mask_part, n, ntok, L, D);
-    hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(D, 256)), dim3(256), 0, st, mask_part, n, D, dmask,
-                       accumulate);
+    fold_rows(mask_part, n, D, dmask, dmask, D, accumulate, st);
   }
   TMAE_LAUNCH_CHECK("tmae_decoder_embed_bwd_gather");
 }

@@ -1,53 +1,73 @@
-"""Distortion terms of MCM.forward_loss (reference MCM.py:690-712).
+"""Distortion terms of MCM.forward_loss (reference MCM.py:690-712) on the HIP kernels of
+csrc/distortion.hip: 1 - SSIM and L1 in one forward launch sequence, their backward in another.
 
-Not part of the measured encode + rate + decode path (SURVEY.md §8d reports it separately); these
-run as device-side torch ops on the reconstruction.  SSIM follows pytorch_msssim (unpinned in
-the reference's requirements): 11-tap gaussian window, sigma 1.5, valid padding, K = (0.01, 0.03),
-data_range 1, mean over channels and batch.
+SSIM follows pytorch_msssim (unpinned in the reference's requirements): 11-tap gaussian window,
+sigma 1.5, valid separable filtering, K = (0.01, 0.03), data_range 1, mean over every channel map.
+Images smaller than the window are filtered only along the dimensions that fit in pytorch_msssim;
+the kernels need H, W >= 11 and raise otherwise.  The VGG term needs downloaded weights (vgg.py:14)
+and is not computed.
 """
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
-_WIN = {}
+from . import _lib
+from .ops import _stream
 
-
-def _window(size, sigma, channels, dtype, device):
-    key = (size, sigma, channels, dtype, device)
-    if key not in _WIN:
-        coords = torch.arange(size, dtype=torch.float) - size // 2
-        g = torch.exp(-(coords ** 2) / (2 * sigma ** 2))
-        g = (g / g.sum()).to(dtype)
-        _WIN[key] = g.reshape(1, 1, 1, size).repeat(channels, 1, 1, 1).to(device)
-    return _WIN[key]
+_PART = {}
 
 
-def _gfilter(x, win):
-    c = x.shape[1]
-    out = x
-    for i, s in enumerate(x.shape[2:]):
-        if s >= win.shape[-1]:
-            out = F.conv2d(out, win.transpose(2 + i, -1), groups=c)
-    return out
+def _part(device):
+    t = _PART.get(device)
+    if t is None:
+        t = _PART[device] = torch.empty(2048, dtype=torch.float64, device=device)
+    return t
 
 
-def ssim(x, y, data_range=1.0, win_size=11, win_sigma=1.5, K=(0.01, 0.03)):
-    win = _window(win_size, win_sigma, x.shape[1], x.dtype, x.device)
-    c1, c2 = (K[0] * data_range) ** 2, (K[1] * data_range) ** 2
-    mu1, mu2 = _gfilter(x, win), _gfilter(y, win)
-    mu1_sq, mu2_sq, mu12 = mu1.pow(2), mu2.pow(2), mu1 * mu2
-    s1 = _gfilter(x * x, win) - mu1_sq
-    s2 = _gfilter(y * y, win) - mu2_sq
-    s12 = _gfilter(x * y, win) - mu12
-    cs_map = (2 * s12 + c2) / (s1 + s2 + c2)
-    ssim_map = ((2 * mu12 + c1) / (mu1_sq + mu2_sq + c1)) * cs_map
-    return torch.flatten(ssim_map, 2).mean(-1).mean()
+class DistortionFn(torch.autograd.Function):
+    """(x_hat, imgs) -> (1 - SSIM(x_hat, imgs), L1(x_hat, imgs)); gradient w.r.t. x_hat"""
+
+    @staticmethod
+    def forward(ctx, x_hat, imgs):
+        x = x_hat.float().contiguous()
+        y = imgs.float().contiguous()
+        n, c, H, W = x.shape
+        if H < 11 or W < 11:
+            raise ValueError(f"SSIM needs images of at least 11x11 (got {H}x{W})")
+        P = n * c
+        need_grad = ctx.needs_input_grad[0]
+        h = torch.empty(5 * P * H * (W - 10), dtype=torch.float32, device=x.device)
+        d = torch.empty(3 * P * (H - 10) * (W - 10), dtype=torch.float32, device=x.device) if need_grad else None
+        out = torch.empty(2, dtype=torch.float32, device=x.device)
+        _lib.call("tmae_distortion_fwd", x.data_ptr(), y.data_ptr(), P, H, W, h.data_ptr(),
+                  None if d is None else d.data_ptr(), _part(x.device).data_ptr(), out.data_ptr(), _stream())
+        if need_grad:
+            ctx.save_for_backward(x, y, d)
+        return out[0], out[1]
+
+    @staticmethod
+    def backward(ctx, g_ssim, g_l1):
+        x, y, d = ctx.saved_tensors
+        n, c, H, W = x.shape
+        P = n * c
+        dev = x.device
+        gout = torch.stack([g_ssim.reshape(()) if g_ssim is not None else torch.zeros((), device=dev),
+                            g_l1.reshape(()) if g_l1 is not None else torch.zeros((), device=dev)]).float().contiguous()
+        v = torch.empty(3 * P * H * (W - 10), dtype=torch.float32, device=dev)
+        gx = torch.empty_like(x)
+        _lib.call("tmae_distortion_bwd", x.data_ptr(), y.data_ptr(), P, H, W, d.data_ptr(), v.data_ptr(),
+                  gout.data_ptr(), gx.data_ptr(), _stream())
+        return gx, None
+
+
+def ssim_l1_loss(x_hat, imgs):
+    """(1 - SSIM, L1) as 0-d device tensors (differentiable w.r.t. x_hat)"""
+    return DistortionFn.apply(x_hat, imgs)
 
 
 def ssim_loss(x_hat, imgs):
-    return 1 - ssim(x_hat, imgs, data_range=1)
+    return ssim_l1_loss(x_hat, imgs)[0]
 
 
 def l1_loss(x_hat, imgs):
-    return F.l1_loss(x_hat, imgs)
+    return ssim_l1_loss(x_hat, imgs)[1]

@@ -223,9 +223,10 @@ class MCM(CompressionModel):
     def forward_loss(self, imgs, x_hat):
         """MCM.forward_loss (MCM.py:690-712): (1 - SSIM, L1, VGG feature loss).  The VGG term needs
         torchvision's pretrained VGG16 (a network download in the reference, vgg.py:14) and is 0 here."""
-        from .distortion import l1_loss, ssim_loss
+        from .distortion import ssim_l1_loss
 
-        return ssim_loss(x_hat, imgs), l1_loss(x_hat, imgs), torch.zeros((), device=imgs.device)
+        s, l1 = ssim_l1_loss(x_hat, imgs)
+        return s, l1, torch.zeros((), device=imgs.device)
 
     def aux_loss(self):
         return self.entropy_bottleneck.loss()

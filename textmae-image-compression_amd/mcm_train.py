@@ -419,6 +419,8 @@ class TrainExec:
         Mp = self.Mp
         self.gflat = gflat
         self.sync = sync
+        if sync is not None:
+            sync.attach(gflat)
         G = self.grad
         dxhat = dxhat.float().contiguous() if dxhat is not None else torch.zeros_like(self.imgs)
         dylik = dylik.float().contiguous() if dylik is not None else None

@@ -1,0 +1,88 @@
+"""Image-batch data parallelism for the training step (the DP that the reference's
+training.py builds a DistributedSampler for but never initialises, training.py:122-129).
+
+One process per GPU, ``torch.distributed`` backend "nccl" = RCCL over xGMI.  The model's backward
+(mcm_train.py) produces every parameter gradient into ONE flat f32 buffer, in the order the reverse
+pass finishes them (decoder first, patch embedding last).  ``GradSync`` cuts that buffer into
+buckets and all-reduces each bucket as soon as the backward reports it final (``ready(upto)``), so
+the collectives overlap the remaining backward kernels: the RCCL call is enqueued on the compute
+stream's timeline (the process group's own stream waits for the point of the call), and
+``finish()`` makes the compute stream wait for the last bucket -- no host synchronisation.
+
+Bucket size: xGMI is point-to-point (7 links per GPU); a ring all-reduce moves 2(W-1)/W of a bucket
+over each link, so buckets of ~64 MB keep every ring step long enough to run near link rate while
+still giving the overlap several hand-off points per backward (804 MB of gradients -> ~13 buckets).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class GradSync:
+    def __init__(self, process_group=None, bucket_mb: float = 64.0, average: bool = True):
+        self.group = process_group
+        self.bucket_elems = max(1, int(bucket_mb * (1 << 20) // 4))
+        self.average = average
+        self.flat = None
+        self._bounds = None
+        self._next = 0
+        self._work = []
+
+    def world(self):
+        return dist.get_world_size(self.group) if dist.is_initialized() else 1
+
+    def _begin(self, flat):
+        if self.flat is None or self.flat.data_ptr() != flat.data_ptr() or self.flat.numel() != flat.numel():
+            n = flat.numel()
+            self._bounds = list(range(0, n, self.bucket_elems)) + [n]
+        self.flat = flat
+        self._next = 0
+        self._work = []
+
+    def attach(self, flat):
+        """start a backward over `flat` (called by the executor before the first ready())"""
+        self._begin(flat)
+
+    def _launch(self, i):
+        a, b = self._bounds[i], self._bounds[i + 1]
+        t = self.flat[a:b]
+        W = self.world()
+        if W <= 1:
+            return
+        if dist.get_backend(self.group) == "nccl":
+            op = dist.ReduceOp.AVG if self.average else dist.ReduceOp.SUM
+            self._work.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
+        else:  # gloo (CPU rehearsal): SUM then scale
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+            if self.average:
+                t.div_(W)
+
+    def ready(self, upto: int):
+        """gradients [0, upto) of the flat buffer are final: launch every bucket they complete"""
+        while self._next < len(self._bounds) - 1 and self._bounds[self._next + 1] <= upto:
+            self._launch(self._next)
+            self._next += 1
+
+    def finish(self):
+        """launch the remaining buckets and order the compute stream after every collective"""
+        self.ready(self._bounds[-1])
+        for w in self._work:
+            w.wait()
+        self._work = []
+
+
+def broadcast_parameters(model, src: int = 0, group=None):
+    """every rank starts from rank `src`'s weights (and buffers: the entropy models' CDF tables)"""
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return
+    with torch.no_grad():
+        for t in list(model.parameters()) + [b for b in model.buffers() if b.numel() > 0]:
+            dist.broadcast(t.data, src=src, group=group)
+
+
+def enable_data_parallel(model, process_group=None, bucket_mb: float = 64.0):
+    """attach a GradSync to `model` (MCM): its backward then all-reduces (averages) the gradients"""
+    model.grad_sync = GradSync(process_group, bucket_mb)
+    broadcast_parameters(model, group=process_group)
+    return model.grad_sync
