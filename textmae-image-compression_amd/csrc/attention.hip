@@ -10,6 +10,8 @@
 //   O^T += V^T · P^T        the score accumulator is fed straight back as the MFMA B operand
 //                           (cdna_hip_programming.md §3 "accumulator tile as the next operand")
 // Online (flash) softmax over key tiles; the [T x T] score matrix never exists in HBM.
+#include <stdlib.h>
+
 #include "common.h"
 
 template <typename T> struct AttnCfg;
@@ -175,16 +177,174 @@ mha_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, float* __restrict
     }
 }
 
+// bf16 forward, VALU-lean form of the kernel above (the softmax VALU, not the MFMA pipe, bounds the loop:
+// a 32-key tile costs DH/16 + DH/16 MFMAs against 16 scores of exp/max/sum per lane):
+//   * the scale rides in the exponent: p = exp2(s * c - m * c) is one FMA + v_exp, no per-score multiply;
+//   * masking only on the ragged last key tile (wave-uniform branch);
+//   * deferred rescaling (cdna_hip_programming.md T13): the running max m only moves when some lane's tile
+//     max exceeds it by more than 8 (log2 units), so O / l are rescaled on the first tile and rarely after;
+//     P <= 2^8, exact after the final 1/l (same m for O and l);
+//   * per-lane partial row sums, combined across the two lane halves once at the end;
+//   * V^T staged with keys on consecutive lanes (2-byte LDS stores to consecutive addresses).
+template <int DH> struct AttnTr;
+// V row stride (elements) for conflict-free ds_read_b64_tr_b16: 4 key rows x 2 lane groups of 8 dwords
+// must cover all 64 banks -> row stride = 16 or 48 dwords mod 64
+template <> struct AttnTr<64> { static constexpr int LDV = 96; };
+template <> struct AttnTr<32> { static constexpr int LDV = 32; };
+
+typedef __attribute__((ext_vector_type(4))) short attn_s4;
+typedef __attribute__((address_space(3))) attn_s4 attn_lds_s4;
+
+template <int DH>
+__global__ void __launch_bounds__(1024)
+mha_fwd_bf16_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int Tn, int H,
+                    int Tpad, float scale_log2e) {
+  constexpr int KPAD = 8, NDT = DH / 32, CPR = DH / 8, LDV = AttnTr<DH>::LDV;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int ldk = DH + KPAD;
+  bf16* Ks = reinterpret_cast<bf16*>(smem);
+  bf16* Vs = Ks + (size_t)Tpad * ldk;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * DH, ld = 3 * D;
+  const bf16* base = qkv + (size_t)b * Tn * ld + h * DH;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  // K and V row-major, 16-B chunks; every load of a thread issued before its first LDS store
+  constexpr int MAXC = 8;  // chunks per thread per operand (Tpad * CPR <= nthr * MAXC)
+  uint4 kv[MAXC], vv[MAXC];
+#pragma unroll
+  for (int u = 0; u < MAXC; ++u) {
+    const int i = tid + u * nthr;
+    const int r = i / CPR, c = i - r * CPR;
+    kv[u] = vv[u] = uint4{0, 0, 0, 0};
+    if (r < Tn && i < Tpad * CPR) {
+      kv[u] = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + D + c * 8);
+      vv[u] = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + 2 * D + c * 8);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < MAXC; ++u) {
+    const int i = tid + u * nthr;
+    if (i < Tpad * CPR) {
+      const int r = i / CPR, c = i - r * CPR;
+      *reinterpret_cast<uint4*>(Ks + (size_t)r * ldk + c * 8) = kv[u];
+      *reinterpret_cast<uint4*>(Vs + (size_t)r * LDV + c * 8) = vv[u];
+    }
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int q0 = wave * 32;
+  if (q0 >= Tn) return;  // whole wave: EXEC stays all-ones for the transposed reads below
+  const int col = lane & 31, hh = lane >> 5;
+  const int q = q0 + col;
+  const int qc = q < Tn ? q : Tn - 1;
+  const bf16* qrow = base + (size_t)qc * ld;
+  bf16x8 qf[DH / 16];
+#pragma unroll
+  for (int s2 = 0; s2 < DH / 16; ++s2) qf[s2] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s2 + 8 * hh);
+  // transposed-read lane roles: group g = lane >> 4 reads keys k0 + 4*(g>>1) + qq, d columns 16*(g&1) + 4*pp
+  const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+  const int trow = 4 * (g >> 1) + qq, tcol = 16 * (g & 1) + 4 * pp;
+
+  f32x16 O[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) O[dt][r] = 0.0f;
+  const float c = scale_log2e;
+  const float thr = 8.0f / c;  // 8 in log2 units, in raw-score units
+  float m_run = -INFINITY, l_run = 0.0f;
+  const int ntiles = Tpad / 32;
+  const bool ragged = (Tn & 31) != 0;
+  for (int kt = 0; kt < ntiles; ++kt) {
+    f32x16 S;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) S[r] = 0.0f;
+    const bf16* krow = Ks + (size_t)(32 * kt + col) * ldk + 8 * hh;
+#pragma unroll
+    for (int s2 = 0; s2 < DH / 16; ++s2) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(krow + 16 * s2);
+      S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s2], S, 0, 0, 0);
+    }
+    if (ragged && kt == ntiles - 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (key >= Tn) S[r] = -INFINITY;
+      }
+    }
+    float t0 = fmaxf(fmaxf(S[0], S[1]), S[2]), t1 = fmaxf(fmaxf(S[3], S[4]), S[5]);
+    float t2 = fmaxf(fmaxf(S[6], S[7]), S[8]), t3 = fmaxf(fmaxf(S[9], S[10]), S[11]);
+    float t4 = fmaxf(fmaxf(S[12], S[13]), S[14]);
+    float tmax = fmaxf(fmaxf(fmaxf(t0, t1), fmaxf(t2, t3)), fmaxf(t4, S[15]));
+    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+    const bool grow = tmax > m_run + thr;
+    if (__builtin_amdgcn_ballot_w64(grow)) {
+      const float m_new = grow ? tmax : m_run;
+      const float alpha = exp2f((m_run - m_new) * c);
+      l_run *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) O[dt] *= alpha;
+      m_run = m_new;
+    }
+    const float mc = -m_run * c;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      S[r] = __builtin_amdgcn_exp2f(fmaf(S[r], c, mc));
+      l_run += S[r];
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 pb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[j] = (bf16)S[8 * s2 + j];
+      const int k0 = 32 * kt + 16 * s2;
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        // A operand = V^T rows (d) x keys k0 + 8(j>>2) + 4hh + (j&3): two 4-key transposed reads
+        const bf16* vp = Vs + (size_t)(k0 + trow) * LDV + 32 * dt + tcol;
+        const attn_s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((attn_lds_s4*)vp);
+        const attn_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((attn_lds_s4*)(vp + 8 * LDV));
+        typedef __attribute__((ext_vector_type(8))) short s8;
+        s8 av;
+        av[0] = lo[0]; av[1] = lo[1]; av[2] = lo[2]; av[3] = lo[3];
+        av[4] = hi[0]; av[5] = hi[1]; av[6] = hi[2]; av[7] = hi[3];
+        O[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<bf16x8*>(&av), pb, O[dt], 0, 0, 0);
+      }
+    }
+  }
+  l_run += __shfl_xor(l_run, 32);
+  if (q >= Tn) return;
+  if (lse && hh == 0) lse[(size_t)bh * Tn + q] = m_run * c + log2f(l_run);
+  const float inv_l = 1.0f / l_run;
+  bf16* orow = out + ((size_t)b * Tn + q) * D + h * DH;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int gg = 0; gg < 4; ++gg) {
+      const int d = 32 * dt + 8 * gg + 4 * hh;
+      f32x4 v{O[dt][4 * gg] * inv_l, O[dt][4 * gg + 1] * inv_l, O[dt][4 * gg + 2] * inv_l, O[dt][4 * gg + 3] * inv_l};
+      store4(orow + d, v);
+    }
+}
+
 template <typename T, int DH>
 static int mha_launch(const void* qkv, void* out, int B, int Tn, int H, float scale, hipStream_t st,
                       float* lse = nullptr) {
   const int Tpad = (Tn + 31) / 32 * 32;
   const int nthr = 64 * (Tpad / 32);
-  const size_t lds = ((size_t)Tpad * (DH + AttnCfg<T>::KPAD) + (size_t)DH * (Tpad + AttnCfg<T>::VPAD)) * sizeof(T);
+  const bool lean = sizeof(T) == 2 && !getenv("TMAE_MHA_PLAIN");
+  const size_t lds = lean ? ((size_t)Tpad * (DH + 8) + (size_t)Tpad * AttnTr<DH>::LDV) * 2
+                          : ((size_t)Tpad * (DH + AttnCfg<T>::KPAD) + (size_t)DH * (Tpad + AttnCfg<T>::VPAD)) * sizeof(T);
   TMAE_REQUIRE(nthr <= 1024 && lds <= 160 * 1024, "tmae_mha_fwd: sequence length %d too long", Tn);
+  TMAE_REQUIRE(!lean || Tpad * (DH / 8) <= nthr * 8, "tmae_mha_fwd: sequence length %d too long", Tn);
   if (B * H == 0 || Tn == 0) return TMAE_OK;
-  hipLaunchKernelGGL((mha_fwd_kernel<T, DH>), dim3(B * H), dim3(nthr), lds, st, (const T*)qkv, (T*)out, lse, Tn, H,
-                     Tpad, scale * 1.4426950408889634f);
+  if (lean)
+    hipLaunchKernelGGL((mha_fwd_bf16_kernel<DH>), dim3(B * H), dim3(nthr), lds, st, (const bf16*)qkv, (bf16*)out, lse,
+                       Tn, H, Tpad, scale * 1.4426950408889634f);
+  else
+    hipLaunchKernelGGL((mha_fwd_kernel<T, DH>), dim3(B * H), dim3(nthr), lds, st, (const T*)qkv, (T*)out, lse, Tn, H,
+                       Tpad, scale * 1.4426950408889634f);
   TMAE_LAUNCH_CHECK("tmae_mha_fwd");
 }
 

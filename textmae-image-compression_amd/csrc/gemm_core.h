@@ -353,6 +353,173 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
                              tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
 }
 
+// ------------------------------------------------------------------ phased kernel (8 waves, 256x256, bf16)
+// cdna_hip_programming.md §5 "256^2 8-phase template", restated for this core's sources and epilogues.
+// A K-tile (64 deep) runs as 4 phases, one per output quadrant of every wave (W-half qa x X-half qb of the
+// wave's 128 x 64 block): (qa0,qb0) (qa0,qb1) (qa1,qb0) (qa1,qb1); fragments are read once per tile
+// (W-qa0 + X-qb0 in phase 0, X-qb1 in 1, W-qa1 in 2, nothing in 3) and kept in registers.
+// The tile image is cut into four "half-tiles" of 128 LDS rows each (W-qa0, X-qb0, X-qb1, W-qa1, the order
+// their regions are released); every phase issues ONE half-tile (2 LDS-DMA per thread) of the tile two
+// ahead into the region the previous phase released, so 5 half-tiles stay in flight: a uniform counted
+// s_waitcnt vmcnt(10) + raw s_barrier closes every phase (never vmcnt(0) in the loop).
+//   issue order: p0(t): W-qa1(t+1)  p1(t): W-qa0(t+2)  p2(t): X-qb0(t+2)  p3(t): X-qb1(t+2)
+// RAW: a half-tile read in phase p was retired by the vmcnt before the barrier closing phase p-1.
+// WAR: each region is restaged one phase after the phase whose barrier follows its last ds_read.
+__device__ __forceinline__ void s_barrier_raw() { __builtin_amdgcn_s_barrier(); }
+
+template <class WS, class XS, class EPI>
+__global__ void __launch_bounds__(512, 1)
+gemm_phased_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
+  constexpr int BN = 256, BM = 256, NW = 8, WGN = 2;
+  constexpr int WN = 128, WM = 64, TN = 8, TM = 4;
+  constexpr int IMG_W = BN * 128, STAGE = (BN + BM) * 128;  // bytes
+  __shared__ __attribute__((aligned(16))) uint4 lds[2 * STAGE / 16];
+
+  const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
+  ws.batch(b1, b2);
+  xs.batch(b1, b2);
+  epi.batch(b1, b2);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave % WGN, wm = wave / WGN;
+  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
+  const int nk = (K + 63) / 64;
+  int tn, tm;
+  tile_order(xcd_remap(blockIdx.x, gridDim.x), ntn, ntm, tn, tm);
+
+  // DMA slots: half-tile h (0 W-qa0, 1 X-qb0, 2 X-qb1, 3 W-qa1), round r: this wave's 8 image rows
+  const int w8 = 8 * wave, lr = lane >> 3, pch = lane & 7;
+  int row0[4][2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    row0[0][r] = 128 * r + w8;                                  // W rows {0-63, 128-191}
+    row0[3][r] = 128 * r + 64 + w8;                             // W rows {64-127, 192-255}
+    row0[1][r] = 128 * r + 64 * (wave >> 2) + 8 * (wave & 3);    // X rows {0-31,64-95 | 128-159,192-223}
+    row0[2][r] = row0[1][r] + 32;
+  }
+  typename WS::Row wrow[2][2];
+  typename XS::Row xrow[2][2];
+  int chk[4][2];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int row = row0[h][r] + lr;
+      chk[h][r] = pch ^ ((row >> 1) & 7);
+    }
+    wrow[0][r] = ws.row(tn * BN + row0[0][r] + lr);
+    wrow[1][r] = ws.row(tn * BN + row0[3][r] + lr);
+    xrow[0][r] = xs.row(tm * BM + row0[1][r] + lr);
+    xrow[1][r] = xs.row(tm * BM + row0[2][r] + lr);
+  }
+  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
+  const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // rows 8*wave.. of each half-tile round, as LDS byte offsets (wave-uniform)
+  auto issue = [&](int h, int kt) {
+    const unsigned sb = lds_base + (unsigned)(kt & 1) * STAGE;
+    const bool live = kt < nk;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      unsigned rowu;
+      const void* src;
+      if (h == 0 || h == 3) {
+        rowu = (h == 0 ? 128u * r : 128u * r + 64u) + 8u * wave_u;
+        src = live ? ws.addr(wrow[h == 3][r], kt, chk[h][r]) : (const void*)g_tmae_zero_page;
+        glds16(src, sb + rowu * 128u);
+      } else {
+        rowu = 128u * r + 64u * (wave_u >> 2) + 8u * (wave_u & 3) + (h == 2 ? 32u : 0u);
+        src = live ? xs.addr(xrow[h == 2][r], kt, chk[h][r]) : (const void*)g_tmae_zero_page;
+        glds16(src, sb + IMG_W + rowu * 128u);
+      }
+    }
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 wa[4][2], xb0[2][2], xb1[2][2];
+  auto read_w = [&](const uint4* base, int qa) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r = wn * WN + 16 * (4 * qa + i) + fr;
+        const int c = 4 * s + fq;
+        uint4 u = base[r * 8 + (c ^ ((r >> 1) & 7))];
+        wa[i][s] = *reinterpret_cast<bf16x8*>(&u);
+      }
+  };
+  auto read_x = [&](const uint4* base, int qb, bf16x8 (&xb)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int r = wm * WM + 16 * (2 * qb + j) + fr;
+        const int c = 4 * s + fq;
+        uint4 u = base[(BN + r) * 8 + (c ^ ((r >> 1) & 7))];
+        xb[j][s] = *reinterpret_cast<bf16x8*>(&u);
+      }
+  };
+  auto mfma_q = [&](int qa, int qb, const bf16x8 (&xb)[2][2]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 * qa + i][2 * qb + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][s], xb[j][s], acc[4 * qa + i][2 * qb + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto close_phase = [&]() {
+    asm volatile("s_waitcnt vmcnt(10)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    s_barrier_raw();
+  };
+
+  if (nk > 0) {
+    // prologue: tile 0 complete, tile 1's first three half-tiles (the steady-state picture at a tile start)
+    issue(0, 0); issue(1, 0); issue(2, 0); issue(3, 0);
+    issue(0, 1); issue(1, 1); issue(2, 1);
+    close_phase();
+    for (int kt = 0; kt < nk; ++kt) {
+      const uint4* base = lds + (kt & 1) * (STAGE / 16);
+      // phase 0: (qa0, qb0)
+      issue(3, kt + 1);
+      read_w(base, 0);
+      read_x(base, 0, xb0);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_q(0, 0, xb0);
+      close_phase();
+      // phase 1: (qa0, qb1)
+      issue(0, kt + 2);
+      read_x(base, 1, xb1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_q(0, 1, xb1);
+      close_phase();
+      // phase 2: (qa1, qb0)
+      issue(1, kt + 2);
+      read_w(base, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_q(1, 0, xb0);
+      close_phase();
+      // phase 3: (qa1, qb1)
+      issue(2, kt + 2);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_q(1, 1, xb1);
+      close_phase();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead DMA lands before the ring is reused
+  s_barrier_raw();
+  static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= 2 * STAGE, "epilogue region exceeds the LDS ring");
+  epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
+                           tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
+}
+
 // ------------------------------------------------------------------ ring kernel (8 waves, bf16)
 // BK = 32 (64-B LDS rows, 4 x 16-B chunks), a 4-slot LDS ring of (BN+BM) x 64 B, up to 4 K-steps of
 // LDS-DMA in flight, and the MFMA fragments register-double-buffered: right after the barrier that
@@ -640,6 +807,16 @@ static int launch_ring(const char* name, const WS& ws, const XS& xs, const EPI& 
   TMAE_LAUNCH_CHECK(name);
 }
 
+template <class WS, class XS, class EPI>
+static int launch_phased(const char* name, const WS& ws, const XS& xs, const EPI& epi, int M, int N, int K, int n1,
+                         int n2, hipStream_t st) {
+  const int tiles = ceil_div(N, 256) * ceil_div(M, 256);
+  if (tiles == 0 || n1 * n2 == 0) return TMAE_OK;
+  hipLaunchKernelGGL((gemm_phased_kernel<WS, XS, EPI>), dim3(tiles, n1 * n2), dim3(512), 0, st, ws, xs, epi, M, N, K,
+                     n2);
+  TMAE_LAUNCH_CHECK(name);
+}
+
 template <bool GLDS, typename T, class XS, class EPI>
 static int launch_gemm(const char* name, const T* w, long long ws1, long long ws2, int N, int K, const XS& xs,
                        const EPI& epi, int M, int n1 = 1, int n2 = 1, hipStream_t st = 0) {
@@ -649,6 +826,7 @@ static int launch_gemm(const char* name, const T* w, long long ws1, long long ws
   if constexpr (GLDS && sizeof(T) == 2) {
     if (tc.nw == 8) {
       if (gemm_knob("TMAE_GEMM_RING", 0)) return launch_ring<256, 256, 2>(name, ws, xs, epi, M, N, K, n1, n2, st);
+      if (gemm_knob("TMAE_GEMM_PHASED", 0)) return launch_phased(name, ws, xs, epi, M, N, K, n1, n2, st);
       return launch_one<GLDS, T, 256, 256, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
     }
   }
