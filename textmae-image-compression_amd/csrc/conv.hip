@@ -1,6 +1,7 @@
 // LIC 3x3 convolutions (h_a, h_s, cc_transform_mean/scale, lrp_transform; MCM.py:115-293) as
 // implicit GEMMs on the MFMA core, batched over independent problems (mean/scale chains of one
 // slice; slices 6..11 whose support is fixed), plus the Gaussian-conditional slice kernel.
+#include "conv_halo.h"
 #include "gemm_core.h"
 
 // conv + PixelShuffle(2) (compressai subpel_conv3x3, r=2): conv channel co = c*4 + i*2 + j goes to
@@ -98,6 +99,21 @@ template <typename OT> struct EpiLRP {
   }
 };
 
+// bf16 stride-1 12x12 convs go to the halo-staged kernel (conv_halo.h); everything else (f32 parity
+// path, strided / 6x6 / 3x3 maps, wide N) to the implicit GEMM
+template <typename T, class XS, class EPI>
+static int conv_go(const char* nm, const tmae_conv_args& a, const T* W, int N, int K, int M, const XS& xs,
+                   const EPI& epi, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    if (conv_halo_ok(a.H, a.W, a.stride, N, a.nb1 * a.nb2)) {
+      const HaloSrc hs{(const bf16*)a.x1, (const bf16*)a.x2, a.c1, a.ld1, a.ld2, a.c1 + a.c2,
+                       BStride{a.x1_s1, a.x1_s2}, BStride{a.x2_s1, a.x2_s2}};
+      return launch_conv_halo(nm, W, BStride{a.w_s1, a.w_s2}, hs, epi, N, a.n, a.nb1, a.nb2, st);
+    }
+  }
+  return launch_gemm<true, T>(nm, W, a.w_s1, a.w_s2, N, K, xs, epi, M, a.nb1, a.nb2, st);
+}
+
 template <typename T>
 static int conv_t(const tmae_conv_args& a, hipStream_t st) {
   const int e = Elt<T>::EPC;
@@ -115,7 +131,7 @@ static int conv_t(const tmae_conv_args& a, hipStream_t st) {
   const int M = xs.rows, K = xs.K, N = a.cout;
   const T* W = (const T*)a.w;
   const char* nm = "tmae_conv3x3";
-#define TMAE_GO(EPI) return launch_gemm<true, T>(nm, W, a.w_s1, a.w_s2, N, K, xs, EPI, M, a.nb1, a.nb2, st)
+#define TMAE_GO(EPI) return conv_go<T>(nm, a, W, N, K, M, xs, EPI, st)
   if (a.pixel_shuffle) {
     TMAE_REQUIRE(a.stride == 1, "tmae_conv3x3: pixel shuffle needs stride 1");
     if (a.y_f32) {

@@ -330,9 +330,10 @@ class _Executor:
         hs_out = [m.h_s_mean[0].out_channels, m.h_s_mean[2][0].out_channels // 4, m.h_s_mean[4].out_channels,
                   m.h_s_mean[6][0].out_channels // 4]
         hs_res = [self.hz, 2 * self.hz, 2 * self.hz, g]
-        self.hs_buf = [z(B * r * r, c, dtype=dt) for c, r in zip(hs_out, hs_res)]
-        self.LS = z(Mp, M, dtype=dt)
-        self.LM = z(Mp, M, dtype=dt)
+        # h_s_scale / h_s_mean run as one 2-problem launch per layer: [scale, mean] slabs
+        self.hs_buf = [z(2, B * r * r, c, dtype=dt) for c, r in zip(hs_out, hs_res)]
+        self.LSM = z(2, Mp, M, dtype=dt)
+        self.LS, self.LM = self.LSM[0], self.LSM[1]
         self.mid = [l.out_channels for l in m.cc_transform_mean[0] if isinstance(l, nn.Conv2d)]
         c0 = self.mid[0]
         self.PW = 3 * S * c0  # partial sums: [mean (S*c0) | lrp (S*c0) | scale (S*c0)]
@@ -379,16 +380,19 @@ class _Executor:
                      for l in m.g_s if isinstance(l, nn.ConvTranspose2d)]
         self.ha_w = [(cast(cw(l.weight)), l.bias.detach(), l.stride[0]) for l in m.h_a if isinstance(l, nn.Conv2d)]
 
-        def hs_w(seq):
+        def hs_convs(seq):  # (conv, followed by PixelShuffle) of h_s_mean / h_s_scale
             out = []
             for l in seq:
                 if isinstance(l, nn.Conv2d):
-                    out.append((cast(cw(l.weight)), l.bias.detach(), False))
+                    out.append((l, False))
                 elif isinstance(l, nn.Sequential):
-                    out.append((cast(cw(l[0].weight)), l[0].bias.detach(), True))
+                    out.append((l[0], True))
             return out
 
-        self.hsm_w, self.hss_w = hs_w(m.h_s_mean), hs_w(m.h_s_scale)
+        # [scale, mean] weights / biases of each layer stacked for the 2-problem launch
+        self.hs2_w = [(cast(torch.stack([cw(s.weight), cw(mn.weight)])),
+                       torch.stack([s.bias, mn.bias]).detach().contiguous(), ps)
+                      for (s, ps), (mn, _) in zip(hs_convs(m.h_s_scale), hs_convs(m.h_s_mean))]
 
         def convs(seq):
             return [l for l in seq if isinstance(l, nn.Conv2d)]
@@ -454,8 +458,7 @@ class _Executor:
                           table=self.eb_table)
 
         # ---- h_s (MCM.py:747-748)
-        self._h_s(self.hss_w, self.LS)
-        self._h_s(self.hsm_w, self.LM)
+        self._h_s()
 
         # ---- slice loop (MCM.py:751-787)
         self._slices(self._gc_forward(y_noise))
@@ -478,8 +481,7 @@ class _Executor:
         # z: symbols round(z - median); z_hat = symbols + median (= EB.decompress of its own strings)
         ops.eb_likelihood(eb, self.Z, B, N, hz * hz, lik=self.ZLIK, zhat=self.ZHAT, table=self.eb_table)
         zsym = ops.eb_symbols(eb, self.Z, B, N, hz * hz, table=self.eb_table)
-        self._h_s(self.hss_w, self.LS)
-        self._h_s(self.hsm_w, self.LM)
+        self._h_s()
         sym = torch.empty(S * B * sw * HW, dtype=torch.int32, device=self.device)
         idx = torch.empty_like(sym)
         self._slices(self._gc_compress(sym, idx))
@@ -504,8 +506,7 @@ class _Executor:
         zidx = eb._channel_indexes(hz * hz)
         zsym = np.stack([eb._decode(s, zidx) for s in strings[1]]).astype(np.int32)
         ops.eb_dequantize(eb, torch.from_numpy(zsym).to(self.device), B, N, hz * hz, self.ZHAT, table=self.eb_table)
-        self._h_s(self.hss_w, self.LS)
-        self._h_s(self.hsm_w, self.LM)
+        self._h_s()
         decoder = RansDecoder()
         decoder.set_stream(strings[0][0])
         self._slices(self._gc_decompress(decoder))
@@ -615,21 +616,24 @@ class _Executor:
             ops.gc_dequantize(sym, mu, ms_stride, sw, B, HW, nbs, sw, i0 * sw, self.SUPY, dt, M, self.YPRE, M)
         return step
 
-    def _h_s(self, layers, out_final):
+    def _h_s(self):
+        """h_s_scale -> LS and h_s_mean -> LM (MCM.py:747-748): both stacks have the same shapes and read
+        the same z_hat, so every layer is ONE launch of 2 problems ([scale, mean] weight / output slabs)"""
         B, dt = self.batch, self.dtype
-        x, cin, H = self.ZHAT, self.m.hyperprior_depth, self.hz
-        for j, (w, b, pshuf) in enumerate(layers):
-            last = j == len(layers) - 1
-            cout = w.shape[0]
-            out = out_final if last else self.hs_buf[j]
-            ops.conv3x3(x, cin, cin, B, H, H, w, b, out, out.shape[1], cout, self.dtype,
-                        act=ops.ACT_NONE if last else ops.ACT_GELU, pixel_shuffle=pshuf)
+        x, xs, cin, H = self.ZHAT, 0, self.m.hyperprior_depth, self.hz
+        for j, (w, b, pshuf) in enumerate(self.hs2_w):
+            last = j == len(self.hs2_w) - 1
+            cout = w.shape[1]
+            out = self.LSM if last else self.hs_buf[j]
+            ops.conv3x3(x, cin, cin, B, H, H, w, b, out, out.shape[2], cout, dt,
+                        act=ops.ACT_NONE if last else ops.ACT_GELU, pixel_shuffle=pshuf, nb=(1, 2),
+                        strides={"x1": (0, xs), "w": (0, w[0].numel()), "b": (0, cout), "y": (0, out[0].numel())})
             if pshuf:
                 H *= 2
                 cin = cout // 4
             else:
                 cin = cout
-            x = out
+            x, xs = out, out[0].numel()
 
     def _slices(self, gc_step):
         m, dt, B, g = self.m, self.dtype, self.batch, self.g
