@@ -19,26 +19,29 @@ __device__ __forceinline__ float softplus_t(float x) {  // F.softplus(beta=1, th
 }
 __device__ __forceinline__ float sigmoid_t(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-__global__ void eb_prep_kernel(tmae_eb_params p, float* __restrict__ tab, int C) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float* t = tab + (size_t)c * EB_PACK;
-  for (int j = 0; j < 3; ++j) {
-    t[0 + j] = softplus_t(p.matrix[0][c * 3 + j]);
-    t[3 + j] = p.bias[0][c * 3 + j];
-    t[6 + j] = tanhf(p.factor[0][c * 3 + j]);
+// per-channel parameter table [C][EB_PACK]: softplus(matrices), biases, tanh(factors), median.
+// One thread per table element (the table is tiny; a thread per channel walking 59 strided loads
+// was latency-bound at ~26 us).
+__global__ void __launch_bounds__(256) eb_prep_kernel(tmae_eb_params p, float* __restrict__ tab, int C) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C * EB_PACK) return;
+  const int c = i / EB_PACK, e = i - c * EB_PACK;
+  float v;
+  if (e < 9) {  // layer 0: matrix [C][3][1], bias [C][3][1], factor [C][3][1]
+    const int g = e / 3, j = e - 3 * g;
+    v = g == 0 ? softplus_t(p.matrix[0][c * 3 + j]) : g == 1 ? p.bias[0][c * 3 + j] : tanhf(p.factor[0][c * 3 + j]);
+  } else if (e < 54) {  // layers 1..3: matrix [C][3][3], bias [C][3][1], factor [C][3][1]
+    const int l = 1 + (e - 9) / 15, q = (e - 9) % 15;
+    v = q < 9 ? softplus_t(p.matrix[l][c * 9 + q])
+              : q < 12 ? p.bias[l][c * 3 + (q - 9)] : tanhf(p.factor[l][c * 3 + (q - 12)]);
+  } else if (e < 57) {  // layer 4: matrix [C][1][3]
+    v = softplus_t(p.matrix[4][c * 3 + (e - 54)]);
+  } else if (e == 57) {
+    v = p.bias[4][c];
+  } else {
+    v = p.quantiles[c * 3 + 1];  // _get_medians(): quantiles[:, :, 1:2]
   }
-  for (int l = 1; l <= 3; ++l) {
-    float* q = t + 9 + 15 * (l - 1);
-    for (int e = 0; e < 9; ++e) q[e] = softplus_t(p.matrix[l][c * 9 + e]);
-    for (int j = 0; j < 3; ++j) {
-      q[9 + j] = p.bias[l][c * 3 + j];
-      q[12 + j] = tanhf(p.factor[l][c * 3 + j]);
-    }
-  }
-  for (int k = 0; k < 3; ++k) t[54 + k] = softplus_t(p.matrix[4][c * 3 + k]);
-  t[57] = p.bias[4][c];
-  t[58] = p.quantiles[c * 3 + 1];  // _get_medians(): quantiles[:, :, 1:2]
+  tab[i] = v;
 }
 
 __device__ __forceinline__ float eb_logits(const float* t, float v) {
@@ -91,7 +94,7 @@ extern "C" int tmae_eb_likelihood_fwd(const float* z, const tmae_eb_params* para
                                       void* zhat, int zhat_dtype, float* table, int n, int C, int HW, void* stream) {
   TMAE_REQUIRE(params != nullptr && table != nullptr, "tmae_eb_likelihood_fwd: params/table required");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, st, *params, table, C);
+  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C * EB_PACK, 256)), dim3(256), 0, st, *params, table, C);
   const int total = n * HW * C;
   if (total > 0)
     hipLaunchKernelGGL(eb_likelihood_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, z, table, noise, lik,
@@ -122,7 +125,7 @@ extern "C" int tmae_eb_aux_loss(const tmae_eb_params* params, const float* targe
                                 void* stream) {
   TMAE_REQUIRE(params != nullptr && table != nullptr, "tmae_eb_aux_loss: params/table required");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, st, *params, table, C);
+  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C * EB_PACK, 256)), dim3(256), 0, st, *params, table, C);
   hipLaunchKernelGGL(eb_aux_loss_kernel, dim3(1), dim3(256), 0, st, table, params->quantiles, target, out, C);
   TMAE_LAUNCH_CHECK("tmae_eb_aux_loss");
 }
@@ -182,7 +185,7 @@ extern "C" int tmae_eb_pmf(const tmae_eb_params* params, float* table, const flo
                            float* pmf, float* tail, void* stream) {
   TMAE_REQUIRE(params && table && pmf_start && pmf && tail && C > 0 && max_length > 0, "tmae_eb_pmf: bad arguments");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, st, *params, table, C);
+  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C * EB_PACK, 256)), dim3(256), 0, st, *params, table, C);
   hipLaunchKernelGGL(eb_pmf_kernel, dim3(ceil_div(C * max_length, 256)), dim3(256), 0, st, table, pmf_start, C,
                      max_length, pmf, tail);
   TMAE_LAUNCH_CHECK("tmae_eb_pmf");
@@ -217,7 +220,7 @@ extern "C" int tmae_eb_symbols(const float* z, const tmae_eb_params* params, flo
                                int* symbols, void* stream) {
   TMAE_REQUIRE(z && params && table && symbols, "tmae_eb_symbols: bad arguments");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, st, *params, table, C);
+  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C * EB_PACK, 256)), dim3(256), 0, st, *params, table, C);
   const int total = n * HW * C;
   if (total > 0)
     hipLaunchKernelGGL(eb_symbols_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, z, table, C, HW, total,
@@ -229,7 +232,7 @@ extern "C" int tmae_eb_dequantize(const int* symbols, const tmae_eb_params* para
                                   void* zhat, int zhat_dtype, void* stream) {
   TMAE_REQUIRE(symbols && params && table && zhat, "tmae_eb_dequantize: bad arguments");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C, 64)), dim3(64), 0, st, *params, table, C);
+  hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C * EB_PACK, 256)), dim3(256), 0, st, *params, table, C);
   const int total = n * HW * C;
   if (total > 0)
     hipLaunchKernelGGL(eb_dequantize_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, symbols, table, C, HW,
