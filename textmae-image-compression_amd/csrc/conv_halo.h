@@ -6,23 +6,37 @@
 // times per K sweep, through L2, with tiles small enough (N <= 224 output channels) that address math
 // and LDS-DMA issue dominate its K-steps.  Here one workgroup owns ONE image x BN output channels:
 //   per 64-channel input chunk: the zero-padded 14x14 halo of that image goes global -> LDS once
-//                               (LDS-DMA, 16-B pieces, row-swizzled like the GEMM core);
-//   per (chunk, tap) K-step:    the BN x 64 weight slab of that tap streams into a 2-stage LDS ring and
+//                               (LDS-DMA, 16-B pieces);
+//   per (chunk, tap) K-step:    the BN x 64 weight slab of that tap streams into a 3-slot LDS ring and
 //                               the 144 output pixels read their shifted halo rows straight from LDS.
-// MFMA v_mfma_f32_16x16x32_bf16 issued swapped (A = weight rows, B = pixel rows) exactly as the GEMM
-// core, so the accumulator layout, the LDS-transposed epilogue (epilogue_lds) and every epilogue
-// functor (bias / GELU / addend / f32 copy / LRP) are shared with it.  4 waves: 2 along N x 2 along M,
-// each wave 5 M-fragments (160 rows >= 144; rows >= 144 are computed on a clamped halo row and dropped).
+// MFMA v_mfma_f32_16x16x32_bf16 issued swapped (A = weight rows, B = pixel rows) as in the GEMM core,
+// so every epilogue functor (bias / GELU / addend / f32 copy / LRP) is shared with it.
+//
+// Addressing is built so the K loop carries no address arithmetic (PMC on the first version: 5 VALU
+// and 4 SALU instructions per MFMA, 38 % of LDS cycles lost to bank conflicts):
+//   * halo rows are LINEAR with a 144-B pitch (128 B of channels + 16 B pad), so the halo row of tap
+//     (ky, kx) is the tap-(0,0) row + (14 ky + kx) rows: with the nine taps unrolled every fragment
+//     read is a per-lane base + a compile-time offset (ds_read_b128 offset field);
+//   * an MFMA M-fragment is a 4x4 pixel block (9 blocks tile the 12x12 map): with the 144-B pitch
+//     its reads are 2-way bank conflicted at worst for every tap (tools: exhaustive check over the
+//     gfx950 ds_read_b128 lane groups; no 16-B layout is conflict-free because a lane group mixes two
+//     k-chunks), and the epilogue maps fragment rows back to pixels;
+//   * the weight ring slot of tap t is t % 3 (nine taps per chunk), also compile-time.
+// 4 waves: 2 along N x 2 along M, 5 M-fragments each (block 9 of the second M-wave is padding).
 #pragma once
 
 #include "gemm_core.h"
 
 namespace halo {
-constexpr int G = 12;          // map side
-constexpr int HP = 14;         // halo side
-constexpr int PIX = G * G;     // 144 output rows per image
-constexpr int HROWS = 224;     // halo rows staged (196 used), 28 LDS-DMA rounds of 8 rows
-constexpr int TMF = 5;         // M fragments per wave
+constexpr int G = 12;                      // map side
+constexpr int HP = 14;                     // halo side
+constexpr int PIX = G * G;                 // 144 output pixels per image
+constexpr int HR = HP * HP;                // 196 halo rows
+constexpr int PITCH = 144;                 // bytes per halo row (8 channel chunks + 1 pad chunk)
+constexpr int HCH = HR * (PITCH / 16);     // 16-B LDS chunks of one halo image (pads included)
+constexpr int HJ = (HCH + 255) / 256;      // LDS-DMA rounds per wave (4 waves x 64 lanes) = 7
+constexpr int HSLOT = HJ * 256 * 16;       // bytes of one halo slot (tail of the last round included)
+constexpr int TMF = 5;                     // M fragments per wave
 }  // namespace halo
 
 // channels [0, c1) of a pixel from x1 (row stride ld1), [c1, Cin) from x2 (torch.cat without a copy)
@@ -35,14 +49,10 @@ struct HaloSrc {
     x1 += bs1.at(b1, b2);
     x2 += bs2.at(b1, b2);
   }
-  // halo row hr (= hy * 14 + hx) of image img, 8 channels from ch; zero outside the map / channel range
-  __device__ const void* addr(int img, int hr, int ch) const {
-    if (hr >= halo::HP * halo::HP || ch >= Cin) return g_tmae_zero_page;
-    const int hy = hr / halo::HP;
-    const int iy = hy - 1, ix = hr - hy * halo::HP - 1;
-    if ((unsigned)iy >= (unsigned)halo::G || (unsigned)ix >= (unsigned)halo::G) return g_tmae_zero_page;
-    const size_t pix = (size_t)img * halo::PIX + iy * halo::G + ix;
-    return ch < c1 ? (const void*)(x1 + pix * ld1 + ch) : (const void*)(x2 + pix * ld2 + (ch - c1));
+  // pixel pix (image-major) channels [ch, ch + 8); zero page for padding / out-of-range channels
+  __device__ const void* addr(int pix, int ch) const {
+    if (pix < 0 || ch >= Cin) return g_tmae_zero_page;
+    return ch < c1 ? (const void*)(x1 + (size_t)pix * ld1 + ch) : (const void*)(x2 + (size_t)pix * ld2 + (ch - c1));
   }
 };
 
@@ -53,8 +63,35 @@ __device__ __forceinline__ void halo_wait_barrier() {
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
-// Pipeline: weights in a 3-slot ring (the slab of step k+2 is issued while step k computes, so each DMA
-// has a whole K-step of slack), halo in 2 slots (chunk c+1 issued at tap 0 of chunk c).  LDS: BN=64
+// Epilogue through each wave's LDS region (as epilogue_lds in gemm_core.h): fragment f = 4x4 block
+// (f / 3, f % 3); transposed row `row` of a fragment is pixel (4 by + row / 4, 4 bx + row % 4).
+template <int TN, int WN, class EPI>
+__device__ __forceinline__ void halo_epilogue(const EPI& epi, const f32x4 (&acc)[TN][halo::TMF], float* region, int n0,
+                                              int img, int wm, int lane, int N) {
+  constexpr int ST = EpiRegion<WN>::ST, LPR = WN / 8, RPI = 64 / LPR;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int rr = lane / LPR, cc = lane - rr * LPR;
+#pragma unroll
+  for (int j = 0; j < halo::TMF; ++j) {
+    const int f = wm * halo::TMF + j;
+    if (f >= 9) break;  // wave-uniform
+    const int by = f / 3, bx = f - 3 * by;
+#pragma unroll
+    for (int i = 0; i < TN; ++i) *reinterpret_cast<f32x4*>(region + fr * ST + 16 * i + 4 * fq) = acc[i][j];
+#pragma unroll
+    for (int q = 0; q < 16 / RPI; ++q) {
+      const int row = q * RPI + rr;
+      const float* src = region + row * ST + 8 * cc;
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
+      const int p = (4 * by + (row >> 2)) * halo::G + 4 * bx + (row & 3);
+      epi_emit8(epi, img * halo::PIX + p, n0 + 8 * cc, lo, hi, N);
+    }
+  }
+}
+
+// Pipeline: weights in a 3-slot ring (the slab of step k+2 is issued while step k computes: a whole
+// K-step of slack per DMA), halo in 2 slots (chunk c+1 issued at tap 0 of chunk c).  LDS: BN=64
 // 3 x 8 KiB + 2 x 28 KiB = 80 KiB (two workgroups per CU), BN=128 104 KiB (one).
 template <int BN, class EPI>
 __global__ void __launch_bounds__(256, BN == 64 ? 2 : 1)
@@ -62,11 +99,12 @@ conv_halo_kernel(const bf16* __restrict__ w, BStride wst, HaloSrc src, EPI epi, 
   using namespace halo;
   constexpr int WN = BN / 2, TN = WN / 16;
   constexpr int NWS = 3;  // weight ring slots
-  constexpr int WBYTES = BN * 128, HBYTES = HROWS * 128, HOFF = NWS * WBYTES;
-  constexpr int WJ = BN / 32, HJ = HROWS / 32;  // LDS-DMA rounds per wave (4 waves x 8 rows each)
+  constexpr int WBYTES = BN * 128, HOFF = NWS * WBYTES;
+  constexpr int WJ = BN / 32;  // weight LDS-DMA rounds per wave (4 waves x 8 rows each)
   static_assert(TN >= 2 && WN % 32 == 0, "conv_halo: tile");
-  static_assert(4 * EpiRegion<WN>::FLOATS * 4 <= NWS * WBYTES + 2 * HBYTES, "conv_halo: epilogue region");
-  __shared__ __attribute__((aligned(16))) uint4 lds[(NWS * WBYTES + 2 * HBYTES) / 16];
+  static_assert(4 * EpiRegion<WN>::FLOATS * 4 <= HOFF + 2 * HSLOT, "conv_halo: epilogue region");
+  __shared__ __attribute__((aligned(16))) uint4 lds[(HOFF + 2 * HSLOT) / 16];
+  const unsigned char* lb = reinterpret_cast<const unsigned char*>(lds);
 
   const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
   w += wst.at(b1, b2);
@@ -74,17 +112,17 @@ conv_halo_kernel(const bf16* __restrict__ w, BStride wst, HaloSrc src, EPI epi, 
   epi.batch(b1, b2);
   const int Cin = src.Cin, ldw = 9 * Cin;
   const int ntn = (N + BN - 1) / BN;
-  const int t = xcd_remap(blockIdx.x, gridDim.x);
-  const int img = t / ntn, tn = t - img * ntn;
+  const int t0 = xcd_remap(blockIdx.x, gridDim.x);
+  const int img = t0 / ntn, tn = t0 - img * ntn;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave & 1, wm = wave >> 1;
   const int nchunk = (Cin + 63) >> 6, nk = 9 * nchunk;
-
-  // LDS-DMA roles: one glds16 moves 8 LDS rows x 128 B; lane -> row +(lane >> 3), 16-B slot (lane & 7).
-  // Slot s of row r holds source chunk s ^ ((r >> 1) & 7) (the GEMM core's swizzle).
-  const int lr = lane >> 3, pch = lane & 7;
   const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
+
+  // weight DMA roles: glds16 = 8 LDS rows x 128 B; lane -> row +(lane >> 3), slot (lane & 7) holding
+  // source chunk slot ^ ((row >> 1) & 7) (the GEMM core's swizzle)
+  const int lr = lane >> 3, pch = lane & 7;
   const bf16* wrow[WJ];
   int wch[WJ];
 #pragma unroll
@@ -93,9 +131,8 @@ conv_halo_kernel(const bf16* __restrict__ w, BStride wst, HaloSrc src, EPI epi, 
     wrow[j] = n < N ? w + (size_t)n * ldw : nullptr;
     wch[j] = 8 * (pch ^ ((r >> 1) & 7));
   }
-  auto issue_w = [&](int stage, int kk) {
-    const int chunk = kk / 9, tap = kk - 9 * chunk;
-    const unsigned sb = lds_base + (unsigned)stage * WBYTES;
+  auto issue_w = [&](int slot, int chunk, int tap) {
+    const unsigned sb = lds_base + (unsigned)slot * WBYTES;
 #pragma unroll
     for (int j = 0; j < WJ; ++j) {
       const int ch = 64 * chunk + wch[j];
@@ -103,14 +140,41 @@ conv_halo_kernel(const bf16* __restrict__ w, BStride wst, HaloSrc src, EPI epi, 
       glds16(s, sb + (8u * (wave_u + 4u * j)) * 128u);
     }
   };
-  auto issue_h = [&](int stage, int chunk) {
-    const unsigned sb = lds_base + (unsigned)HOFF + (unsigned)stage * HBYTES;
+  // halo DMA roles: 16-B chunk q = 64 (wave + 4 j) + lane of the linear image -> halo row q / 9,
+  // channel chunk q % 9 (8 = the pad); source pixel (or -1 for the zero border / pads / tail)
+  int hpix[HJ], hch[HJ];
 #pragma unroll
-    for (int j = 0; j < HJ; ++j) {
-      const int r = 8 * (wave + 4 * j) + lr;
-      glds16(src.addr(img, r, 64 * chunk + 8 * (pch ^ ((r >> 1) & 7))), sb + (8u * (wave_u + 4u * j)) * 128u);
-    }
+  for (int j = 0; j < HJ; ++j) {
+    const int q = 64 * (wave + 4 * j) + lane;
+    const int row = q / 9, sl = q - 9 * row;
+    const int hy = row / HP, hx = row - hy * HP;
+    const bool ok = row < HR && sl < 8 && hy >= 1 && hy <= G && hx >= 1 && hx <= G;
+    hpix[j] = ok ? img * PIX + (hy - 1) * G + (hx - 1) : -1;
+    hch[j] = 8 * sl;
+  }
+  auto issue_h = [&](int slot, int chunk) {
+    const unsigned sb = lds_base + (unsigned)HOFF + (unsigned)slot * HSLOT;
+#pragma unroll
+    for (int j = 0; j < HJ; ++j) glds16(src.addr(hpix[j], 64 * chunk + hch[j]), sb + 1024u * (wave_u + 4u * j));
   };
+
+  // per-lane fragment read offsets (bytes): weights per (i, s), halo per j (tap (0,0), k-chunk fq)
+  const int fr = lane & 15, fq = lane >> 4;
+  int woff[TN][2];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int r = wn * WN + 16 * i + fr;
+      woff[i][s] = r * 128 + 16 * ((4 * s + fq) ^ ((r >> 1) & 7));
+    }
+  int hoff[TMF];
+#pragma unroll
+  for (int j = 0; j < TMF; ++j) {
+    const int f = wm * TMF + j, by = f / 3, bx = f - 3 * by;
+    const int y = 4 * by + (fr >> 2), x = 4 * bx + (fr & 3);
+    hoff[j] = f < 9 ? (y * HP + x) * PITCH + 16 * fq : 16 * fq;  // padding block: any in-range rows
+  }
 
   f32x4 acc[TN][TMF];
 #pragma unroll
@@ -118,71 +182,46 @@ conv_halo_kernel(const bf16* __restrict__ w, BStride wst, HaloSrc src, EPI epi, 
 #pragma unroll
     for (int j = 0; j < TMF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int fr = lane & 15, fq = lane >> 4;
-  int hr0[TMF];  // halo row of tap (0, 0) for this lane's pixel in each M fragment
-#pragma unroll
-  for (int j = 0; j < TMF; ++j) {
-    const int p = 16 * (wm * TMF + j) + fr;
-    const int y = p / G;
-    hr0[j] = p < PIX ? y * HP + (p - y * G) : 0;
-  }
-
   if (nk > 0) {
     // prologue: halo(0), w(0) landed; w(1) may stay in flight
     issue_h(0, 0);
-    issue_w(0, 0);
-    if (nk > 1) {
-      issue_w(1, 1);
-      halo_wait_barrier<WJ>();
-    } else {
-      halo_wait_barrier<0>();
-    }
-    int chunk = 0, tap = 0, wslot = 0;
-    for (int kk = 0; kk < nk; ++kk) {
-      // slot (kk+2)%3 was last read by step kk-1, retired by the barrier that closed it
-      const bool more = kk + 2 < nk;
-      if (more) issue_w(wslot == 0 ? 2 : wslot - 1, kk + 2);
-      const bool hnext = tap == 0 && chunk + 1 < nchunk;  // implies `more` (9 steps per chunk)
-      if (hnext) issue_h((chunk + 1) & 1, chunk + 1);
-      const uint4* wb = lds + wslot * (WBYTES / 16);
-      const unsigned char* hb = reinterpret_cast<const unsigned char*>(lds) + HOFF + (chunk & 1) * HBYTES;
-      const int ky = (tap * 11) >> 5;  // tap / 3
-      const int toff = ky * HP + (tap - 3 * ky);
+    issue_w(0, 0, 0);
+    issue_w(1, 0, 1);
+    halo_wait_barrier<WJ>();
+    for (int chunk = 0; chunk < nchunk; ++chunk) {
+      const unsigned char* hb = lb + HOFF + (chunk & 1) * HSLOT;
+      const bool last = chunk + 1 == nchunk;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int c = 4 * s + fq;
-        bf16x8 a[TN], b[TMF];
+      for (int t = 0; t < 9; ++t) {
+        // slot (t+2)%3 was last read by the previous step, retired by the barrier that closed it
+        const bool more = !last || t + 2 < 9;
+        if (more) issue_w((t + 2) % 3, t + 2 < 9 ? chunk : chunk + 1, (t + 2) % 9);
+        const bool hnext = t == 0 && !last;
+        if (hnext) issue_h((chunk + 1) & 1, chunk + 1);
+        const unsigned char* wb = lb + (t % 3) * WBYTES;
+        const int toff = ((t / 3) * HP + (t % 3)) * PITCH;
 #pragma unroll
-        for (int i = 0; i < TN; ++i) {
-          const int r = wn * WN + 16 * i + fr;
-          uint4 u = wb[r * 8 + (c ^ ((r >> 1) & 7))];
-          a[i] = *reinterpret_cast<bf16x8*>(&u);
+        for (int s = 0; s < 2; ++s) {
+          bf16x8 a[TN], b[TMF];
+#pragma unroll
+          for (int i = 0; i < TN; ++i) a[i] = *reinterpret_cast<const bf16x8*>(wb + woff[i][s]);
+#pragma unroll
+          for (int j = 0; j < TMF; ++j) b[j] = *reinterpret_cast<const bf16x8*>(hb + hoff[j] + toff + 64 * s);
+#pragma unroll
+          for (int i = 0; i < TN; ++i)
+#pragma unroll
+            for (int j = 0; j < TMF; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
         }
-#pragma unroll
-        for (int j = 0; j < TMF; ++j) {
-          const int hr = hr0[j] + toff;
-          uint4 u = *reinterpret_cast<const uint4*>(hb + hr * 128 + 16 * (c ^ ((hr >> 1) & 7)));
-          b[j] = *reinterpret_cast<bf16x8*>(&u);
-        }
-#pragma unroll
-        for (int i = 0; i < TN; ++i)
-#pragma unroll
-          for (int j = 0; j < TMF; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-      }
-      // w(kk+1) must have landed for the next step; this step's own issues (w(kk+2), halo) stay in flight
-      if (hnext) halo_wait_barrier<WJ + HJ>();
-      else if (more) halo_wait_barrier<WJ>();
-      else halo_wait_barrier<0>();
-      wslot = wslot == NWS - 1 ? 0 : wslot + 1;
-      if (++tap == 9) {
-        tap = 0;
-        ++chunk;
+        // w(next step) must have landed; this step's own issues (w(+2), halo) stay in flight
+        if (hnext) halo_wait_barrier<WJ + HJ>();
+        else if (more) halo_wait_barrier<WJ>();
+        else halo_wait_barrier<0>();
       }
     }
   }
-  // rows >= 144 of the last fragments belong to no pixel: the epilogue's row limit drops them
-  epilogue_lds<TN, TMF, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS, tn * BN + wn * WN,
-                            img * PIX + wm * (16 * TMF), lane, (img + 1) * PIX, N);
+  halo_epilogue<TN, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS, tn * BN + wn * WN,
+                        img, wm, lane, N);
 }
 
 // BN: the tile with the least channel padding; 64 when 128 would leave the chip short of workgroups
