@@ -302,7 +302,8 @@ int tmae_colsum(const void* x, int x_dtype, int ld, int rows, int C, int row_gro
  * dxop (optional, op_dtype) = the same; dgamma / dbeta (=/+=).  work >= 2*D*(rows/8 + 4) floats. */
 int tmae_layernorm_bwd(const float* x, const float* gamma, const float* dy, const float* dres, float* dx32, void* dxop,
                        int op_dtype, int rows, int D, int row_group, int group_stride, int row_offset, float eps,
-                       float* work, long long work_elems, float* dgamma, float* dbeta, int accumulate, void* stream);
+                       float* work, long long work_elems, float* dgamma, float* dbeta, float* dres_colsum, int accumulate,
+                       void* stream);
 
 /* subpel_conv3x3 (PixelShuffle(2)) backward: dpre [n*H*W][C4] = unshuffle(dy) * gelu'(pre) (pre optional) */
 int tmae_unshuffle_bwd(const void* dy, int dy_f32, int ldy, const void* pre, int ldp, void* out, int n, int H, int W,

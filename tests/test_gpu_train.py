@@ -153,10 +153,11 @@ def test_layernorm_bwd_remap(T):
     dres = _rnd(B * Tn, D, seed=20)
     dx = torch.zeros(B * Tn, D, device="cuda")
     dxop = torch.zeros(B * Tn, D, device="cuda", dtype=torch.bfloat16)
-    dg, db = torch.empty(D, device="cuda"), torch.empty(D, device="cuda")
+    dg, db, drs = torch.empty(D, device="cuda"), torch.empty(D, device="cuda"), torch.empty(D, device="cuda")
     T.layernorm_bwd(x.cuda(), gamma.cuda(), dy.cuda(), dx, len(rows), D, 1e-6, dg, db, dres=dres.cuda(), dxop=dxop,
-                    row_group=Tn - 1, group_stride=Tn, row_offset=1)
+                    row_group=Tn - 1, group_stride=Tn, row_offset=1, dres_colsum=drs)
     torch.cuda.synchronize()
+    assert _rel(drs, dres[rows].sum(0)) < 1e-5  # bias gradient of the residual's Linear, folded in
     ref = xr.grad.clone()
     ref[rows] += dres[rows]
     assert _rel(dx, ref) < 1e-5

@@ -118,7 +118,7 @@ SIGNATURES = {
     "tmae_conv_dgrad": [ctypes.POINTER(ConvDgradArgs), I, P],
     "tmae_relayout": [P, P, I, I, I, I, I, LL, LL, LL, LL, P],
     "tmae_colsum": [P, I, I, I, I, I, I, I, P, LL, P, I, P],
-    "tmae_layernorm_bwd": [P, P, P, P, P, P, I, I, I, I, I, I, F, P, LL, P, P, I, P],
+    "tmae_layernorm_bwd": [P, P, P, P, P, P, I, I, I, I, I, I, F, P, LL, P, P, P, I, P],
     "tmae_unshuffle_bwd": [P, I, I, P, I, P, I, I, I, I, I, P],
     "tmae_gelu_bwd": [P, I, P, P, LL, I, P],
     "tmae_lrp_bwd": [P, I, P, I, P, I, P, I, P, I, I, I, I, P],

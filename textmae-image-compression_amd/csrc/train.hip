@@ -331,10 +331,11 @@ colsum_partial_kernel(const T* __restrict__ x, int ld, int rows, int C, int G, i
 }
 
 // fold [rows][C] partials over rows: 64 columns x 16 row-lanes per block, fixed-order LDS tree
-// (deterministic); columns [0, split) -> out0[c], [split, C) -> out1[c - split]
+// (deterministic); columns [0, split) -> out0[c], [split, split2) -> out1[c - split], [split2, C) ->
+// out2[c - split2]
 __global__ void __launch_bounds__(1024)
 fold_rows_kernel(const float* __restrict__ part, int rows, int C, float* __restrict__ out0, float* __restrict__ out1,
-                 int split, int accumulate) {
+                 int split, int accumulate, float* __restrict__ out2, int split2) {
   __shared__ float red[16][65];
   const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cx;
@@ -348,15 +349,15 @@ fold_rows_kernel(const float* __restrict__ part, int rows, int C, float* __restr
     __syncthreads();
   }
   if (ry == 0 && c < C) {
-    float* dst = c < split ? out0 + c : out1 + (c - split);
+    float* dst = c < split ? out0 + c : c < split2 ? out1 + (c - split) : out2 + (c - split2);
     *dst = accumulate ? *dst + red[0][cx] : red[0][cx];
   }
 }
 
 static void fold_rows(const float* part, int rows, int C, float* out0, float* out1, int split, int accumulate,
-                      hipStream_t st) {
+                      hipStream_t st, float* out2 = nullptr, int split2 = -1) {
   hipLaunchKernelGGL(fold_rows_kernel, dim3(ceil_div(C, 64)), dim3(1024), 0, st, part, rows, C, out0, out1, split,
-                     accumulate);
+                     accumulate, out2, split2 < 0 ? C : split2);
 }
 
 extern "C" int tmae_colsum(const void* x, int x_dtype, int ld, int rows, int C, int row_group, int group_stride,
@@ -383,7 +384,9 @@ extern "C" int tmae_colsum(const void* x, int x_dtype, int ld, int rows, int C, 
 // x rows remapped like the forward (source row sr = (r / G) * Gs + off + r % G); dy dense [rows][D] f32.
 // dx lands at row sr of dx32 (f32; + dres[sr] when given) and of dxop (operand dtype copy, optional).
 // Each wave walks a contiguous run of rows and keeps its dgamma / dbeta partial in registers -> part.
-template <typename OT, int VPL>
+// RS: also the column sums of dres (the bias gradient of the Linear whose output the residual adds:
+// fc2 before norm2's input gradient, proj before norm1's) -> a third partial block; part is [wave][3D].
+template <typename OT, int VPL, bool RS>
 __global__ void __launch_bounds__(256)
 layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ dy,
                      const float* __restrict__ dres, float* __restrict__ dx32, OT* __restrict__ dxop, int rows, int D,
@@ -391,10 +394,10 @@ layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamm
   const int lane = threadIdx.x & 63;
   const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int nch = D >> 2;
-  f32x4 dg[VPL], db[VPL], gm[VPL];
+  f32x4 dg[VPL], db[VPL], gm[VPL], dr[VPL];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
-    dg[i] = db[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dg[i] = db[i] = dr[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     const int c = lane + 64 * i;
     gm[i] = c < nch ? load4f(gamma + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -461,45 +464,58 @@ layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamm
         f32x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = rstd * (g[i][j] * gm[i][j] - sa - v[i][j] * sb);
-        if (dres) o += load4f(dres + (size_t)sr * D + 4 * c);
+        if (dres) {
+          const f32x4 rv = load4f(dres + (size_t)sr * D + 4 * c);
+          o += rv;
+          if (RS) dr[i] += rv;
+        }
         store4(dx32 + (size_t)sr * D + 4 * c, o);
         if (dxop) store4(dxop + (size_t)sr * D + 4 * c, o);
       }
     }
   }
-  float* pw = part + (size_t)wave * 2 * D;
+  float* pw = part + (size_t)wave * (RS ? 3 : 2) * D;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = lane + 64 * i;
     if (c < nch) {
       store4(pw + 4 * c, dg[i]);
       store4(pw + D + 4 * c, db[i]);
+      if (RS) store4(pw + 2 * D + 4 * c, dr[i]);
     }
   }
 }
 
-static int tmae_ln_fold(const float* part, int waves, int D, float* dg, float* db, int accumulate, hipStream_t st) {
-  fold_rows(part, waves, 2 * D, dg, db, D, accumulate, st);
+static int tmae_ln_fold(const float* part, int waves, int D, float* dg, float* db, float* drs, int accumulate,
+                        hipStream_t st) {
+  if (drs) fold_rows(part, waves, 3 * D, dg, db, D, accumulate, st, drs, 2 * D);
+  else fold_rows(part, waves, 2 * D, dg, db, D, accumulate, st);
   TMAE_LAUNCH_CHECK("tmae_layernorm_bwd");
 }
 
 extern "C" int tmae_layernorm_bwd(const float* x, const float* gamma, const float* dy, const float* dres, float* dx32,
                                   void* dxop, int op_dtype, int rows, int D, int row_group, int group_stride,
                                   int row_offset, float eps, float* work, long long work_elems, float* dgamma,
-                                  float* dbeta, int accumulate, void* stream) {
+                                  float* dbeta, float* dres_colsum, int accumulate, void* stream) {
   TMAE_REQUIRE(D % 4 == 0 && D <= 2048 && row_group > 0, "tmae_layernorm_bwd: D=%d", D);
   TMAE_REQUIRE(x && gamma && dy && dx32 && work && dgamma && dbeta, "tmae_layernorm_bwd: null argument");
+  TMAE_REQUIRE(!dres_colsum || dres, "tmae_layernorm_bwd: dres_colsum needs dres");
   hipStream_t st = (hipStream_t)stream;
+  const int np = dres_colsum ? 3 : 2;  // partial blocks per wave
   int waves = std::min(1024, std::max(4, rows / 8));
-  while ((long long)(waves + 4) * 2 * D > work_elems && waves > 4) waves /= 2;
+  while ((long long)(waves + 4) * np * D > work_elems && waves > 4) waves /= 2;
   const int rpw = ceil_div(std::max(rows, 1), waves);
   waves = ceil_div(ceil_div(std::max(rows, 1), rpw), 4) * 4;
-  TMAE_REQUIRE((long long)waves * 2 * D <= work_elems, "tmae_layernorm_bwd: workspace too small");
+  TMAE_REQUIRE((long long)waves * np * D <= work_elems, "tmae_layernorm_bwd: workspace too small");
   const int vpl = ceil_div(D / 4, 64);
   const dim3 grid(waves / 4);
-#define TMAE_LNB(OT, V)                                                                                              \
-  hipLaunchKernelGGL((layernorm_bwd_kernel<OT, V>), grid, dim3(256), 0, st, x, gamma, dy, dres, dx32, (OT*)dxop, rows, \
-                     D, row_group, group_stride, row_offset, eps, rpw, work)
+#define TMAE_LNB(OT, V)                                                                                               \
+  if (dres_colsum)                                                                                                    \
+    hipLaunchKernelGGL((layernorm_bwd_kernel<OT, V, true>), grid, dim3(256), 0, st, x, gamma, dy, dres, dx32,           \
+                       (OT*)dxop, rows, D, row_group, group_stride, row_offset, eps, rpw, work);                      \
+  else                                                                                                                \
+    hipLaunchKernelGGL((layernorm_bwd_kernel<OT, V, false>), grid, dim3(256), 0, st, x, gamma, dy, dres, dx32,          \
+                       (OT*)dxop, rows, D, row_group, group_stride, row_offset, eps, rpw, work)
 #define TMAE_LNB_V(OT)          \
   if (vpl <= 1) TMAE_LNB(OT, 1);  \
   else if (vpl <= 2) TMAE_LNB(OT, 2); \
@@ -518,7 +534,7 @@ extern "C" int tmae_layernorm_bwd(const float* x, const float* gamma, const floa
     tmae_set_error(TMAE_EHIP, "tmae_layernorm_bwd: launch failed: %s", hipGetErrorString(e));
     return TMAE_EHIP;
   }
-  return tmae_ln_fold(work, waves, D, dgamma, dbeta, accumulate, st);
+  return tmae_ln_fold(work, waves, D, dgamma, dbeta, dres_colsum, accumulate, st);
 }
 
 // ================================================================== elementwise backward pieces

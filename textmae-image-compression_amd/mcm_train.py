@@ -570,8 +570,7 @@ class TrainExec:
         H = blk.attn.num_heads
         f32 = dt == torch.float32
         # fc2 (+ GELU of fc1 in the data-gradient epilogue)
-        T.wgrad(dres_op, s.h, D, hid, rows, G(blk.mlp.fc2.weight), dt)
-        T.colsum(dres, rows, D, G(blk.mlp.fc2.bias))
+        T.wgrad(dres_op, s.h, D, hid, rows, G(blk.mlp.fc2.weight), dt)  # fc2.bias: folded into norm2's backward
         dh = self._e(rows, hid)
         T.dgrad_linear(dres_op, W.t(blk.mlp.fc2.weight), rows, D, hid, dt, out=dh, pre=s.hpre)
         # fc1
@@ -583,10 +582,9 @@ class TrainExec:
         dmid = torch.empty((rows, D), dtype=torch.float32, device=self.device)
         dmid_op = dmid if f32 else self._e(rows, D)
         T.layernorm_bwd(s.xmid, blk.norm2.weight, da2, dmid, rows, D, blk.norm2.eps, G(blk.norm2.weight),
-                        G(blk.norm2.bias), dres=dres, dxop=None if f32 else dmid_op)
+                        G(blk.norm2.bias), dres=dres, dxop=None if f32 else dmid_op, dres_colsum=G(blk.mlp.fc2.bias))
         # proj
-        T.wgrad(dmid_op, s.att, D, D, rows, G(blk.attn.proj.weight), dt)
-        T.colsum(dmid, rows, D, G(blk.attn.proj.bias))
+        T.wgrad(dmid_op, s.att, D, D, rows, G(blk.attn.proj.weight), dt)  # proj.bias: folded into norm1's backward
         datt = self._e(rows, D)
         T.dgrad_linear(dmid_op, W.t(blk.attn.proj.weight), rows, D, D, dt, out=datt)
         # attention core
@@ -602,7 +600,7 @@ class TrainExec:
         dx = torch.empty((rows, D), dtype=torch.float32, device=self.device)
         dx_op = dx if f32 else self._e(rows, D)
         T.layernorm_bwd(s.x, blk.norm1.weight, da1, dx, rows, D, blk.norm1.eps, G(blk.norm1.weight),
-                        G(blk.norm1.bias), dres=dmid, dxop=None if f32 else dx_op)
+                        G(blk.norm1.bias), dres=dmid, dxop=None if f32 else dx_op, dres_colsum=G(blk.attn.proj.bias))
         return dx, dx_op
 
     def _h_s_bwd(self, seq, saved, dout32, dZH):

@@ -171,12 +171,14 @@ def colsum(x, rows, C, out, ld=None, row_group=None, group_stride=0, row_offset=
 
 
 def layernorm_bwd(x, gamma, dy, dx32, rows, D, eps, dgamma, dbeta, dres=None, dxop=None, row_group=None,
-                  group_stride=0, row_offset=0, accumulate=False):
-    ws = scratch(dx32.device, 2 * D * (rows // 8 + 8), slot=2)
+                  group_stride=0, row_offset=0, accumulate=False, dres_colsum=None):
+    """LayerNorm backward; dres_colsum (optional) receives the column sums of dres over the same rows
+    (the bias gradient of the Linear whose output the residual adds), folded with dgamma / dbeta"""
+    ws = scratch(dx32.device, 3 * D * (rows // 8 + 8), slot=2)
     op = dxop.dtype if dxop is not None else torch.float32
     _lib.call("tmae_layernorm_bwd", _p(x), _p(gamma), _p(dy), _p(dres), _p(dx32), _p(dxop), dtype_code(op), rows, D,
               row_group or max(rows, 1), group_stride, row_offset, float(eps), ws.data_ptr(), ws.numel(),
-              _p(dgamma), _p(dbeta), int(accumulate), _stream())
+              _p(dgamma), _p(dbeta), _p(dres_colsum), int(accumulate), _stream())
 
 
 def unshuffle_bwd(dy, ldy, pre, ldp, out, n, H, W, C4, dtype, dy_f32):
