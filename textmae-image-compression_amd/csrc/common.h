@@ -59,6 +59,23 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return x >= 0.0f ? fmaf(h, erf_abs, h) : h * p * e;
 }
 
+// GELU for bf16 outputs: x * sigmoid(x (a + b x^2 + c x^4)), coefficients fitted to the erf GELU by
+// minimax over [-10, 10] (x clamped there inside the sigmoid, saturated beyond): |error| <= 2.6e-5 absolute, far below bf16 resolution of the stored value
+// (half an ulp is 2^-9 relative).  One v_exp + one v_rcp + five FMA-class ops against gelu_erf's
+// fifteen: the GELU of the fc1 / decoder-fc1 epilogues was 14 us of a 74 us launch.  The log2(e)
+// of exp is folded into the coefficients.  Large |x|: exp2 -> inf gives 0 (x < 0), exp2 -> 0 gives x.
+__device__ __forceinline__ float gelu_bf16out(float x) {
+  const float xc = __builtin_amdgcn_fmed3f(x, -10.0f, 10.0f);  // the quintic turns over past |x| ~ 11
+  const float x2 = xc * xc;
+  const float z = xc * fmaf(fmaf(1.0142631e-3f, x2, -0.10677572f), x2, -2.3011213f);  // -log2e (a + b x2 + c x4)
+  return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z));
+}
+// the GELU an epilogue storing OT applies
+template <typename OT> __device__ __forceinline__ float gelu_for(float x) {
+  if constexpr (sizeof(OT) == 2) return gelu_bf16out(x);
+  else return gelu_erf(x);
+}
+
 template <typename T> __device__ __forceinline__ T to_out(float v);
 template <> __device__ __forceinline__ float to_out<float>(float v) { return v; }
 template <> __device__ __forceinline__ bf16 to_out<bf16>(float v) { return (bf16)v; }

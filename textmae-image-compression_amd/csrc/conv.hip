@@ -30,18 +30,21 @@ template <typename OT, int ACT> struct EpiPixelShuffle2 {
       const int oy = 2 * y + (j >> 1), ox = 2 * x + (j & 1);
       const size_t at = (((size_t)b * 2 * H + oy) * 2 * W + ox) * ldo + c;
       if (pre) pre[at] = to_out<OT>(o);
-      if (ACT == TMAE_ACT_GELU) o = gelu_erf(o);
+      if (ACT == TMAE_ACT_GELU) o = gelu_for<OT>(o);
       out[at] = to_out<OT>(o);
     }
+  }
+  f32x4 pb0, pb1;  // this lane's bias columns (epilogue_lds prefetch hook)
+  __device__ void prefetch(int n, int N) {
+    pb0 = pb1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (n + 8 <= N) load8f(bias + n, pb0, pb1);
   }
   // 8 columns = output channels c, c+1 of the 4 sub-pixels: four 2-channel stores
   __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
     const int hw = H * W;
     const int b = m / hw, rem = m - b * hw;
     const int y = rem / W, x = rem - y * W;
-    f32x4 b0, b1;
-    load8f(bias + n, b0, b1);
-    lo += b0; hi += b1;
+    lo += pb0; hi += pb1;
     const int c = n >> 2;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -49,7 +52,7 @@ template <typename OT, int ACT> struct EpiPixelShuffle2 {
       const int oy = 2 * y + (j >> 1), ox = 2 * x + (j & 1);
       const size_t at = (((size_t)b * 2 * H + oy) * 2 * W + ox) * ldo + c;
       if (pre) { pre[at] = to_out<OT>(o0); pre[at + 1] = to_out<OT>(o1); }
-      if (ACT == TMAE_ACT_GELU) { o0 = gelu_erf(o0); o1 = gelu_erf(o1); }
+      if (ACT == TMAE_ACT_GELU) { o0 = gelu_for<OT>(o0); o1 = gelu_for<OT>(o1); }
       OT* p = out + at;
       p[0] = to_out<OT>(o0);
       p[1] = to_out<OT>(o1);
@@ -86,18 +89,27 @@ template <typename OT> struct EpiLRP {
     store4(out + (size_t)m * ldo + n, o);
     if (out2) store4(out2 + (size_t)m * ldo2 + n, o);
   }
-  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
-    f32x4 b0, b1, o0, o1;
-    load8f(bias + n, b0, b1);
-    load8f(src + (size_t)m * lds + n, o0, o1);
-    lo += b0; hi += b1;
+  // epilogue_lds hooks: bias once per lane, the y_hat_pre rows one block ahead
+  f32x4 pb0, pb1;
+  __device__ void prefetch(int n, int N) {
+    pb0 = pb1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (n + 8 <= N) load8f(bias + n, pb0, pb1);
+  }
+  struct Pre { f32x4 o0, o1; };
+  __device__ Pre fetch(int m, int n) const {
+    Pre p;
+    load8f(src + (size_t)m * lds + n, p.o0, p.o1);
+    return p;
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi, const Pre& p) const {
+    f32x4 o0 = p.o0, o1 = p.o1;
+    lo += pb0; hi += pb1;
     if (pre) store8(pre + (size_t)m * ldp + n, lo, hi);
 #pragma unroll
     for (int j = 0; j < 4; ++j) { o0[j] += 0.5f * tanhf(lo[j]); o1[j] += 0.5f * tanhf(hi[j]); }
     store8(out + (size_t)m * ldo + n, o0, o1);
     if (out2) store8(out2 + (size_t)m * ldo2 + n, o0, o1);
-  }
-};
+  }};
 
 // bf16 stride-1 12x12 convs go to the halo-staged kernel (conv_halo.h); everything else (f32 parity
 // path, strided / 6x6 / 3x3 maps, wide N) to the implicit GEMM

@@ -33,18 +33,21 @@ struct EpiResidual {
     if (bias) v += load4f(bias + n);
     store4(p, load4f(p) + v);
   }
-  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
-    float* p = out + (size_t)m * ldo + n;
-    f32x4 r0, r1;
-    load8f(p, r0, r1);
-    if (bias) {
-      f32x4 b0, b1;
-      load8f(bias + n, b0, b1);
-      lo += b0; hi += b1;
-    }
-    store8(p, r0 + lo, r1 + hi);
+  // epilogue_lds hooks (gemm_core.h): bias once per lane, the residual rows one block ahead
+  f32x4 pb0, pb1;
+  __device__ void prefetch(int n, int N) {
+    pb0 = pb1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (bias && n + 8 <= N) load8f(bias + n, pb0, pb1);
   }
-};
+  struct Pre { f32x4 r0, r1; };
+  __device__ Pre fetch(int m, int n) const {
+    Pre p;
+    load8f(out + (size_t)m * ldo + n, p.r0, p.r1);
+    return p;
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi, const Pre& p) const {
+    store8(out + (size_t)m * ldo + n, p.r0 + (lo + pb0), p.r1 + (hi + pb1));
+  }};
 
 // patch embed: token row b*(keep+1) + 1 + k  <-  acc + bias + pos[1 + p]   (MCM.py:615-626)
 struct EpiPatchEmbed {
@@ -61,13 +64,17 @@ struct EpiPatchEmbed {
     v += load4f(pos + (size_t)(1 + p) * D + n);
     store4(tok + ((size_t)b * (keep + 1) + 1 + k) * D + n, v);
   }
+  f32x4 pb0, pb1;  // this lane's bias columns (epilogue_lds prefetch hook)
+  __device__ void prefetch(int n, int N) {
+    pb0 = pb1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (n + 8 <= N) load8f(bias + n, pb0, pb1);
+  }
   __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
     const int b = m / keep, k = m - b * keep;
     const int p = (int)ids[(size_t)b * L + k];
-    f32x4 b0, b1, p0, p1;
-    load8f(bias + n, b0, b1);
+    f32x4 p0, p1;
     load8f(pos + (size_t)(1 + p) * D + n, p0, p1);
-    store8(tok + ((size_t)b * (keep + 1) + 1 + k) * D + n, lo + b0 + p0, hi + b1 + p1);
+    store8(tok + ((size_t)b * (keep + 1) + 1 + k) * D + n, lo + pb0 + p0, hi + pb1 + p1);
   }
 };
 
@@ -87,13 +94,17 @@ struct EpiDecoderEmbed {
     v += load4f(pos + (size_t)row * D + n);
     store4(out + ((size_t)b * (L + 1) + row) * D + n, v);
   }
+  f32x4 pb0, pb1;  // this lane's bias columns (epilogue_lds prefetch hook)
+  __device__ void prefetch(int n, int N) {
+    pb0 = pb1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (n + 8 <= N) load8f(bias + n, pb0, pb1);
+  }
   __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
     const int b = m / ntok, k = m - b * ntok;
     const int row = (k == 0) ? 0 : 1 + (int)ids[(size_t)b * L + (k - 1)];
-    f32x4 b0, b1, p0, p1;
-    load8f(bias + n, b0, b1);
+    f32x4 p0, p1;
     load8f(pos + (size_t)row * D + n, p0, p1);
-    store8(out + ((size_t)b * (L + 1) + row) * D + n, lo + b0 + p0, hi + b1 + p1);
+    store8(out + ((size_t)b * (L + 1) + row) * D + n, lo + pb0 + p0, hi + pb1 + p1);
   }
 };
 
@@ -128,17 +139,20 @@ struct EpiResidualOut {
     if (bias) v += load4f(bias + n);
     store4(out + (size_t)m * ld + n, load4f(resid + (size_t)m * ld + n) + v);
   }
-  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
-    f32x4 r0, r1;
-    load8f(resid + (size_t)m * ld + n, r0, r1);
-    if (bias) {
-      f32x4 b0, b1;
-      load8f(bias + n, b0, b1);
-      lo += b0; hi += b1;
-    }
-    store8(out + (size_t)m * ld + n, r0 + lo, r1 + hi);
+  f32x4 pb0, pb1;
+  __device__ void prefetch(int n, int N) {
+    pb0 = pb1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (bias && n + 8 <= N) load8f(bias + n, pb0, pb1);
   }
-};
+  struct Pre { f32x4 r0, r1; };
+  __device__ Pre fetch(int m, int n) const {
+    Pre p;
+    load8f(resid + (size_t)m * ld + n, p.r0, p.r1);
+    return p;
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi, const Pre& p) const {
+    store8(out + (size_t)m * ld + n, p.r0 + (lo + pb0), p.r1 + (hi + pb1));
+  }};
 
 template <typename T> static int check_k(int K) { return (K % Elt<T>::EPC) == 0; }
 

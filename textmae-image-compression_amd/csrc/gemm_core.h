@@ -222,9 +222,25 @@ __device__ __forceinline__ void mfma_tile(const uint4* base, int wn, int wm, int
 // segment of WN columns (full 128-256 B lines for bf16 out).
 //
 // Functors provide operator()(m, n, f32x4) for 4 columns and optionally wide(m, n, lo, hi) for 8.
+//
+// The epilogue's own global loads must not wait behind its stores: gfx9 counts loads and stores in
+// one in-order vmcnt, so a load issued after a store and then waited for (s_waitcnt vmcnt(0)) waits
+// for that store's completion too.  Loaded inline per 8-column emit, every bias / residual load exposed
+// a full store round trip (the 256 x 256 fc1 epilogue ran at 2 TB/s).  Two optional hooks let the
+// epilogue issue them ahead of the stores instead:
+//   prefetch(n, N)     per-lane column data (bias of this lane's 8 columns; the column of a lane is
+//                      fixed for the whole epilogue), loaded once into the functor's local copy;
+//   fetch(m, n) -> Pre per-(row, 8 columns) operands (residual, addend), issued one 16-row block ahead
+//                      and consumed by wide(m, n, lo, hi, pre).
 template <class E, class = void> struct HasWide : std::false_type {};
 template <class E>
 struct HasWide<E, std::void_t<decltype(std::declval<const E&>().wide(0, 0, f32x4{}, f32x4{}))>> : std::true_type {};
+template <class E, class = void> struct HasPrefetch : std::false_type {};
+template <class E>
+struct HasPrefetch<E, std::void_t<decltype(std::declval<E&>().prefetch(0, 0))>> : std::true_type {};
+template <class E, class = void> struct HasFetch : std::false_type {};
+template <class E>
+struct HasFetch<E, std::void_t<decltype(std::declval<const E&>().fetch(0, 0))>> : std::true_type {};
 
 template <class EPI>
 __device__ __forceinline__ void epi_emit8(const EPI& epi, int m, int n, f32x4 lo, f32x4 hi, int N) {
@@ -236,6 +252,40 @@ __device__ __forceinline__ void epi_emit8(const EPI& epi, int m, int n, f32x4 lo
   }
   if (n < N) epi(m, n, lo);
   if (n + 4 < N) epi(m, n + 4, hi);
+}
+
+// the functor copy one lane's epilogue runs on (column data prefetched)
+template <class EPI> __device__ __forceinline__ EPI epi_for_lane(const EPI& epi, int n, int N) {
+  EPI e = epi;
+  if constexpr (HasPrefetch<EPI>::value) e.prefetch(n, N);
+  return e;
+}
+
+template <class EPI> struct EpiPre { struct None {}; };
+template <class EPI, bool F = HasFetch<EPI>::value> struct PreOf { using type = typename EpiPre<EPI>::None; };
+template <class EPI> struct PreOf<EPI, true> { using type = decltype(std::declval<const EPI&>().fetch(0, 0)); };
+
+template <class EPI>
+__device__ __forceinline__ void epi_fetch(const EPI& e, int m, int n, int M, int N, typename PreOf<EPI>::type& p) {
+  if constexpr (HasFetch<EPI>::value) {
+    if (m < M && n + 8 <= N) p = e.fetch(m, n);
+  }
+}
+
+// emit with a fetched operand set (wide path) or the plain 4-column path at the N tail
+template <class EPI>
+__device__ __forceinline__ void epi_emit8_pre(const EPI& e, int m, int n, f32x4 lo, f32x4 hi, int N,
+                                              const typename PreOf<EPI>::type& p) {
+  if constexpr (HasFetch<EPI>::value) {
+    if (n + 8 <= N) {
+      e.wide(m, n, lo, hi, p);
+      return;
+    }
+    if (n < N) e(m, n, lo);
+    if (n + 4 < N) e(m, n + 4, hi);
+  } else {
+    epi_emit8(e, m, n, lo, hi, N);
+  }
 }
 
 template <int WN> struct EpiRegion {
@@ -251,20 +301,31 @@ __device__ __forceinline__ void epilogue_lds(const EPI& epi, const f32x4 (&acc)[
   constexpr int ST = EpiRegion<WN>::ST;
   constexpr int LPR = WN / 8;   // lanes per row
   constexpr int RPI = 64 / LPR; // rows per read round
+  constexpr int QR = 16 / RPI;  // read rounds per 16-row block
   const int fr = lane & 15, fq = lane >> 4;
   const int rr = lane / LPR, cc = lane - rr * LPR;
+  const int ncol = n0 + 8 * cc;
+  const EPI e = epi_for_lane(epi, ncol, N);
+  using Pre = typename PreOf<EPI>::type;
+  Pre pf[2][QR];
+#pragma unroll
+  for (int q = 0; q < QR; ++q) epi_fetch(e, m0 + q * RPI + rr, ncol, M, N, pf[0][q]);
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
 #pragma unroll
     for (int i = 0; i < TN; ++i) *reinterpret_cast<f32x4*>(region + fr * ST + 16 * i + 4 * fq) = acc[i][j];
+    if (j + 1 < TM) {
 #pragma unroll
-    for (int q = 0; q < 16 / RPI; ++q) {
+      for (int q = 0; q < QR; ++q) epi_fetch(e, m0 + 16 * (j + 1) + q * RPI + rr, ncol, M, N, pf[(j + 1) & 1][q]);
+    }
+#pragma unroll
+    for (int q = 0; q < QR; ++q) {
       const int row = q * RPI + rr;
       const float* src = region + row * ST + 8 * cc;
       const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
       const int m = m0 + 16 * j + row;
-      if (m < M) epi_emit8(epi, m, n0 + 8 * cc, lo, hi, N);
+      if (m < M) epi_emit8_pre(e, m, ncol, lo, hi, N, pf[j & 1][q]);
     }
   }
 }
@@ -881,31 +942,34 @@ template <typename OT, int ACT> struct EpiStore {
     if (pre) store4(pre + (size_t)m * ldp + n, v);
     if (ACT == TMAE_ACT_GELU) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = gelu_erf(v[j]);
+      for (int j = 0; j < 4; ++j) v[j] = gelu_for<OT>(v[j]);
     }
     store4(out + (size_t)m * ldo + n, v);
     if (out32) store4(out32 + (size_t)m * ld32 + n, v);
   }
-  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
-    if (bias) {
-      f32x4 b0, b1;
-      load8f(bias + n, b0, b1);
-      lo += b0; hi += b1;
-    }
-    if (addend) {
-      f32x4 a0, a1;
-      load8f(addend + (size_t)m * ld_add + n, a0, a1);
-      lo += a0; hi += a1;
-    }
+  // epilogue_lds hooks: this lane's bias columns once, the addend one row block ahead
+  f32x4 pb0, pb1;
+  __device__ void prefetch(int n, int N) {
+    pb0 = pb1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (bias && n + 8 <= N) load8f(bias + n, pb0, pb1);
+  }
+  struct Pre { f32x4 a0, a1; };
+  __device__ Pre fetch(int m, int n) const {
+    Pre p;
+    if (addend) load8f(addend + (size_t)m * ld_add + n, p.a0, p.a1);
+    return p;
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi, const Pre& p) const {
+    lo += pb0; hi += pb1;
+    if (addend) { lo += p.a0; hi += p.a1; }
     if (pre) store8(pre + (size_t)m * ldp + n, lo, hi);
     if (ACT == TMAE_ACT_GELU) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { lo[j] = gelu_erf(lo[j]); hi[j] = gelu_erf(hi[j]); }
+      for (int j = 0; j < 4; ++j) { lo[j] = gelu_for<OT>(lo[j]); hi[j] = gelu_for<OT>(hi[j]); }
     }
     store8(out + (size_t)m * ldo + n, lo, hi);
     if (out32) store8(out32 + (size_t)m * ld32 + n, lo, hi);
-  }
-};
+  }};
 
 template <typename OT, int ACT>
 static inline EpiStore<OT, ACT> make_store(OT* out, int ldo, const float* bias) {

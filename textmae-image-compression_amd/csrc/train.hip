@@ -114,22 +114,22 @@ template <typename OT, typename PT> struct EpiDgrad {
       store4(q, load4f(q) + v);
     }
   }
-  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
+  // epilogue_lds hook: the GELU inputs and the f32 accumulator rows one block ahead of the stores
+  struct Pre { f32x4 p0, p1, a0, a1; };
+  __device__ Pre fetch(int m, int n) const {
+    Pre q;
+    if (pre) load8f(pre + (size_t)m * ldp + n, q.p0, q.p1);
+    if (acc) load8f(acc + (size_t)m * lda + n, q.a0, q.a1);
+    return q;
+  }
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi, const Pre& q) const {
     if (pre) {
-      f32x4 p0, p1;
-      load8f(pre + (size_t)m * ldp + n, p0, p1);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { lo[j] *= gelu_grad(p0[j]); hi[j] *= gelu_grad(p1[j]); }
+      for (int j = 0; j < 4; ++j) { lo[j] *= gelu_grad(q.p0[j]); hi[j] *= gelu_grad(q.p1[j]); }
     }
     if (out) store8(out + (size_t)m * ldo + n, lo, hi);
-    if (acc) {
-      float* q = acc + (size_t)m * lda + n;
-      f32x4 a0, a1;
-      load8f(q, a0, a1);
-      store8(q, a0 + lo, a1 + hi);
-    }
-  }
-};
+    if (acc) store8(acc + (size_t)m * lda + n, q.a0 + lo, q.a1 + hi);
+  }};
 
 // columns [0, lim0) -> d0, [lim0, lim1) -> d1, [lim1, lim2) -> d2; each f32 +=  (conv input = channel concat)
 struct EpiRoute3 {
