@@ -825,28 +825,37 @@ struct TileChoice { int bn, bm, nw; };
 // The 8-wave 256 x 192 tile (waves 2 x 4, 128 x 48 each) exists for the tail: 9280- and 16448-row token
 // GEMMs whose 256 x 256 tile count lands just past a multiple of 256 CUs (enc qkv 333 tiles = 1.3
 // rounds, dec fc1 520 = 2.03, dec proj/fc2 130 = 0.5).
-static constexpr int kNumTiles = 7;
+static constexpr int kNumTiles = 8;
 static constexpr int kTileCand[kNumTiles][3] = {{256, 256, 8}, {128, 128, 4}, {64, 128, 4}, {32, 128, 4},
-                                                {64, 64, 4},   {32, 64, 4},   {256, 192, 8}};
+                                                {64, 64, 4},   {32, 64, 4},   {256, 192, 8}, {128, 160, 4}};
+// candidates only the bf16 LDS-DMA path instantiates
+static inline bool tile_bf16_only(int i) { return kTileCand[i][2] == 8 || i >= 7; }
 // eff = per-CU throughput relative to two 128 x 128 workgroups.  Forced-tile runs of the bench's token
 // GEMMs (tools/gemm_bench.py) put the 8-wave tiles at 0.94-1.09 of it per CU at K <= 768 (two 4-wave
 // workgroups per CU overlap one's epilogue with the other's main loop) and 1.24x at K = 3072 (fragment
 // reuse amortising prologue / epilogue): eff(K) = e * (1 + 0.12 log2(K / 768)), with e (1.10 for
 // 256x256, 1.08 for 256x192) picked by whole-forward A/B runs (bench.py: 8.57 ms vs 8.63 at 0.97 /
 // 0.96 and 8.83 at 1.45 / 1.38).  The tile count's tail (ceil of rounds) decides the rest.
+// The 4-wave 128 x 160 tile (waves 2 x 2, 64 x 80 each; 72 KiB LDS, two per CU) fits the token counts:
+// 9280 = 58 x 160 and 16448 = 102.8 x 160 rows, where 128-row tiles leave a 2-4 % tail or a few
+// workgroups past a full round (dec proj/fc2: 516 tiles for 512 slots).  Forced-tile runs: best on
+// dec qkv / fc1 / fc2 / proj and enc fc1 (dec fc2 39.7 us vs 49.4 on 256 x 192); e160 = 1.22 from the
+// constraints those runs put on the score and a whole-forward A/B (8070 img/s vs 8060 at 1.10, 7940 at
+// 1.35, 7824 without the tile).
 static inline TileChoice choose_tile(int M, int N, int K, int batch, bool allow_big) {
   const double kf = 1.0 + 0.12 * std::log2(std::max(K, 768) / 768.0);
   static const double e256 = gemm_knob("TMAE_GEMM_E256", 110) / 100.0;  // knobs: percent, for A/B runs
   static const double e192 = gemm_knob("TMAE_GEMM_E192", 108) / 100.0;
-  const double eff[kNumTiles] = {e256 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, e192 * kf};
+  static const double e160 = gemm_knob("TMAE_GEMM_E160", 122) / 100.0;
+  const double eff[kNumTiles] = {e256 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, e192 * kf, e160};
   const int forced = gemm_knob("TMAE_GEMM_TILE", -1);
-  if (forced >= 0 && forced < kNumTiles && (allow_big || kTileCand[forced][2] == 4))
+  if (forced >= 0 && forced < kNumTiles && (allow_big || !tile_bf16_only(forced)))
     return TileChoice{kTileCand[forced][0], kTileCand[forced][1], kTileCand[forced][2]};
   const bool t192 = gemm_knob("TMAE_GEMM_T192", 1) != 0;
   double best = -1.0;
   TileChoice tc{128, 128, 4};
   for (int i = 0; i < kNumTiles; ++i) {
-    if (kTileCand[i][2] == 8 && !allow_big) continue;
+    if (tile_bf16_only(i) && !allow_big) continue;
     if (i == 6 && !t192) continue;
     const int bn = kTileCand[i][0], bm = kTileCand[i][1];
     const double tn = ceil_div(N, bn), tm = ceil_div(M, bm);
@@ -903,6 +912,7 @@ static int launch_gemm(const char* name, const T* w, long long ws1, long long ws
   const TileChoice tc = choose_tile(M, N, K, n1 * n2, GLDS && sizeof(T) == 2);
   if constexpr (GLDS && sizeof(T) == 2) {
     if (tc.nw == 8 && tc.bm == 192) return launch_one<GLDS, T, 256, 192, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
+    if (tc.nw == 4 && tc.bm == 160) return launch_one<GLDS, T, 128, 160, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 8) {
       if (gemm_knob("TMAE_GEMM_RING", 0)) return launch_ring<256, 256, 2>(name, ws, xs, epi, M, N, K, n1, n2, st);
       if (gemm_knob("TMAE_GEMM_PHASED", 0)) return launch_phased(name, ws, xs, epi, M, N, K, n1, n2, st);

@@ -14,7 +14,7 @@ from textmae_amd import ops  # noqa: E402
 SHAPES = {  # name: (M, N, K, act)
     "enc_qkv": (9280, 2304, 768, 0), "enc_fc1": (9280, 3072, 768, 1), "enc_fc2": (9280, 768, 3072, 0),
     "enc_proj": (9280, 768, 768, 0), "dec_qkv": (16448, 1536, 512, 0), "dec_fc1": (16448, 2048, 512, 1),
-    "dec_fc2": (16448, 512, 2048, 0), "big": (8192, 8192, 8192, 0), "enc_fc1_noact": (9280, 3072, 768, 0),
+    "dec_fc2": (16448, 512, 2048, 0), "big": (8192, 8192, 8192, 0), "enc_fc1_noact": (9280, 3072, 768, 0), "dec_proj": (16448, 512, 512, 0),
 }
 
 
