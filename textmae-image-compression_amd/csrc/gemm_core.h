@@ -335,6 +335,10 @@ __device__ __forceinline__ void epilogue_lds(const EPI& epi, const f32x4 (&acc)[
 // LDS-DMA is in flight under the current K-step's MFMAs.  After the last K-step the ring is reused
 // as the epilogue's transpose buffer.  (A persistent walk with the next tile's first K-step in flight
 // under the epilogue measured no better on the hot shapes and was dropped.)
+// Also measured and dropped: a half-step software pipeline (second-half fragments loaded under the
+// first half's MFMAs, the next step's first half under the second's, DMA two steps ahead): 1-3 %
+// faster on isolated 8-wave GEMMs, 4 % slower on the whole forward (256 VGPRs on the 256 x 256 tile;
+// the 4-wave tiles lost 5-8 % in isolation).
 template <typename T, int BN, int BM, int WGN, int NW, class WS, class XS, class EPI>
 __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2)
 gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
