@@ -14,6 +14,8 @@ operand type: torch.float32 (exact f32 MFMA; the parity path, default) or torch.
 """
 from __future__ import annotations
 
+import os
+
 from functools import partial
 
 import numpy as np
@@ -338,6 +340,9 @@ class _Executor:
         c0 = self.mid[0]
         self.PW = 3 * S * c0  # partial sums: [mean (S*c0) | lrp (S*c0) | scale (S*c0)]
         self.Pbuf = z(Mp, self.PW)
+        # side stream for the partial sums under the serial slice steps (_slices); TMAE_LIC_OVERLAP=0 disables
+        self.overlap = os.environ.get("TMAE_LIC_OVERLAP", "1") != "0" and torch.device(dev).type == "cuda"
+        self.side_stream = torch.cuda.Stream(device=dev) if self.overlap else None
         self.SUPY = z(Mp, M, dtype=dt)    # y_hat slices (post-LRP for i < maxsup; pre-LRP for the batched ones)
         self.YPRE = z(Mp, M)              # f32 pre-LRP y_hat = round(y - mu) + mu
         self.YH = z(Mp, M, dtype=dt)      # final y_hat (g_s input)
@@ -648,10 +653,41 @@ class _Executor:
         esz = self.SUPY.element_size()
         supy, ypre, yh = self.SUPY.data_ptr(), self.YPRE.data_ptr(), self.YH.data_ptr()
         e4 = 4
-        # latent-channel partial sums of all first convs
-        ops.conv3x3(self.LM, M, M, B, g, g, self.w_pre_ml, None, pbase + off_mean * eP, Pw, 2 * S * c0, dt,
-                    y_f32=True)
-        ops.conv3x3(self.LS, M, M, B, g, g, self.w_pre_s, None, pbase + off_scale * eP, Pw, S * c0, dt, y_f32=True)
+        # latent-channel partial sums of the first convs of slices [i0, i1): mean + lrp (one 2-problem launch
+        # on LM, weight / output slabs S*c0 apart) and scale (on LS)
+        wrow = self.w_pre_ml[0].numel()
+
+        def pre(i0, i1):
+            n = (i1 - i0) * c0
+            ops.conv3x3(self.LM, M, M, B, g, g, self.w_pre_ml[i0 * c0:], None, pbase + (off_mean + i0 * c0) * eP, Pw,
+                        n, dt, y_f32=True, nb=(1, 2), strides={"w": (0, S * c0 * wrow), "y": (0, S * c0)})
+            ops.conv3x3(self.LS, M, M, B, g, g, self.w_pre_s[i0 * c0:], None, pbase + (off_scale + i0 * c0) * eP,
+                        Pw, n, dt, y_f32=True)
+
+        # The serial slice steps run 64-256-workgroup launches that leave most CUs idle: the partial sums of
+        # slices 1.. are computed on a side stream under them (fork / join by events, graph-capturable);
+        # slice i's first conv waits only for its own group.  Slice 0's group runs first on the main stream.
+        ready = {}
+        groups = [(i, i + 1) for i in range(1, ms)] + ([(ms, S)] if nb > 0 else [])
+        if self.overlap and groups:
+            main = torch.cuda.current_stream()
+            pre(0, 1)
+            fork = torch.cuda.Event()
+            fork.record(main)
+            side = self.side_stream
+            side.wait_event(fork)
+            with torch.cuda.stream(side):
+                for i0, i1 in groups:
+                    pre(i0, i1)
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    ready[i0] = ev
+        else:
+            pre(0, S)
+
+        def wait_pre(i0):
+            if i0 in ready:
+                torch.cuda.current_stream().wait_event(ready.pop(i0))
 
         cm = [t.data_ptr() for t in self.CM]
         cl = [t.data_ptr() for t in self.CL]
@@ -703,11 +739,15 @@ class _Executor:
 
         # slices 0..ms-1: serial (slice i conditions on y_hat 0..i-1)
         for i in range(ms):
+            wait_pre(i)
             ms_stack(self.ms_first[i], self.ms_layers[i], supy, sw * i, i, 1)
             gc_step(i, 1, musig, musig + ms_s1 * e4, Mp * sw)
             lrp_stack(self.lrp_first[i], self.lrp_layers[i], i, 1)
         # slices ms..S-1: batched on the fixed support y_hat 0..ms-1
         if nb > 0:
+            wait_pre(ms)
             ms_stack(self.b_ms_first, self.b_ms_layers, supy, sw * ms, ms, nb)
             gc_step(ms, nb, musig, musig + ms_s1 * e4, Mp * sw)
             lrp_stack(self.b_lrp_first, self.b_lrp_layers, ms, nb, x2=supy + ms * sw * esz)
+        for k in list(ready):  # join the side stream in every case
+            wait_pre(k)
