@@ -829,9 +829,10 @@ struct TileChoice { int bn, bm, nw; };
 // The 8-wave 256 x 192 tile (waves 2 x 4, 128 x 48 each) exists for the tail: 9280- and 16448-row token
 // GEMMs whose 256 x 256 tile count lands just past a multiple of 256 CUs (enc qkv 333 tiles = 1.3
 // rounds, dec fc1 520 = 2.03, dec proj/fc2 130 = 0.5).
-static constexpr int kNumTiles = 8;
+static constexpr int kNumTiles = 10;
 static constexpr int kTileCand[kNumTiles][3] = {{256, 256, 8}, {128, 128, 4}, {64, 128, 4}, {32, 128, 4},
-                                                {64, 64, 4},   {32, 64, 4},   {256, 192, 8}, {128, 160, 4}};
+                                                {64, 64, 4},   {32, 64, 4},   {256, 192, 8}, {128, 160, 4},
+                                                {192, 128, 4}, {128, 192, 4}};
 // candidates only the bf16 LDS-DMA path instantiates
 static inline bool tile_bf16_only(int i) { return kTileCand[i][2] == 8 || i >= 7; }
 // eff = per-CU throughput relative to two 128 x 128 workgroups.  Forced-tile runs of the bench's token
@@ -846,12 +847,17 @@ static inline bool tile_bf16_only(int i) { return kTileCand[i][2] == 8 || i >= 7
 // dec qkv / fc1 / fc2 / proj and enc fc1 (dec fc2 39.7 us vs 49.4 on 256 x 192); e160 = 1.22 from the
 // constraints those runs put on the score and a whole-forward A/B (8070 img/s vs 8060 at 1.10, 7940 at
 // 1.35, 7824 without the tile).
+// 128 x 192 (waves 2 x 2, 64 x 96 each; 80 KiB LDS, exactly two per CU): enc qkv 42.2 us vs 49.6 on
+// 256 x 192, dec fc1 54.6 vs 56.4 on 128 x 160; e = 1.25 inside the (1.10, 1.46) window those runs
+// leave (whole forward 8108 img/s vs 8041 without it).  192 x 128 was never the best tile (off).
 static inline TileChoice choose_tile(int M, int N, int K, int batch, bool allow_big) {
   const double kf = 1.0 + 0.12 * std::log2(std::max(K, 768) / 768.0);
   static const double e256 = gemm_knob("TMAE_GEMM_E256", 110) / 100.0;  // knobs: percent, for A/B runs
   static const double e192 = gemm_knob("TMAE_GEMM_E192", 108) / 100.0;
   static const double e160 = gemm_knob("TMAE_GEMM_E160", 122) / 100.0;
-  const double eff[kNumTiles] = {e256 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, e192 * kf, e160};
+  static const double e192n = gemm_knob("TMAE_GEMM_E192N", 0) / 100.0;  // 192 x 128: never best, off
+  static const double e192m = gemm_knob("TMAE_GEMM_E192M", 125) / 100.0;
+  const double eff[kNumTiles] = {e256 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, e192 * kf, e160, e192n, e192m};
   const int forced = gemm_knob("TMAE_GEMM_TILE", -1);
   if (forced >= 0 && forced < kNumTiles && (allow_big || !tile_bf16_only(forced)))
     return TileChoice{kTileCand[forced][0], kTileCand[forced][1], kTileCand[forced][2]};
@@ -917,6 +923,8 @@ static int launch_gemm(const char* name, const T* w, long long ws1, long long ws
   if constexpr (GLDS && sizeof(T) == 2) {
     if (tc.nw == 8 && tc.bm == 192) return launch_one<GLDS, T, 256, 192, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 4 && tc.bm == 160) return launch_one<GLDS, T, 128, 160, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
+    if (tc.nw == 4 && tc.bn == 192) return launch_one<GLDS, T, 192, 128, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
+    if (tc.nw == 4 && tc.bm == 192) return launch_one<GLDS, T, 128, 192, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 8) {
       if (gemm_knob("TMAE_GEMM_RING", 0)) return launch_ring<256, 256, 2>(name, ws, xs, epi, M, N, K, n1, n2, st);
       if (gemm_knob("TMAE_GEMM_PHASED", 0)) return launch_phased(name, ws, xs, epi, M, N, K, n1, n2, st);
