@@ -143,7 +143,7 @@ def train_bench(model, args, rank, world, dev, barrier):
             + ")", "value": round(ips, 2), "unit": "images/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
             "steps": args.train_steps, "warmup": args.train_warmup, "per_gpu_batch": args.train_batch,
             "global_batch": args.train_batch * world, "parallelism": f"dp{world}", "dtype": "bf16",
-            "loss_last": round(float(out["loss"]), 6), "step_mfma_frac": round(ips * TRAIN_GFLOP_PER_IMG * 1e9 /
+            "loss_last": round(float(out["loss"].detach()), 6), "step_mfma_frac": round(ips * TRAIN_GFLOP_PER_IMG * 1e9 /
                                                                              (world * PEAK_BF16), 4),
             "hip_graph": False}
 

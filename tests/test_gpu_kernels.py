@@ -257,7 +257,7 @@ def test_entropy_bottleneck(tmae, training):
     assert rel(lik, lik_ref) < 1e-5
     if not training:
         assert torch.equal(out.cpu(), zhat_ref)
-    np.testing.assert_allclose(float(eb.loss()), float(orc.eb_aux_loss(sd, "eb.")), rtol=1e-5)
+    np.testing.assert_allclose(float(eb.loss().detach()), float(orc.eb_aux_loss(sd, "eb.")), rtol=1e-5)
 
 
 @pytest.mark.parametrize("training", [False, True])
