@@ -72,7 +72,7 @@ def test_mcm_vs_reference_golden(golden_dir, tmae, name, cfgd, seed, mode):
     assert abs(got_bpp - float(f[f"{mode}_bpp_loss"])) <= 1e-3 * abs(float(f[f"{mode}_bpp_loss"]))
     np.testing.assert_allclose(float(out["loss"][0]), f[f"{mode}_ssim_loss"], rtol=1e-3)
     np.testing.assert_allclose(float(out["loss"][1]), f[f"{mode}_l1_loss"], rtol=1e-3)
-    np.testing.assert_allclose(float(m.aux_loss()), f["aux_loss"], rtol=1e-4)
+    np.testing.assert_allclose(float(m.aux_loss().detach()), f["aux_loss"], rtol=1e-4)
     from textmae_amd.rd_loss import RateDistortionLoss
 
     rd = RateDistortionLoss(lmbda=1e-4)(out, imgs)

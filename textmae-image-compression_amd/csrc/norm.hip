@@ -15,14 +15,18 @@ layernorm_kernel(const float* __restrict__ x, const float* __restrict__ gamma, c
   const int sr = (r / G) * Gs + off + (r % G);
   const float* xr = x + (size_t)sr * D;
   const int nch = D >> 2;
-  f32x4 v[VPL];
-  float s = 0.0f;
+  // gamma / beta are loaded with the row, so the wave's only dependent memory latency is the row itself
+  f32x4 v[VPL], gv[VPL], bv[VPL];
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = lane + 64 * i;
     v[i] = (c < nch) ? load4f(xr + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+    gv[i] = (c < nch) ? load4f(gamma + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    bv[i] = (c < nch) ? load4f(beta + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
   const float mean = s / (float)D;
@@ -46,10 +50,9 @@ layernorm_kernel(const float* __restrict__ x, const float* __restrict__ gamma, c
   for (int i = 0; i < VPL; ++i) {
     const int c = lane + 64 * i;
     if (c < nch) {
-      const f32x4 g = load4f(gamma + 4 * c), bb = load4f(beta + 4 * c);
       f32x4 o;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * g[j] + bb[j];
+      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * gv[i][j] + bv[i][j];
       store4(yr + 4 * c, o);
     }
   }
