@@ -90,6 +90,11 @@ int tmae_mask_rows(float* out, const float* mask_token, const float* pos, const 
  * the decoder, cls excluded) -> imgs [n][C][H][W] f32 */
 int tmae_decoder_pred_fwd(const void* x, const void* w, const float* bias, float* imgs, int n, int L, int Din,
                           int C, int H, int W, int patch, int dtype, void* stream);
+/* same computation with the weight rows and bias in channel-planar order, row (c*patch + py)*patch + px
+ * (the reference's row (py*patch + px)*C + c; the inference executor permutes them once per weight
+ * version); patch % 8 == 0. Every lane stores 8 consecutive pixels of one image row. */
+int tmae_decoder_pred_cp_fwd(const void* x, const void* w, const float* bias, float* imgs, int n, int L, int Din,
+                             int C, int H, int W, int patch, int dtype, void* stream);
 
 /* ---- learned-image-compression stack (MCM.py:729-792), NHWC f32 feature maps ------------------ */
 

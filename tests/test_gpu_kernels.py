@@ -324,6 +324,24 @@ def test_decoder_pred_unpatchify(tmae):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("n,L,P,C", [(2, 16, 16, 3), (3, 256, 16, 3), (2, 4, 8, 1)])
+def test_decoder_pred_channel_planar(tmae, dtype, n, L, P, C):
+    """the channel-planar weight order (inference executor) gives the reference-order result bit for bit"""
+    torch.manual_seed(L + P)
+    Din = 64
+    G = int(L ** 0.5)
+    x = torch.randn(n * L, Din).to(dtype).to(DEV)
+    w, b = (torch.randn(P * P * C, Din) / 8).to(dtype).to(DEV), torch.randn(P * P * C, device=DEV)
+    ref = torch.empty(n, C, G * P, G * P, device=DEV)
+    tmae.ops.decoder_pred(x, w, b, ref, n, L, P, dtype)
+    perm = tmae.ops.pred_channel_planar_perm(P, C).to(DEV)
+    out = torch.full_like(ref, float("nan"))
+    tmae.ops.decoder_pred(x, w[perm].contiguous(), b[perm].contiguous(), out, n, L, P, dtype, channel_planar=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
 def test_block_module(tmae, dtype):
     torch.manual_seed(0)
     blk = tmae.Block(128, 4, qkv_bias=True, norm_layer=lambda d: torch.nn.LayerNorm(d, eps=1e-6))

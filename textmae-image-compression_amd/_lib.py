@@ -80,6 +80,7 @@ SIGNATURES = {
     "tmae_decoder_embed_fwd": [P, I, P, P, P, P, P, I, I, I, I, I, I, P],
     "tmae_mask_rows": [P, P, P, P, I, I, I, I, P],
     "tmae_decoder_pred_fwd": [P, P, P, P, I, I, I, I, I, I, I, I, P],
+    "tmae_decoder_pred_cp_fwd": [P, P, P, P, I, I, I, I, I, I, I, I, P],
     "tmae_conv3x3": [ctypes.POINTER(ConvArgs), I, P],
     "tmae_gc_slices_fwd": [P, I, I, P, P, LL, I, P, P, I, P, I, I, P, I, I, I, I, I, P],
     "tmae_eb_likelihood_fwd": [P, ctypes.POINTER(EBParams), P, P, P, I, P, I, I, I, P],

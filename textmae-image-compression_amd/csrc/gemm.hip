@@ -128,6 +128,40 @@ struct EpiUnpatchify {
   }
 };
 
+// decoder_pred + unpatchify with channel-planar weight rows: row n = (c*P + py)*P + px (the reference's
+// (py*P + px)*C + c, permuted once on the host). Eight consecutive columns are then eight consecutive
+// pixels of one image row, so a lane's wide emit is two 16-B stores instead of eight 4-B stores spread
+// over three channel planes.
+struct EpiUnpatchifyCP {
+  float* img;
+  const float* bias;
+  int L, G, P, C, H, W;
+  __device__ void batch(int, int) {}
+  __device__ float* pix(int m, int nn) const {
+    const int b = m / L, p = m - b * L;
+    const int hy = p / G, hx = p - hy * G;
+    const int c = nn / (P * P), r = nn - c * P * P;
+    const int py = r / P, px = r - py * P;
+    return img + (((size_t)b * C + c) * H + hy * P + py) * W + hx * P + px;
+  }
+  __device__ void operator()(int m, int n, f32x4 v) const {
+    v += load4f(bias + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *pix(m, n + j) = v[j];
+  }
+  f32x4 pb0, pb1;  // this lane's bias columns (epilogue_lds prefetch hook)
+  __device__ void prefetch(int n, int N) {
+    pb0 = pb1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (n + 8 <= N) load8f(bias + n, pb0, pb1);
+  }
+  // n is a multiple of 8; with P % 8 == 0 (host-checked) the 8 columns share (c, py)
+  __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const {
+    float* o = pix(m, n);
+    store4(o, lo + pb0);
+    store4(o + 4, hi + pb1);
+  }
+};
+
 // out = resid + W·a + b, out-of-place (training keeps the block input for the LayerNorm backward)
 struct EpiResidualOut {
   const float* resid;
@@ -302,6 +336,24 @@ static int dec_pred_t(const void* x, const void* w, const float* bias, float* im
   DenseSrc<T> xs{(const T*)x, Din, n * L, Din, 1 << 30, 0, 0, BStride{0, 0}};
   return launch_gemm<true, T>("tmae_decoder_pred_fwd", (const T*)w, 0, 0, N, Din, xs,
                               EpiUnpatchify{imgs, bias, L, G, P, C, H, W}, n * L, 1, 1, st);
+}
+
+template <typename T>
+static int dec_pred_cp_t(const void* x, const void* w, const float* bias, float* imgs, int n, int L, int Din, int C,
+                         int H, int W, int P, hipStream_t st) {
+  const int G = W / P;
+  const int N = P * P * C;
+  TMAE_REQUIRE(H == W && G * G == L && check_k<T>(Din) && P % 8 == 0 && W % 4 == 0,
+               "tmae_decoder_pred_cp_fwd: bad geometry (patch must be a multiple of 8)");
+  DenseSrc<T> xs{(const T*)x, Din, n * L, Din, 1 << 30, 0, 0, BStride{0, 0}};
+  return launch_gemm<true, T>("tmae_decoder_pred_cp_fwd", (const T*)w, 0, 0, N, Din, xs,
+                              EpiUnpatchifyCP{imgs, bias, L, G, P, C, H, W}, n * L, 1, 1, st);
+}
+
+extern "C" int tmae_decoder_pred_cp_fwd(const void* x, const void* w, const float* bias, float* imgs, int n, int L,
+                                        int Din, int C, int H, int W, int patch, int dtype, void* stream) {
+  if (dtype == TMAE_BF16) return dec_pred_cp_t<bf16>(x, w, bias, imgs, n, L, Din, C, H, W, patch, (hipStream_t)stream);
+  return dec_pred_cp_t<float>(x, w, bias, imgs, n, L, Din, C, H, W, patch, (hipStream_t)stream);
 }
 
 extern "C" int tmae_decoder_pred_fwd(const void* x, const void* w, const float* bias, float* imgs, int n, int L,

@@ -434,7 +434,15 @@ class _Executor:
         self.b_lrp_layers = [(cast(torch.stack([cw(lrp[i][j].weight) for i in bs])),
                               torch.stack([lrp[i][j].bias for i in bs]).detach().contiguous()) for j in range(1, 5)]
         self.w_de = cast(m.decoder_embed.weight)
-        self.w_dp = cast(m.decoder_pred.weight)
+        # decoder_pred rows in channel-planar order: the unpatchify epilogue stores whole pixel runs
+        pp = m.encoder_embed.patch_size[0]
+        perm = ops.pred_channel_planar_perm(pp, m.encoder_embed.proj.in_channels)
+        pred_cp = pp % 8 == 0
+        self.pred_cp = pred_cp
+        self.w_dp = cast(m.decoder_pred.weight[perm.to(m.decoder_pred.weight.device)] if pred_cp
+                         else m.decoder_pred.weight)
+        self.b_dp = (m.decoder_pred.bias[perm.to(m.decoder_pred.bias.device)] if pred_cp
+                     else m.decoder_pred.bias).detach().contiguous()
 
     # ------------------------------------------------------------------ forward
     def _check_imgs(self, imgs):
@@ -577,7 +585,7 @@ class _Executor:
         ops.layernorm(self.dec, m.decoder_norm.weight, m.decoder_norm.bias, m.decoder_norm.eps, dt, rows=B * L,
                       row_group=L, group_stride=Td, row_offset=1, out=self.dn)
         x_hat = torch.empty((B, in_chans, self.img, self.img), dtype=torch.float32, device=self.device)
-        ops.decoder_pred(self.dn, self.w_dp, m.decoder_pred.bias.detach(), x_hat, B, L, P, dt)
+        ops.decoder_pred(self.dn, self.w_dp, self.b_dp, x_hat, B, L, P, dt, channel_planar=self.pred_cp)
         return x_hat
 
     # ------------------------------------------------------------------ Gaussian-conditional slice steps

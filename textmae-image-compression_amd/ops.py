@@ -144,11 +144,17 @@ def mask_rows(out, mask_token, pos, ids_shuffle, n, L, ntok, D):
               ntok, D, _stream())
 
 
-def decoder_pred(x, w, b, imgs, n, L, patch, dtype):
+def decoder_pred(x, w, b, imgs, n, L, patch, dtype, channel_planar=False):
+    """channel_planar: w / b rows already in (c, py, px) order (see pred_channel_planar_perm)"""
     N, Din = w.shape
     C, H, W = imgs.shape[1:]
-    _lib.call("tmae_decoder_pred_fwd", x.data_ptr(), w.data_ptr(), b.data_ptr(), imgs.data_ptr(), n, L, Din, C, H, W,
-              patch, dtype_code(dtype), _stream())
+    _lib.call("tmae_decoder_pred_cp_fwd" if channel_planar else "tmae_decoder_pred_fwd", x.data_ptr(), w.data_ptr(),
+              b.data_ptr(), imgs.data_ptr(), n, L, Din, C, H, W, patch, dtype_code(dtype), _stream())
+
+
+def pred_channel_planar_perm(patch, chans):
+    """row permutation taking decoder_pred rows (py, px, c) (MCM.py:524-546 "nhwpqc") to (c, py, px)"""
+    return torch.arange(patch * patch * chans).view(patch, patch, chans).permute(2, 0, 1).reshape(-1)
 
 
 # --------------------------------------------------------------------------------------- LIC
