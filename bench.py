@@ -7,14 +7,23 @@ f32 entropy models).  The forward is replayed as a HIP graph; inputs are residen
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+    python bench.py --enc-dim 1024 --enc-depth 24 --enc-heads 16 --batch 128     # BASELINE config 4
 
-Multi-GPU: images are independent, so every rank runs its own batch of 64 with no
+Multi-GPU: images are independent, so every rank runs its own batch with no
 collective on the data path ("weak" scaling); the barrier + max-over-ranks timing follows the
 driver contract.  Rank 0 prints one JSON line.
+
+Roofline (rank 0): one extra eager forward with a HIP event pair around EVERY library launch, on the
+stream it is launched on (the LIC side stream included), gives each kernel family's time and
+algorithmic FLOPs per forward (DESIGN.md §5 lists the shape -> family mapping):
+  * ``roofline`` = the family with the most kernel time (the dominant kernel), FLOPs / time;
+  * ``roofline.attention_block`` = encoder / decoder (qkv GEMM + attention core + proj GEMM);
+  * ``roofline.attention_core`` = the fused attention kernels alone (HBM/LDS-bound by AI, SURVEY (v)).
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -24,9 +33,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "images/sec encode+decode+rate, ViT-B 256×256 batch64, 1/2/4/8 MI355X"
-FWD_GFLOP_PER_IMG = 61.48        # BASELINE.md §2, config 2 (K=144)
-TRAIN_GFLOP_PER_IMG = 184.4      # fwd + bwd = 3x fwd
 PEAK_BF16 = 2.5e15               # MI355X_MICROARCH.md: dense bf16 MFMA
+PEAK_HBM = 8.0e12
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
 
@@ -39,15 +47,20 @@ def parse():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--img", type=int, default=256)
     ap.add_argument("--keep", type=int, default=144)
+    ap.add_argument("--enc-dim", type=int, default=768)
+    ap.add_argument("--enc-depth", type=int, default=12)
+    ap.add_argument("--enc-heads", type=int, default=12)
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="all-threads oracle sample length")
+    ap.add_argument("--cpu-batch", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--train-steps", type=int, default=10, help="training steps timed after the inference run")
     ap.add_argument("--train-warmup", type=int, default=3)
     ap.add_argument("--train-batch", type=int, default=64)
     ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--kernel-reps", type=int, default=0, help="unused (kept for older command lines)")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for a one-GPU rehearsal)")
     return ap.parse_args()
 
@@ -62,45 +75,179 @@ def synthetic_inputs(batch, img, L, seed, device):
     return x.to(device), s.to(device)
 
 
-def time_kernel(fn, reps):
-    """average duration of one launch, HIP events on the stream the kernel is launched on"""
-    st = torch.cuda.current_stream()
-    fn()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for _ in range(reps):
-        fn()
-    e1.record(st)
-    e1.synchronize()
-    return e0.elapsed_time(e1) / reps * 1e-3
+# ------------------------------------------------------------------------------ algorithmic work
+def gflop_per_image(m):
+    """forward FLOPs per image by component (2 * MAC), from the constructor arithmetic MCM.py:77-354;
+    counts what the reference computes (all L patches embedded, decoder_pred on L + 1 rows)"""
+    E, Dd, M, N, S = m.encoder_embed_dim, m.decoder_embed_dim, m.latent_depth, m.hyperprior_depth, m.num_slices
+    P, C = m.encoder_embed.patch_size[0], m.encoder_embed.proj.in_channels
+    L, K = m.encoder_embed.num_patches, m.num_keep_patches
+    g = int(round(K ** 0.5))
+    f = {"patch_embed": 2 * L * E * C * P * P}
+
+    def blocks(T, blks):
+        gemm = core = 0
+        for b in blks:
+            D, h = b.attn.qkv.in_features, b.mlp.fc1.out_features
+            gemm += 2 * T * D * (4 * D + 2 * h)
+            core += 4 * T * T * D
+        return gemm, core
+
+    f["enc_gemm"], f["enc_core"] = blocks(K + 1, m.encoder_blocks)
+    ga = [l for l in m.g_a if isinstance(l, torch.nn.Conv2d)]
+    f["g_a"] = f["g_s"] = sum(2 * K * l.in_channels * l.out_channels for l in ga)
+    tot, r = 0, g
+    for l in m.h_a:
+        if isinstance(l, torch.nn.Conv2d):
+            ro = (r + 2 - 3) // l.stride[0] + 1
+            tot += 2 * ro * ro * l.out_channels * l.in_channels * 9
+            r = ro
+    f["h_a"], hz = tot, r
+    tot, r = 0, hz
+    for l in m.h_s_mean:
+        c = l if isinstance(l, torch.nn.Conv2d) else (l[0] if isinstance(l, torch.nn.Sequential) else None)
+        if c is not None:
+            tot += 2 * r * r * c.out_channels * c.in_channels * 9
+            if c is not l:
+                r *= 2
+    f["h_s"] = 2 * tot
+
+    def stack(seq):
+        return sum(2 * K * c.in_channels * c.out_channels * 9 for c in seq if isinstance(c, torch.nn.Conv2d))
+
+    f["cc"] = sum(stack(a) + stack(b) for a, b in zip(m.cc_transform_mean, m.cc_transform_scale))
+    f["lrp"] = sum(stack(s) for s in m.lrp_transform)
+    f["dec_embed"] = 2 * K * E * Dd
+    f["dec_gemm"], f["dec_core"] = blocks(L + 1, m.decoder_blocks)
+    f["dec_pred"] = 2 * (L + 1) * Dd * P * P * C
+    return {k: v / 1e9 for k, v in f.items()}
 
 
-def dominant_kernel_roofline(model, batch, reps, dtype):
-    """Encoder MLP fc1 GEMM (M = 64*145, N = 3072, K = 768, GELU epilogue): the single launch
-    that carries the most FLOPs of the step (12 per forward, each 2*M*N*K)."""
-    from textmae_amd import ops
+# ------------------------------------------------------------------------------ per-launch timing
+class LaunchTimer:
+    """Wraps the library's call gate: a HIP event pair on the launching stream around every entry
+    point, tagged with (family, FLOPs).  A long spin kernel queued first lets the host enqueue the whole
+    forward before the GPU reaches it, so event intervals are kernel time, not host launch latency."""
 
-    blk = model.encoder_blocks[0]
-    T = model.num_keep_patches + 1
-    M, N, K = batch * T, blk.mlp.fc1.out_features, blk.mlp.fc1.in_features
-    x = torch.randn(M, K, device="cuda").to(dtype)
-    w = blk.mlp.fc1.weight.detach().to(dtype).contiguous()
-    b = blk.mlp.fc1.bias.detach()
-    out = torch.empty(M, N, device="cuda", dtype=dtype)
-    t = time_kernel(lambda: ops.linear(x, w, b, dtype, act=ops.ACT_GELU, out=out), reps)
-    flops = 2.0 * M * N * K
-    ach = flops / t / 1e12
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_fc1_gemm.json")
+    def __init__(self, m, batch):
+        from textmae_amd import _lib
+
+        self._lib = _lib
+        self.m, self.B = m, batch
+        self.E, self.Dd = m.encoder_embed_dim, m.decoder_embed_dim
+        self.Te, self.Td = m.num_keep_patches + 1, m.encoder_embed.num_patches + 1
+        self.recs = []
+
+    def classify(self, name, a):
+        B, E, Dd, Te, Td = self.B, self.E, self.Dd, self.Te, self.Td
+        if name == "tmae_linear_fwd" or name == "tmae_linear_residual_fwd":
+            M, N, K = (a[13], a[14], a[15]) if name == "tmae_linear_fwd" else (a[6], a[7], a[8])
+            fl = 2.0 * M * N * K
+            for side, D, T in (("enc", E, Te), ("dec", Dd, Td)):
+                if M == B * T:
+                    if name == "tmae_linear_fwd" and (N, K) == (3 * D, D):
+                        return f"{side}_qkv", fl
+                    if name == "tmae_linear_residual_fwd" and (N, K) == (D, D):
+                        return f"{side}_proj", fl
+                    if name == "tmae_linear_fwd" and K == D:
+                        return f"{side}_fc1", fl
+                    if name == "tmae_linear_residual_fwd":
+                        return f"{side}_fc2", fl
+            return "lic_1x1_gemm", fl
+        if name == "tmae_mha_fwd":
+            Bq, T, H, dh = a[2], a[3], a[4], a[5]
+            return ("enc_attn_core" if T == Te else "dec_attn_core"), 4.0 * Bq * H * T * T * dh
+        if name == "tmae_conv3x3":
+            c = a[0]._obj
+            Ho = (c.H + 2 - 3) // c.stride + 1
+            Wo = (c.W + 2 - 3) // c.stride + 1
+            return "lic_conv3x3", 2.0 * c.nb1 * c.nb2 * c.n * Ho * Wo * c.cout * 9 * (c.c1 + c.c2)
+        if name == "tmae_patch_embed_fwd":
+            return "patch_embed", 2.0 * a[6] * a[13] * a[11] * a[7] * a[10] * a[10]
+        if name == "tmae_decoder_embed_fwd":
+            return "dec_embed", 2.0 * a[7] * a[8] * a[10] * a[11]
+        if name in ("tmae_decoder_pred_fwd", "tmae_decoder_pred_cp_fwd"):
+            return "dec_pred", 2.0 * a[4] * a[5] * a[6] * a[7] * a[10] * a[10]
+        if name == "tmae_layernorm_fwd":
+            return "layernorm", 0.0
+        return "other:" + name, 0.0
+
+    def run(self, fn):
+        orig = self._lib.call
+        recs = self.recs
+
+        def timed(name, *args):
+            fam, fl = self.classify(name, args)
+            st = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            rc = orig(name, *args)
+            e1.record(st)
+            recs.append((fam, fl, e0, e1))
+            return rc
+
+        try:
+            torch._C._cuda_sleep(int(2e8))  # ~0.1 s of spin ahead of the forward
+        except Exception:
+            pass
+        self._lib.call = timed
+        try:
+            fn()
+        finally:
+            self._lib.call = orig
+        torch.cuda.synchronize()
+        fam = {}
+        for f, fl, e0, e1 in recs:
+            t = fam.setdefault(f, [0, 0.0, 0.0])
+            t[0] += 1
+            t[1] += e0.elapsed_time(e1) * 1e-3
+            t[2] += fl
+        return fam
+
+
+def roofline_report(m, imgs, scores, batch):
+    lt = LaunchTimer(m, batch)
+    with torch.no_grad():
+        fam = lt.run(lambda: m(imgs, scores))
+    mf = {k: v for k, v in fam.items() if v[2] > 0}
+    agg = {"token_gemm": [k for k in mf if k.split("_")[-1] in ("qkv", "proj", "fc1", "fc2")],
+           "lic_conv3x3": ["lic_conv3x3"]}
+
+    def stat(keys):
+        n = sum(fam[k][0] for k in keys if k in fam)
+        t = sum(fam[k][1] for k in keys if k in fam)
+        fl = sum(fam[k][2] for k in keys if k in fam)
+        ach = fl / t if t > 0 else 0.0
+        return {"launches": n, "time_us": round(t * 1e6, 1), "gflop": round(fl / 1e9, 3),
+                "achieved": round(ach / 1e12, 2), "frac": round(ach / PEAK_BF16, 4)}
+
+    per = {k: stat([k]) for k in sorted(fam)}
+    total_t = sum(v[1] for v in fam.values())
+    dom = max(fam, key=lambda k: fam[k][1] if fam[k][2] > 0 else -1)
+    d = stat([dom])
+    roof = {"kernel": dom + (" (conv_halo_kernel + conv-source GEMM tiles, every 3x3 conv of h_a / h_s / "
+                             "cc_transform / lrp_transform)" if dom == "lic_conv3x3" else ""),
+            "bound": "mfma", "achieved": d["achieved"], "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
+            "frac": d["frac"], "traffic": None, "launches_per_step": d["launches"],
+            "avg_launch_us": round(d["time_us"] / max(d["launches"], 1), 2),
+            "flops_per_launch": round(d["gflop"] * 1e9 / max(d["launches"], 1)),
+            "share_of_kernel_time": round(fam[dom][1] / total_t, 4),
+            "kernel_time_per_step_us": round(total_t * 1e6, 1)}
+    for side in ("enc", "dec"):
+        roof[f"attention_block_{side}"] = stat([f"{side}_qkv", f"{side}_attn_core", f"{side}_proj"])
+        roof[f"attention_core_{side}"] = stat([f"{side}_attn_core"])
+    roof["families"] = per
+    roof["aggregates"] = {k: stat(v) for k, v in agg.items()}
+    pmc = os.path.join(ROOT, "profiles", "r02", "pmc_dominant.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            j = json.load(open(pmc))
+            if j.get("family") == dom:
+                roof["traffic"] = j.get("hbm_bytes_per_launch")
+                roof["traffic_source"] = os.path.relpath(pmc, ROOT)
         except Exception:
-            traffic = None
-    plan = ops.gemm_plan(M, N, K, dtype)
-    return {"kernel": "%s enc fc1+GELU (M=%d,N=%d,K=%d)" % (plan, M, N, K), "bound": "mfma",
-            "achieved": round(ach, 2), "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s", "frac": round(ach * 1e12 / PEAK_BF16, 4),
-            "traffic": traffic, "avg_launch_us": round(t * 1e6, 2), "flops_per_launch": flops}
+            pass
+    return roof
 
 
 def train_bench(model, args, rank, world, dev, barrier):
@@ -133,38 +280,82 @@ def train_bench(model, args, rank, world, dev, barrier):
         out = step()
     torch.cuda.synchronize()
     barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        el = float(t.item())
+    el = max_over_ranks(time.perf_counter() - t0, world, dev, args.backend)
     ips = world * args.train_batch * args.train_steps / el
+    fl = 3 * sum(gflop_per_image(model).values())
     return {"metric": "training images/s (fwd + bwd + clip + 2x Adam" + (", RCCL grad all-reduce" if world > 1 else "")
             + ")", "value": round(ips, 2), "unit": "images/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
             "steps": args.train_steps, "warmup": args.train_warmup, "per_gpu_batch": args.train_batch,
             "global_batch": args.train_batch * world, "parallelism": f"dp{world}", "dtype": "bf16",
-            "loss_last": round(float(out["loss"].detach()), 6), "step_mfma_frac": round(ips * TRAIN_GFLOP_PER_IMG * 1e9 /
-                                                                             (world * PEAK_BF16), 4),
-            "hip_graph": False}
+            "loss_last": round(float(out["loss"].detach()), 6), "gflop_per_image": round(fl, 2),
+            "step_mfma_frac": round(ips * fl * 1e9 / (world * PEAK_BF16), 4), "hip_graph": False}
 
 
-def cpu_baseline(img, keep, seconds):
-    """The oracle (CPU restatement, fp32) on the host cores: a bounded 2-image sample of the workload."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(args, model_kwargs):
+    """the oracle (CPU restatement of MCM.forward, fp32) on the host cores over a bounded
+    sample of the same workload: batch 8 at every thread the process is given, and at 1 thread (the
+    reference eval convention, testing.py:29); plus the reference-semantics get_ids_shuffle alone
+    (the C restatement of MCM.py:364-423, batch 64)."""
+    import numpy as np
+
+    from oracle import ids as ids_oracle
     from oracle.mcm_oracle import MCMConfig, make_state_dict, mcm_forward
 
-    cfg = MCMConfig(img_size=img, num_keep_patches=keep)
+    cfg = MCMConfig(**model_kwargs)
     sd = make_state_dict(cfg, 0)
-    x, s = synthetic_inputs(2, img, (img // 16) ** 2, 0, "cpu")
-    n = 0
-    t0 = time.perf_counter()
+    L = (cfg.img_size // cfg.patch_size) ** 2
+    nb = args.cpu_batch
+    x, s = synthetic_inputs(nb, cfg.img_size, L, 0, "cpu")
+    nthreads = torch.get_num_threads()
+    n, t0 = 0, time.perf_counter()
     while True:
         mcm_forward(sd, cfg, x, s)
-        n += 2
+        n += nb
         el = time.perf_counter() - t0
-        if el >= seconds:
+        if el >= args.cpu_seconds:
             break
-    return {"value": round(n / el, 3), "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{n} images ({n // 2} oracle forwards of 2 x 256x256, K=144, fp32) in {el:.1f}s"}
+    all_ips = n / el
+    torch.set_num_threads(1)
+    try:
+        t1 = time.perf_counter()
+        mcm_forward(sd, cfg, x, s)
+        one_ips = nb / (time.perf_counter() - t1)
+    finally:
+        torch.set_num_threads(nthreads)
+    s64 = torch.rand(64, L, generator=torch.Generator().manual_seed(5)).numpy().astype(np.float32)
+    ids_oracle.ids_shuffle(s64, cfg.num_keep_patches)
+    reps, t2 = 0, time.perf_counter()
+    while time.perf_counter() - t2 < 1.0:
+        ids_oracle.ids_shuffle(s64, cfg.num_keep_patches)
+        reps += 1
+    ids_ms = (time.perf_counter() - t2) / reps * 1e3
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = None
+    return {"value": round(all_ips, 3), "unit": "images/s", "cores": nthreads, "kind": "port",
+            "sample": f"{n} images (oracle MCM.forward, fp32, batches of {nb} at {cfg.img_size}^2, "
+                      f"K={cfg.num_keep_patches}) in {el:.1f}s on {nthreads} threads; 1 thread: one batch of {nb}",
+            "value_1thread": round(one_ips, 3), "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
+            "affinity_cpus": aff, "ids_shuffle_ms_per_batch64_1thread": round(ids_ms, 3)}
+
+
+def max_over_ranks(el, world, dev, backend):
+    if world <= 1:
+        return el
+    t = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    return float(t.item())
 
 
 def main():
@@ -191,11 +382,15 @@ def main():
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
-    model = textmae_amd.MCM(img_size=args.img, num_keep_patches=args.keep).to(dev).eval()
+    kw = dict(img_size=args.img, num_keep_patches=args.keep, encoder_embed_dim=args.enc_dim,
+              encoder_depth=args.enc_depth, encoder_num_heads=args.enc_heads)
+    model = textmae_amd.MCM(**kw).to(dev).eval()
     model.compute_dtype = dtype
     model.distortion = "none"  # metric = encode + rate + decode; forward_loss is reported separately
     L = model.encoder_embed.num_patches
     imgs, scores = synthetic_inputs(args.batch, args.img, L, 1000 + rank, dev)
+    gf = gflop_per_image(model)
+    gf_img = sum(gf.values())
 
     graph = None
     with torch.no_grad():
@@ -225,36 +420,39 @@ def main():
             step()
         torch.cuda.synchronize()
         barrier()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], device=dev, dtype=torch.float64)
-            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-            el = float(t.item())
-        roof = dominant_kernel_roofline(model, args.batch, args.kernel_reps, dtype) if rank == 0 else None
+        el = max_over_ranks(time.perf_counter() - t0, world, dev, args.backend)
+    roof = None
+    if rank == 0 and not args.no_roofline:
+        roof = roofline_report(model, imgs, scores, args.batch)
+    graph = None
 
     train = None
     if not args.no_train and args.train_steps > 0:
-        graph = None
         train = train_bench(model, args, rank, world, dev, barrier)
 
+    vitb = args.enc_dim == 768 and args.enc_depth == 12
     value = world * args.batch * args.steps / el
     rec = {
         "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded uniform RGB, "
         "ImageNet-normalised; uniform patch scores; seeded random-init weights)",
-        "config": {"workload": "MCM forward eval: ids+ViT-B/16 enc (K=144 of 256 patches) + LIC hyperprior + "
-                   "EB/GC rates + ViT dec + unpatchify", "img_size": args.img, "num_keep_patches": args.keep,
-                   "per_gpu_batch": args.batch, "global_batch": args.batch * world, "parallelism": f"replicas x{world}",
+        "config": {"workload": ("MCM forward eval: ids+ViT-B/16 enc" if vitb else
+                                f"BASELINE config 4 MCM forward eval: ids+ViT enc {args.enc_dim}/{args.enc_depth}/"
+                                f"{args.enc_heads}") + f" (K={args.keep} of {L} patches) + LIC hyperprior + EB/GC "
+                                "rates + ViT dec 512/8/16 + unpatchify",
+                   "img_size": args.img, "num_keep_patches": args.keep, "per_gpu_batch": args.batch,
+                   "global_batch": args.batch * world, "parallelism": f"replicas x{world}",
                    "hip_graph": not args.no_graph},
-        "step_mfma_frac": round(value * FWD_GFLOP_PER_IMG * 1e9 / (world * PEAK_BF16), 4),
+        "gflop_per_image": round(gf_img, 3),
+        "step_mfma_frac": round(value * gf_img * 1e9 / (world * PEAK_BF16), 4),
         "roofline": roof,
     }
     if train is not None:
         rec["train"] = train
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(args.img, args.keep, args.cpu_seconds)
+            rec["cpu_baseline"] = cpu_baseline(args, kw)
         print(json.dumps(rec), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

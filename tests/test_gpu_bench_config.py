@@ -1,0 +1,205 @@
+"""Parity at the BENCHMARKED configurations (BASELINE.json configs 2 and 4).
+
+The bench times MCM(img_size=256, num_keep_patches=144) at batch 64 in bf16, replayed as a HIP graph
+with the LIC side stream; tile choice, persistent grids, halo-conv problem batching and the side-stream
+overlap all depend on the batch.  Here the same executor path runs at that batch and every image is
+checked against the oracle (oracle/mcm_oracle.py, pinned to the reference's golden outputs):
+
+* f32 operands (the parity path) at batch 64, K=144 and K=64 (§8(d) config 2'), tie-free and
+  tie-heavy scores: ids bit-exact, per-image x_hat max|a-b|/max|b| <= 1e-3, y / z likelihoods, bpp;
+* bf16 operands through the captured HIP graph exactly as bench.py replays it: the graph output equals
+  the eager forward bit for bit, and stays within the bf16 bound of the oracle (relative L2 <= 3e-2);
+* config 4 (MCM with a ViT-L/16 encoder 1024/24/16) at batch 2 in f32 against the oracle, and its
+  bench batch (128) in bf16 against the oracle on a sample of images.
+
+Rounding flips: eval quantisation rounds y - mu.  An f32 summation-order difference moves a latent
+sitting within ~1e-6 of a .5 boundary to the other side: that latent's y_hat changes by exactly 1 and
+the later slices / decoder of that ONE image follow it.  Flips are detected explicitly (y_hat
+differs by > 0.5 from the oracle's); images without a flip must meet 1e-3 on x_hat, and flips must be
+rare (<= 1e-5 of the latents, at most 2 images of 64).
+"""
+import math
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.mcm_oracle import MCMConfig, make_state_dict, mcm_forward
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+
+    return bench
+
+
+def tie_heavy_scores(B, L, seed):
+    """integer products, min-max normalised: the shape of generate_scores_file.py:26-29 (t_score * s_score
+    of int patch means) with heavy ties"""
+    rng = np.random.default_rng(seed)
+    t = rng.integers(0, 12, (B, L)) * rng.integers(0, 6, (B, L))
+    t = (t - t.min(1, keepdims=True)) / (t.max(1, keepdims=True) - t.min(1, keepdims=True))
+    return torch.from_numpy(t.astype(np.float32))
+
+
+def _model(tmae, cfgd, seed, dt):
+    cfg = MCMConfig(**cfgd)
+    m = tmae.MCM(**cfg.kwargs())
+    full = m.state_dict()
+    sd = make_state_dict(cfg, seed)
+    full.update(sd)
+    m.load_state_dict(full)
+    m.compute_dtype = dt
+    m.distortion = "none"
+    return m.to(DEV).eval(), cfg, sd
+
+
+def _maxrel(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return float((a - b).abs().max() / b.abs().max())
+
+
+def _bpp(y, z, px):
+    return sum(float(torch.log(torch.as_tensor(l).double()).sum()) for l in (y, z)) / (-math.log(2) * px)
+
+
+def _check_f32(m, cfg, sd, imgs, scores):
+    from textmae_amd import ops
+
+    B = imgs.shape[0]
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    ref = mcm_forward(sd, cfg, imgs.cpu(), scores.cpu(), keep_intermediates=True)
+    with torch.no_grad():
+        out = m(imgs.to(DEV), scores.to(DEV))
+        shuf, rest = ops.ids_shuffle(scores.to(DEV), cfg.num_keep_patches)
+    torch.cuda.synchronize()
+    assert torch.equal(shuf.cpu(), ref.ids_shuffle) and torch.equal(rest.cpu(), ref.ids_restore)
+    g = int(cfg.num_keep_patches ** 0.5)
+    yh = m._exec.YH.float().view(B, g, g, -1).permute(0, 3, 1, 2).cpu()
+    flips = ((yh - ref.inter["y_hat"]).abs() > 0.5).flatten(1).sum(1)
+    n_lat = ref.inter["y_hat"][0].numel()
+    per_img = [_maxrel(out["x_hat"][b], ref.x_hat[b]) for b in range(B)]
+    clean = [e for e, f in zip(per_img, flips.tolist()) if f == 0]
+    print(f"B={B} K={cfg.num_keep_patches}: flips per image {flips.tolist()}; worst clean x_hat err "
+          f"{max(clean):.2e}; worst overall {max(per_img):.2e}")
+    assert int((flips > 0).sum()) <= 2 and int(flips.sum()) <= max(1, int(1e-5 * B * n_lat)), flips.tolist()
+    assert max(clean) < 1e-3
+    ylik, rlik = out["likelihoods"]["y"].double().cpu(), ref.y_likelihood.double()
+    assert float(((ylik - rlik).abs() > 1e-3 * rlik.abs() + 1e-7).double().mean()) <= 1e-3
+    assert _maxrel(out["likelihoods"]["z"], ref.z_likelihood) < 1e-3
+    px = B * imgs.shape[2] * imgs.shape[3]
+    b_ref = _bpp(ref.y_likelihood, ref.z_likelihood, px)
+    assert abs(_bpp(out["likelihoods"]["y"], out["likelihoods"]["z"], px) - b_ref) <= 1e-3 * abs(b_ref)
+    return ref
+
+
+@pytest.fixture(scope="module")
+def vitb64(tmae):
+    m, cfg, sd = _model(tmae, dict(img_size=256, num_keep_patches=144), 5, torch.float32)
+    imgs, scores = _bench().synthetic_inputs(64, 256, 256, 1000, "cpu")
+    return m, cfg, sd, imgs, scores
+
+
+@pytest.mark.parametrize("scores_kind", ["tie_free", "tie_heavy"])
+def test_bench_config_f32_batch64(vitb64, scores_kind):
+    m, cfg, sd, imgs, scores = vitb64
+    if scores_kind == "tie_heavy":
+        scores = tie_heavy_scores(64, 256, 7)
+    m.compute_dtype = torch.float32
+    _check_f32(m, cfg, sd, imgs, scores)
+
+
+@pytest.mark.parametrize("scores_kind", ["tie_free", "tie_heavy"])
+def test_bench_config_k64_f32_batch64(tmae, scores_kind):
+    """§8(d) config 2': same model, mask 0.75 (K=64 of 256 patches: 8x8 latent grid, 2x2 z grid)"""
+    m, cfg, sd = _model(tmae, dict(img_size=256, num_keep_patches=64), 6, torch.float32)
+    imgs, scores = _bench().synthetic_inputs(64, 256, 256, 1000, "cpu")
+    if scores_kind == "tie_heavy":
+        scores = tie_heavy_scores(64, 256, 8)
+    _check_f32(m, cfg, sd, imgs, scores)
+
+
+def _graph_forward(m, imgs, scores):
+    """bench.py's capture: two warm-up forwards on a side stream, then one captured forward"""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.no_grad():
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                m(imgs, scores)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = m(imgs, scores)
+    return graph, out
+
+
+@pytest.mark.parametrize("scores_kind", ["tie_free", "tie_heavy"])
+def test_bench_config_bf16_graph_batch64(vitb64, scores_kind):
+    m, cfg, sd, imgs, scores = vitb64
+    if scores_kind == "tie_heavy":
+        scores = tie_heavy_scores(64, 256, 7)
+    m.compute_dtype = torch.bfloat16
+    try:
+        x, s = imgs.to(DEV), scores.to(DEV)
+        with torch.no_grad():
+            eager = m(x, s)
+            eager = {"x_hat": eager["x_hat"].clone(), "y": eager["likelihoods"]["y"].clone(),
+                     "z": eager["likelihoods"]["z"].clone()}
+        graph, out = _graph_forward(m, x, s)
+        for _ in range(3):
+            graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out["x_hat"], eager["x_hat"])
+        assert torch.equal(out["likelihoods"]["y"], eager["y"]) and torch.equal(out["likelihoods"]["z"], eager["z"])
+        ref = mcm_forward(sd, cfg, imgs, scores)
+        xh = out["x_hat"].double().cpu()
+        per = [float((xh[b] - ref.x_hat[b].double()).norm() / ref.x_hat[b].double().norm()) for b in range(64)]
+        print(f"bf16 graph vs oracle: per-image rel L2 max {max(per):.2e} mean {np.mean(per):.2e}")
+        assert max(per) < 3e-2
+        px = 64 * 256 * 256
+        b_ref = _bpp(ref.y_likelihood, ref.z_likelihood, px)
+        assert abs(_bpp(out["likelihoods"]["y"], out["likelihoods"]["z"], px) - b_ref) <= 3e-2 * abs(b_ref)
+        del graph
+    finally:
+        m.compute_dtype = torch.float32
+
+
+VITL = dict(img_size=256, encoder_embed_dim=1024, encoder_depth=24, encoder_num_heads=16, num_keep_patches=144)
+
+
+def test_config4_vitl_encoder_f32(tmae):
+    """BASELINE config 4: MCM with a ViT-L/16 encoder (MCM.py:34-52; g_a 1024 -> 896 -> 768 -> 512 -> 384,
+    MCM.py:77-93), decoder 512/8/16"""
+    m, cfg, sd = _model(tmae, VITL, 9, torch.float32)
+    assert [l.out_channels for l in m.g_a if isinstance(l, torch.nn.Conv2d)] == [896, 768, 512, 384]
+    rng = np.random.default_rng(10)
+    imgs = torch.from_numpy(((rng.random((2, 3, 256, 256), dtype=np.float32) - 0.45) / 0.225).astype(np.float32))
+    scores = torch.from_numpy(rng.random((2, 256), dtype=np.float32))
+    _check_f32(m, cfg, sd, imgs, scores)
+
+
+def test_config4_vitl_bench_batch_bf16(tmae):
+    """config 4 at its bench batch (128) in bf16 through the HIP graph: images 0, 63 and 127 of the
+    batch against the oracle (bf16 bound), and the batch is image-independent"""
+    m, cfg, sd = _model(tmae, VITL, 9, torch.bfloat16)
+    imgs, scores = _bench().synthetic_inputs(128, 256, 256, 3000, "cpu")
+    x, s = imgs.to(DEV), scores.to(DEV)
+    graph, out = _graph_forward(m, x, s)
+    graph.replay()
+    torch.cuda.synchronize()
+    pick = [0, 63, 127]
+    ref = mcm_forward(sd, cfg, imgs[pick], scores[pick])
+    xh = out["x_hat"][pick].double().cpu()
+    per = [float((xh[i] - ref.x_hat[i].double()).norm() / ref.x_hat[i].double().norm()) for i in range(3)]
+    print(f"config 4 bf16 (batch 128) vs oracle: {per}")
+    assert max(per) < 3e-2
+    assert torch.isfinite(out["likelihoods"]["y"]).all() and torch.isfinite(out["likelihoods"]["z"]).all()

@@ -1,0 +1,300 @@
+"""Optimizer and data-parallel hand-off on the MI355X (the training call site, utils/engine.py:75-91).
+
+* FusedAdam against torch.optim.Adam over several real MCM training steps (f32 and bf16 operands):
+  the executors' weight caches must follow the in-place parameter updates;
+* FusedAdam checkpoints in torch.optim.Adam's format (model_utils.py:9-55 save / resume);
+* the DP bucket hand-off: every ``ready(upto)`` the HIP backward reports must come after the last write
+  into gradients [0, upto) -- checked with a recording GradSync on one GPU, and with two ranks on
+  cuda:0 over gloo, whose averaged gradients must equal a single-process full-batch backward and be
+  bitwise identical to a run that defers every bucket to ``finish()``.
+"""
+import io
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SMALL = dict(img_size=64, patch_size=16, encoder_embed_dim=64, encoder_depth=2, encoder_num_heads=2,
+             decoder_embed_dim=64, decoder_depth=2, decoder_num_heads=2, latent_depth=192, hyperprior_depth=96,
+             num_slices=12, num_keep_patches=16)
+
+
+def _model(cfgd, seed, dt):
+    import textmae_amd
+    from oracle.mcm_oracle import MCMConfig, make_state_dict
+
+    cfg = MCMConfig(**cfgd)
+    m = textmae_amd.MCM(**cfg.kwargs())
+    full = m.state_dict()
+    full.update(make_state_dict(cfg, seed))
+    m.load_state_dict(full)
+    m = m.cuda().train()
+    m.compute_dtype = dt
+    return m, cfg
+
+
+def _inputs(cfg, B, seed):
+    rng = np.random.default_rng(seed)
+    L = (cfg.img_size // cfg.patch_size) ** 2
+    g = int(cfg.num_keep_patches ** 0.5)
+    imgs = torch.from_numpy(rng.random((B, 3, cfg.img_size, cfg.img_size), dtype=np.float32))
+    scores = torch.from_numpy(rng.random((B, L), dtype=np.float32))
+    zn = torch.from_numpy(rng.uniform(-0.5, 0.5, (B, cfg.hyperprior_depth, g // 4, g // 4)).astype(np.float32))
+    yn = torch.from_numpy(rng.uniform(-0.5, 0.5, (B, cfg.latent_depth, g, g)).astype(np.float32))
+    return imgs, scores, zn, yn
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    d = b.abs().max().item()
+    return (a - b).abs().max().item() / (d if d > 0 else 1.0)
+
+
+def _train_steps(m, opt, aux_opt, batches, crit):
+    from textmae_amd import engine
+
+    losses = []
+    for imgs, scores, zn, yn in batches:
+        out = engine.train_step(m, crit, imgs.cuda(), scores.cuda(), opt, aux_opt, clip_max_norm=1.0,
+                                noise=(zn.cuda(), yn.cuda()))
+        losses.append(float(out["loss"].detach()))
+    torch.cuda.synchronize()
+    return losses
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_fused_adam_tracks_torch_adam(dt):
+    """3 training steps: FusedAdam and torch.optim.Adam give the same losses and weights.  With stale
+    weight caches (the update kernel writes through raw pointers) the FusedAdam run would keep
+    forwarding the step-0 weights in bf16, and its losses would drift from the torch run."""
+    from textmae_amd.optim import configure_optimizers
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    crit = RateDistortionLoss(lmbda=1e-2)
+    m1, cfg = _model(SMALL, 21, dt)
+    m2, _ = _model(SMALL, 21, dt)
+    m1.distortion = m2.distortion = "ssim+l1"
+    batches = [_inputs(cfg, 2, 100 + i) for i in range(3)]
+    o1 = configure_optimizers(m1, lr=3e-3, aux_lr=1e-3, fused=True)
+    o2 = configure_optimizers(m2, lr=3e-3, aux_lr=1e-3, fused=False)
+    l1 = _train_steps(m1, *o1, batches, crit)
+    l2 = _train_steps(m2, *o2, batches, crit)
+    tol = 1e-4 if dt == torch.float32 else 2e-3
+    assert np.allclose(l1, l2, rtol=tol), (l1, l2)
+    # Adam moves every weight by at most ~lr per step: the two updates agree to a small part of that
+    p1, p2 = dict(m1.named_parameters()), dict(m2.named_parameters())
+    atol = (1e-2 if dt == torch.float32 else 1e-1) * 3e-3 * len(batches)
+    bad = [(n, float((p1[n] - p2[n]).abs().max())) for n in p1 if float((p1[n] - p2[n]).abs().max()) > atol]
+    assert not bad, bad[:10]
+    # the eval executor after FusedAdam steps == a fresh model carrying the same weights
+    import textmae_amd
+
+    m1.eval()
+    fresh = textmae_amd.MCM(**cfg.kwargs())
+    fresh.load_state_dict(m1.state_dict())
+    fresh = fresh.cuda().eval()
+    fresh.compute_dtype = dt
+    imgs, scores, _, _ = batches[0]
+    with torch.no_grad():
+        a = m1(imgs.cuda(), scores.cuda())["x_hat"]
+        b = fresh(imgs.cuda(), scores.cuda())["x_hat"]
+    assert torch.equal(a, b)
+
+
+def test_fused_adam_checkpoint_roundtrip():
+    """save_model / load_model (model_utils.py:9-55): the optimizer state goes through torch.save,
+    comes back on the CPU (map_location="cpu") and the resumed run continues bit for bit; the state is
+    torch.optim.Adam's format in both directions."""
+    from textmae_amd.optim import FusedAdam
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    crit = RateDistortionLoss(lmbda=1e-2)
+    m, cfg = _model(SMALL, 22, torch.float32)
+    m.distortion = "none"
+    batches = [_inputs(cfg, 2, 200 + i) for i in range(3)]
+    main = [p for n, p in m.named_parameters() if not n.endswith(".quantiles")]
+    aux = [m.entropy_bottleneck.quantiles]
+    opt, aux_opt = FusedAdam(main, lr=1e-3), FusedAdam(aux, lr=1e-3)
+    _train_steps(m, opt, aux_opt, batches[:2], crit)
+    buf = io.BytesIO()
+    torch.save({"model": m.state_dict(), "optimizer": opt.state_dict(), "aux_optimizer": aux_opt.state_dict()}, buf)
+    buf.seek(0)
+    ck = torch.load(buf, map_location="cpu", weights_only=True)
+    assert set(ck["optimizer"]["state"][0]) == {"step", "exp_avg", "exp_avg_sq"}
+
+    m2, _ = _model(SMALL, 0, torch.float32)
+    m2.distortion = "none"
+    m2.load_state_dict(ck["model"])
+    main2 = [p for n, p in m2.named_parameters() if not n.endswith(".quantiles")]
+    opt2, aux2 = FusedAdam(main2, lr=1e-3), FusedAdam([m2.entropy_bottleneck.quantiles], lr=1e-3)
+    opt2.load_state_dict(ck["optimizer"])
+    aux2.load_state_dict(ck["aux_optimizer"])
+    la = _train_steps(m, opt, aux_opt, batches[2:], crit)
+    lb = _train_steps(m2, opt2, aux2, batches[2:], crit)
+    assert la == lb
+    for (n, p), q in zip(m.named_parameters(), m2.parameters()):
+        assert torch.equal(p, q), n
+    # a torch.optim.Adam checkpoint resumes in FusedAdam and the other way round
+    tadam = torch.optim.Adam(main2, lr=1e-3)
+    tadam.load_state_dict(opt2.state_dict())
+    st = tadam.state_dict()
+    opt3 = FusedAdam(main2, lr=1e-3)
+    opt3.load_state_dict(st)
+    s2, s3 = opt2.state_dict()["state"], opt3.state_dict()["state"]
+    assert all(torch.equal(s2[k]["exp_avg"], s3[k]["exp_avg"]) and float(s2[k]["step"]) == float(s3[k]["step"])
+               for k in s2)
+
+
+class _Recorder:
+    """GradSync stand-in: snapshots gflat[:upto] at every hand-off"""
+
+    def __init__(self):
+        self.snaps, self.uptos = [], []
+
+    def attach(self, flat):
+        self.flat = flat
+
+    def ready(self, upto):
+        self.uptos.append(upto)
+        self.snaps.append(self.flat[:upto].clone())
+
+    def finish(self):
+        pass
+
+
+@pytest.mark.parametrize("geom", ["small", "vitb"])
+def test_backward_ready_points_are_final(geom):
+    """every gradient below a ready() offset is final when ready() is called: a bucket launched there
+    must not see a later write (mcm_train.py _ready / parallel.GradSync)"""
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    if geom == "small":
+        m, cfg = _model(SMALL, 23, torch.float32)
+    else:
+        import textmae_amd
+        from oracle.mcm_oracle import MCMConfig
+
+        torch.manual_seed(0)
+        cfg = MCMConfig(img_size=256, num_keep_patches=144)
+        m = textmae_amd.MCM(img_size=256, num_keep_patches=144).cuda().train()
+        m.compute_dtype = torch.bfloat16
+    m.distortion = "ssim+l1"
+    rec = _Recorder()
+    m.grad_sync = rec
+    imgs, scores, zn, yn = _inputs(cfg, 2, 300)
+    out = m(imgs.cuda(), scores.cuda(), noise=(zn.cuda(), yn.cuda()))
+    loss = RateDistortionLoss(lmbda=1e-2)(out, imgs.cuda())["loss"]
+    m.zero_grad(set_to_none=True)
+    loss.backward()
+    torch.cuda.synchronize()
+    final = rec.flat
+    assert rec.uptos == sorted(rec.uptos) and rec.uptos[-1] == final.numel()
+    assert len(rec.uptos) >= 2 * (m.decoder_depth + m.encoder_depth)
+    stale = [(u, int((s != final[:u]).sum())) for u, s in zip(rec.uptos, rec.snaps) if not torch.equal(s, final[:u])]
+    assert not stale, stale[:5]
+
+
+# ------------------------------------------------------------------------------ two ranks on cuda:0
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import textmae_amd  # noqa: F401
+        from textmae_amd.parallel import GradSync, enable_data_parallel
+        from textmae_amd.rd_loss import RateDistortionLoss
+
+        crit = RateDistortionLoss(lmbda=1e-2)
+        m, cfg = _model(SMALL, 24 + rank, torch.float32)  # rank 1 starts from other weights: broadcast fixes it
+        m.distortion = "ssim+l1"
+        imgs, scores, zn, yn = _inputs(cfg, 4, 400)
+        half = slice(2 * rank, 2 * rank + 2)
+
+        def grads(sync):
+            m.grad_sync = sync
+            m.zero_grad(set_to_none=True)
+            out = m(imgs[half].cuda(), scores[half].cuda(), noise=(zn[half].cuda(), yn[half].cuda()))
+            crit(out, imgs[half].cuda())["loss"].backward()
+            torch.cuda.synchronize()
+            return torch.cat([p.grad.reshape(-1).cpu() for p in m.parameters() if p.requires_grad])
+
+        sync = enable_data_parallel(m, bucket_mb=0.05)  # small buckets: many early launches
+        g_early = grads(sync)
+        nb = len(sync._bounds) - 1
+
+        class Deferred(GradSync):
+            def ready(self, upto):
+                pass
+
+        g_deferred = grads(Deferred(bucket_mb=0.05))
+        q.put((rank, g_early, g_deferred, nb))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_two_ranks_match_full_batch():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    (_, e0, d0, nb), (_, e1, d1, _) = res
+    assert nb > 10
+    assert torch.equal(e0, e1) and torch.equal(e0, d0) and torch.equal(d0, d1)
+
+    # single process, full batch of 4, rank 0's weights
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    m, cfg = _model(SMALL, 24, torch.float32)
+    m.distortion = "ssim+l1"
+    imgs, scores, zn, yn = _inputs(cfg, 4, 400)
+    out = m(imgs.cuda(), scores.cuda(), noise=(zn.cuda(), yn.cuda()))
+    RateDistortionLoss(lmbda=1e-2)(out, imgs.cuda())["loss"].backward()
+    torch.cuda.synchronize()
+    ref = torch.cat([p.grad.reshape(-1).cpu() for p in m.parameters() if p.requires_grad])
+    rel2 = float((e0.double() - ref.double()).norm() / ref.double().norm())
+    assert rel2 < 1e-5, rel2
+    assert _rel(e0, ref) < 1e-4
+
+
+def test_bench_two_ranks_gloo_prints_one_line():
+    """the driver's N>1 launch line (torch.distributed.run, one rank per GPU) rehearsed with two
+    ranks on one GPU over gloo: one JSON line, value aggregated over both ranks"""
+    import json
+
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo",
+           "--steps", "2", "--warmup", "1", "--batch", "4", "--train-steps", "1", "--train-warmup", "1",
+           "--train-batch", "2", "--kernel-reps", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["train"]["global_batch"] == 4

@@ -1,13 +1,9 @@
-"""Optimizer split — counterpart of reference models/Compression/common/model_utils.py:67-90:
-Adam over every trainable parameter except ``*.quantiles``; a second (aux) Adam over ``*.quantiles``."""
-import torch.optim as optim
+"""Optimizer split — counterpart of reference models/Compression/common/model_utils.py:67-90 with the
+reference's signature ``configure_optimizers(model, args)``: Adam over every trainable parameter except
+``*.quantiles``; a second (aux) Adam over ``*.quantiles``.  ``fused=True`` gives the HIP FusedAdam
+(optim.py) — same torch.optim.Adam arithmetic and checkpoint format."""
+from . import optim
 
 
-def configure_optimizers(model, args):
-    parameters = {n for n, p in model.named_parameters() if not n.endswith(".quantiles") and p.requires_grad}
-    aux_parameters = {n for n, p in model.named_parameters() if n.endswith(".quantiles") and p.requires_grad}
-    params = dict(model.named_parameters())
-    assert not (parameters & aux_parameters)
-    optimizer = optim.Adam((params[n] for n in sorted(parameters)), lr=args.learning_rate)
-    aux_optimizer = optim.Adam((params[n] for n in sorted(aux_parameters)), lr=args.aux_learning_rate)
-    return optimizer, aux_optimizer
+def configure_optimizers(model, args, fused=False):
+    return optim.configure_optimizers(model, lr=args.learning_rate, aux_lr=args.aux_learning_rate, fused=fused)

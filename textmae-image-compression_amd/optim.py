@@ -2,7 +2,10 @@
 models/Compression/common/model_utils.py:67-90).
 
 * ``FusedAdam`` — torch.optim.Adam semantics (amsgrad=False, L2 weight decay), every parameter of
-  a group updated by ONE HIP launch (tmae_adam_multi over a device table of tensors).
+  a group updated by ONE HIP launch (tmae_adam_multi over a device table of tensors).  The moments
+  live in one flat f32 buffer per group; ``state_dict()`` / ``load_state_dict()`` speak torch.optim.Adam's
+  per-parameter format (``step``, ``exp_avg``, ``exp_avg_sq``), so a checkpoint written by the
+  reference's ``save_model`` (model_utils.py:30-55, torch Adam) resumes here and vice versa.
 * ``clip_grad_norm_`` — torch.nn.utils.clip_grad_norm_ semantics; when every gradient lives in the
   training executor's flat buffer (the normal case after MCM's backward) it is one f64 reduction +
   one in-place scale over that buffer, with no host synchronisation.
@@ -19,6 +22,15 @@ from . import train_ops as T
 CHUNK = 1024
 
 
+def bump_versions(params):
+    """The update kernel writes parameters through raw pointers, which autograd's version counters do
+    not see; the weight caches of the executors (bf16 casts, conv relayouts) are keyed on
+    (data_ptr, _version), so every updated parameter gets its version advanced here."""
+    ps = tuple(params)
+    if ps:
+        torch._C._autograd._unsafe_set_version_counter(ps, tuple(p._version + 1 for p in ps))
+
+
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
@@ -26,22 +38,31 @@ class FusedAdam(torch.optim.Optimizer):
             for p in group["params"]:
                 if p.dtype != torch.float32 or not p.is_cuda or not p.is_contiguous():
                     raise ValueError("FusedAdam needs contiguous f32 device parameters")
-            n = sum(p.numel() for p in group["params"])
-            dev = group["params"][0].device if group["params"] else None
-            group["_m"] = torch.zeros(n, dtype=torch.float32, device=dev)
-            group["_v"] = torch.zeros(n, dtype=torch.float32, device=dev)
-            group["_step"] = 0
-            group["_tab_key"] = None
+        self._flat = [self._new_flat(g) for g in self.param_groups]  # per group: [m, v, step, offsets]
+        self._tabs = [None] * len(self.param_groups)
 
-    def _table(self, group, live):
-        key = tuple((p.data_ptr(), p.grad.data_ptr()) for p in live)
-        if group["_tab_key"] == key:
-            return group["_tab"], group["_nchunks"]
+    @staticmethod
+    def _new_flat(group):
         off, o = {}, 0
         for p in group["params"]:
             off[id(p)] = o
             o += p.numel()
-        mb, vb = group["_m"], group["_v"]
+        dev = group["params"][0].device if group["params"] else None
+        z = torch.zeros(o, dtype=torch.float32, device=dev)
+        return [z, torch.zeros_like(z), 0, off]
+
+    def add_param_group(self, param_group):
+        super().add_param_group(param_group)
+        if hasattr(self, "_flat"):
+            self._flat.append(self._new_flat(self.param_groups[-1]))
+            self._tabs.append(None)
+
+    def _table(self, gi, live):
+        key = tuple((p.data_ptr(), p.grad.data_ptr()) for p in live)
+        hit = self._tabs[gi]
+        if hit is not None and hit[0] == key:
+            return hit[1], hit[2]
+        mb, vb, _, off = self._flat[gi]
         rows, chunk = [], 0
         for p in live:
             n = p.numel()
@@ -49,7 +70,7 @@ class FusedAdam(torch.optim.Optimizer):
                          chunk])
             chunk += (n + CHUNK - 1) // CHUNK
         tab = torch.tensor(rows, dtype=torch.int64).to(mb.device)
-        group["_tab"], group["_nchunks"], group["_tab_key"] = tab, chunk, key
+        self._tabs[gi] = (key, tab, chunk)
         return tab, chunk
 
     @torch.no_grad()
@@ -58,20 +79,60 @@ class FusedAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             live = [p for p in group["params"] if p.grad is not None]
             if not live:
                 continue
             for p in live:
                 if p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
                     raise ValueError("FusedAdam needs contiguous f32 gradients")
-            group["_step"] += 1
-            tab, nchunks = self._table(group, live)
+            flat = self._flat[gi]
+            flat[2] += 1
+            tab, nchunks = self._table(gi, live)
             b1, b2 = group["betas"]
             _lib.call("tmae_adam_multi", tab.data_ptr(), len(live), nchunks, float(group["lr"]), float(b1), float(b2),
-                      float(group["eps"]), float(group["weight_decay"]), group["_step"], None,
+                      float(group["eps"]), float(group["weight_decay"]), flat[2], None,
                       torch.cuda.current_stream().cuda_stream)
+            bump_versions(live)
         return loss
+
+    # ------------------------------------------------------------------ checkpoints (torch.optim.Adam format)
+    def state_dict(self):
+        self.state.clear()
+        for gi, group in enumerate(self.param_groups):
+            mb, vb, step, off = self._flat[gi]
+            if step == 0:
+                continue  # torch Adam has no state before its first step
+            for p in group["params"]:
+                o, n = off[id(p)], p.numel()
+                self.state[p] = {"step": torch.tensor(float(step)), "exp_avg": mb[o:o + n].view_as(p).clone(),
+                                 "exp_avg_sq": vb[o:o + n].view_as(p).clone()}
+        try:
+            return super().state_dict()
+        finally:
+            self.state.clear()
+
+    def load_state_dict(self, state_dict):
+        # torch moves per-parameter state to each parameter's device (the reference loads with
+        # map_location="cpu", model_utils.py:14-17); the flat moments are rebuilt from it
+        super().load_state_dict(state_dict)
+        self._flat = [self._new_flat(g) for g in self.param_groups]
+        self._tabs = [None] * len(self.param_groups)
+        for gi, group in enumerate(self.param_groups):
+            mb, vb, _, off = self._flat[gi]
+            steps = set()
+            for p in group["params"]:
+                st = self.state.get(p)
+                if not st:
+                    continue
+                o, n = off[id(p)], p.numel()
+                mb[o:o + n].copy_(st["exp_avg"].reshape(-1))
+                vb[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.add(int(float(st["step"])))
+            if len(steps) > 1:
+                raise ValueError(f"FusedAdam keeps one step count per group; the checkpoint has {sorted(steps)}")
+            self._flat[gi][2] = steps.pop() if steps else 0
+        self.state.clear()
 
 
 def _flat_owner(params):

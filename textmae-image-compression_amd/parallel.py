@@ -53,8 +53,8 @@ class GradSync:
         if dist.get_backend(self.group) == "nccl":
             op = dist.ReduceOp.AVG if self.average else dist.ReduceOp.SUM
             self._work.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
-        else:  # gloo (CPU rehearsal): SUM then scale
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        else:  # gloo (CPU rehearsal, or several ranks sharing one GPU in tests): SUM then scale
+            _host_all_reduce_sum(t, self.group)
             if self.average:
                 t.div_(W)
 
@@ -72,13 +72,34 @@ class GradSync:
         self._work = []
 
 
+def _host_all_reduce_sum(t, group):
+    """gloo all-reduce of a tensor that may live on the GPU: staged through host memory (the device
+    copy also orders the collective after every kernel that wrote `t` on the current stream)"""
+    if not t.is_cuda:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        return
+    h = t.cpu()
+    dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+    t.copy_(h)
+
+
 def broadcast_parameters(model, src: int = 0, group=None):
     """every rank starts from rank `src`'s weights (and buffers: the entropy models' CDF tables)"""
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return
+    staged = dist.get_backend(group) != "nccl"
     with torch.no_grad():
         for t in list(model.parameters()) + [b for b in model.buffers() if b.numel() > 0]:
-            dist.broadcast(t.data, src=src, group=group)
+            if staged and t.is_cuda:
+                h = t.data.cpu()
+                dist.broadcast(h, src=src, group=group)
+                t.data.copy_(h)
+            else:
+                dist.broadcast(t.data, src=src, group=group)
+    # the executors' weight caches are keyed on parameter versions, which these raw writes do not advance
+    from .optim import bump_versions
+
+    bump_versions(model.parameters())
 
 
 def enable_data_parallel(model, process_group=None, bucket_mb: float = 64.0):
