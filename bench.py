@@ -13,9 +13,10 @@ Multi-GPU: images are independent, so every rank runs its own b
 collective on the data path ("weak" scaling); the barrier + max-over-ranks timing follows the
 driver contract.  Rank 0 prints one JSON line.
 
-Roofline (rank 0): one extra eager forward with a HIP event pair around EVERY library launch, on the
-stream it is launched on (the LIC side stream included), gives each kernel family's time and
-algorithmic FLOPs per forward (DESIGN.md §5 lists the shape -> family mapping):
+Roofline (rank 0): one extra eager forward records every library launch with its kernel family and
+algorithmic FLOPs; each family's launches are then replayed back to back between a HIP event pair on
+the stream they run on, giving the family's kernel time per forward (DESIGN.md §5 lists the shape ->
+family mapping; tools/family_summary.py gives the same split from a rocprofv3 kernel trace):
   * ``roofline`` = the family with the most kernel time (the dominant kernel), FLOPs / time;
   * ``roofline.attention_block`` = encoder / decoder (qkv GEMM + attention core + proj GEMM);
   * ``roofline.attention_core`` = the fused attention kernels alone (HBM/LDS-bound by AI, SURVEY (v)).
@@ -125,18 +126,20 @@ def gflop_per_image(m):
 
 # ------------------------------------------------------------------------------ per-launch timing
 class LaunchTimer:
-    """Wraps the library's call gate: a HIP event pair on the launching stream around every entry
-    point, tagged with (family, FLOPs).  A long spin kernel queued first lets the host enqueue the whole
-    forward before the GPU reaches it, so event intervals are kernel time, not host launch latency."""
+    """Records every launch of one eager forward through the library's call gate, tagged with its
+    kernel family and algorithmic FLOPs, then replays each family's launches back to back on one
+    stream (same arguments, same workspaces, in forward order) between a HIP event pair: the family's
+    kernel time per forward without launch gaps or side-stream overlap -- the number a rocprofv3
+    kernel trace sums for those kernels (cross-checked by tools/family_summary.py)."""
 
-    def __init__(self, m, batch):
+    def __init__(self, m, batch, reps=5):
         from textmae_amd import _lib
 
         self._lib = _lib
-        self.m, self.B = m, batch
+        self.m, self.B, self.reps = m, batch, reps
         self.E, self.Dd = m.encoder_embed_dim, m.decoder_embed_dim
         self.Te, self.Td = m.num_keep_patches + 1, m.encoder_embed.num_patches + 1
-        self.recs = []
+        self.calls = []
 
     def classify(self, name, a):
         B, E, Dd, Te, Td = self.B, self.E, self.Dd, self.Te, self.Td
@@ -174,35 +177,41 @@ class LaunchTimer:
 
     def run(self, fn):
         orig = self._lib.call
-        recs = self.recs
+        calls = self.calls
 
-        def timed(name, *args):
+        def record(name, *args):
             fam, fl = self.classify(name, args)
-            st = torch.cuda.current_stream()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            rc = orig(name, *args)
-            e1.record(st)
-            recs.append((fam, fl, e0, e1))
-            return rc
+            calls.append((fam, fl, name, args))
+            return orig(name, *args)
 
-        try:
-            torch._C._cuda_sleep(int(2e8))  # ~0.1 s of spin ahead of the forward
-        except Exception:
-            pass
-        self._lib.call = timed
+        self._lib.call = record
         try:
             fn()
         finally:
             self._lib.call = orig
         torch.cuda.synchronize()
-        fam = {}
-        for f, fl, e0, e1 in recs:
-            t = fam.setdefault(f, [0, 0.0, 0.0])
-            t[0] += 1
-            t[1] += e0.elapsed_time(e1) * 1e-3
-            t[2] += fl
-        return fam
+        fams = {}
+        for fam, fl, name, args in calls:
+            t = fams.setdefault(fam, [[], 0.0])
+            t[0].append((name, args))
+            t[1] += fl
+        out = {}
+        st = torch.cuda.current_stream()
+        for fam, (launches, fl) in fams.items():
+            if fl <= 0 and fam != "layernorm":
+                continue  # entropy models / ids / copies: not replayed (state-carrying, tiny)
+            launches = [(name, args[:-1] + (st.cuda_stream,)) for name, args in launches]  # stream is the last arg
+            for name, args in launches:  # warm
+                orig(name, *args)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(self.reps):
+                for name, args in launches:
+                    orig(name, *args)
+            e1.record(st)
+            e1.synchronize()
+            out[fam] = [len(launches), e0.elapsed_time(e1) * 1e-3 / self.reps, fl]
+        return out
 
 
 def roofline_report(m, imgs, scores, batch):
@@ -222,7 +231,7 @@ def roofline_report(m, imgs, scores, batch):
                 "achieved": round(ach / 1e12, 2), "frac": round(ach / PEAK_BF16, 4)}
 
     per = {k: stat([k]) for k in sorted(fam)}
-    total_t = sum(v[1] for v in fam.values())
+    total_t = sum(v[1] for v in fam.values())  # replayed families only (entropy models / ids excluded)
     dom = max(fam, key=lambda k: fam[k][1] if fam[k][2] > 0 else -1)
     d = stat([dom])
     roof = {"kernel": dom + (" (conv_halo_kernel + conv-source GEMM tiles, every 3x3 conv of h_a / h_s / "

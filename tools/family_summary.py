@@ -1,0 +1,69 @@
+"""Per-forward kernel time by family from a rocprofv3 kernel trace (CSV), for cross-checking the
+bench's live per-launch event timing (bench.py LaunchTimer).  Forwards are counted by the
+ids-shuffle kernel (once per MCM forward).
+
+Kernel name -> family (the shape -> family mapping of bench.py, by what the trace can tell apart):
+  lic_conv3x3     conv_halo_kernel<...> and every GEMM tile with a ConvSrc operand source
+  enc_attn_core   mha_fwd_bf16_kernel<64>        dec_attn_core  mha_fwd_bf16_kernel<32>
+  layernorm       layernorm_kernel
+  token_gemm      every other gemm_glds / gemm_reg / gemm_phased launch (qkv, proj, fc1, fc2, g_a, g_s,
+                  patch embed, decoder embed / pred)
+  other           entropy models, ids, copies
+
+usage: python tools/family_summary.py <kernel_trace.csv> [--json out.json]
+"""
+import argparse
+import csv
+import json
+from collections import defaultdict
+
+
+def family(name):
+    if "conv_halo_kernel" in name or ("gemm" in name and "ConvSrc" in name):
+        return "lic_conv3x3"
+    if "mha_fwd" in name:
+        return "enc_attn_core" if "<64>" in name or "ILi64E" in name else "dec_attn_core"
+    if "layernorm_kernel" in name:
+        return "layernorm"
+    if "gemm_" in name:
+        return "token_gemm"
+    if "spin_kernel" in name:
+        return None
+    return "other"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    fam = defaultdict(lambda: [0, 0.0])
+    halo = defaultdict(lambda: [0, 0.0])
+    nfwd = 0
+    for r in csv.DictReader(open(a.trace)):
+        n = r["Kernel_Name"]
+        if "ids_shuffle" in n:
+            nfwd += 1
+        f = family(n)
+        if f is None:
+            continue
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
+        fam[f][0] += 1
+        fam[f][1] += d
+        if f == "lic_conv3x3":
+            k = "conv_halo_kernel" if "conv_halo" in n else "gemm(ConvSrc)"
+            halo[k][0] += 1
+            halo[k][1] += d
+    nfwd = max(nfwd, 1)
+    out = {"forwards": nfwd, "families": {k: {"launches_per_fwd": v[0] / nfwd, "us_per_fwd": round(v[1] / nfwd, 1),
+                                               "avg_launch_us": round(v[1] / max(v[0], 1), 2)}
+                                           for k, v in sorted(fam.items(), key=lambda kv: -kv[1][1])},
+           "lic_conv3x3_split": {k: {"launches_per_fwd": v[0] / nfwd, "us_per_fwd": round(v[1] / nfwd, 1),
+                                     "avg_launch_us": round(v[1] / max(v[0], 1), 2)} for k, v in halo.items()}}
+    print(json.dumps(out, indent=1))
+    if a.json:
+        json.dump(out, open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
