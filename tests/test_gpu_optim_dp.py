@@ -88,13 +88,14 @@ def test_fused_adam_tracks_torch_adam(dt):
     l2 = _train_steps(m2, *o2, batches, crit)
     tol = 1e-4 if dt == torch.float32 else 2e-3
     assert np.allclose(l1, l2, rtol=tol), (l1, l2)
-    # Adam moves every weight by at most ~lr per step: the two updates agree to a small part of that
-    p1, p2 = dict(m1.named_parameters()), dict(m2.named_parameters())
-    # (bf16: a last-ulp difference in an updated weight can flip its bf16 cast, and Adam's normalised step
-    # turns the resulting gradient noise on a near-zero gradient into up to ~lr per step)
-    atol = (5e-2 if dt == torch.float32 else 1.0) * 3e-3 * len(batches)
-    bad = [(n, float((p1[n] - p2[n]).abs().max())) for n in p1 if float((p1[n] - p2[n]).abs().max()) > atol]
-    assert not bad, bad[:10]
+    # Adam moves every weight by at most ~lr per step: in f32 the two updates agree to a small part of that.
+    # (Not checked in bf16: a last-ulp difference in an updated weight can flip its bf16 cast, and Adam's
+    # normalised step turns the gradient noise on a near-zero gradient into up to ~lr per step.)
+    if dt == torch.float32:
+        atol = 5e-2 * 3e-3 * len(batches)
+        p1, p2 = dict(m1.named_parameters()), dict(m2.named_parameters())
+        bad = [(n, float((p1[n] - p2[n]).abs().max())) for n in p1 if float((p1[n] - p2[n]).abs().max()) > atol]
+        assert not bad, bad[:10]
     # the eval executor after FusedAdam steps == a fresh model carrying the same weights
     import textmae_amd
 
@@ -243,8 +244,16 @@ def _dp_worker(rank, world, port, q):
         nb = len(sync._bounds) - 1
 
         class Deferred(GradSync):
+            """every bucket waits for finish()"""
+            armed = False
+
             def ready(self, upto):
-                pass
+                if self.armed:
+                    super().ready(upto)
+
+            def finish(self):
+                self.armed = True
+                super().finish()
 
         g_deferred = grads(Deferred(bucket_mb=0.05))
         q.put((rank, g_early.numpy(), g_deferred.numpy(), nb))  # plain arrays: no shared-memory fds to outlive us

@@ -10,7 +10,10 @@ Kernel name -> family (the shape -> family mapping of bench.py, by what the trac
                   patch embed, decoder embed / pred)
   other           entropy models, ids, copies
 
-usage: python tools/family_summary.py <kernel_trace.csv> [--json out.json]
+--replay: only the kernels after the last spin kernel, i.e. bench.py's family replays (1 warm-up + 5 timed
+passes of each family's launches, back to back); the per-launch averages are what the bench line reports.
+
+usage: python tools/family_summary.py <kernel_trace.csv> [--replay] [--json out.json]
 """
 import argparse
 import csv
@@ -36,11 +39,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--json")
+    ap.add_argument("--replay", action="store_true")
     a = ap.parse_args()
+    rows = list(csv.DictReader(open(a.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    if a.replay:
+        last = max((i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]), default=-1)
+        rows = rows[last + 1:]
     fam = defaultdict(lambda: [0, 0.0])
     halo = defaultdict(lambda: [0, 0.0])
     nfwd = 0
-    for r in csv.DictReader(open(a.trace)):
+    for r in rows:
         n = r["Kernel_Name"]
         if "ids_shuffle" in n:
             nfwd += 1
@@ -54,7 +63,7 @@ def main():
             k = "conv_halo_kernel" if "conv_halo" in n else "gemm(ConvSrc)"
             halo[k][0] += 1
             halo[k][1] += d
-    nfwd = max(nfwd, 1)
+    nfwd = 6 if a.replay else max(nfwd, 1)  # replay mode: 1 warm-up + 5 timed passes
     out = {"forwards": nfwd, "families": {k: {"launches_per_fwd": v[0] / nfwd, "us_per_fwd": round(v[1] / nfwd, 1),
                                                "avg_launch_us": round(v[1] / max(v[0], 1), 2)}
                                            for k, v in sorted(fam.items(), key=lambda kv: -kv[1][1])},
