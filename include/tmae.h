@@ -236,6 +236,30 @@ int tmae_rans_decode_with_indexes(void* handle, const int32_t* indexes, long lon
                                   int32_t* out);
 int tmae_rans_decoder_destroy(void* handle);
 
+/* ---------------------------------------------------------------- Kodak eval harness (testing.py, §8f row 4)
+ * HuffmanCoding (utils/huffman.py:6-171, host, no device work): the code table of a tensor of int64 values
+ * (first-occurrence order, CPython heapq tie order, pre-order codes MSB-first in the low `lens` bits of
+ * `codes`), its '0'/'1' encoding (out = NULL: only *nbits) and the prefix decode. */
+int tmae_huffman_build(const int64_t* values, long long n, int64_t* syms, int32_t* lens, uint64_t* codes, int cap,
+                       int* nsym);
+int tmae_huffman_encode(const int64_t* values, long long n, const int64_t* syms, const int32_t* lens,
+                        const uint64_t* codes, int nsym, char* out, long long cap, long long* nbits);
+int tmae_huffman_decode(const char* bits, long long nbits, const int64_t* syms, const int32_t* lens,
+                        const uint64_t* codes, int nsym, int64_t* out, long long cap, long long* nout);
+
+/* compute_metrics (testing.py:40-49) on f32 NCHW images in [0, 1]: both rounded to 0..255, then
+ * out[0] = PSNR over the batch (max 255), out[1] = pytorch_msssim.ms_ssim(data_range=255) (device). */
+long long tmae_metrics_workspace(int n, int C, int H, int W); /* floats */
+int tmae_image_metrics(const float* org, const float* rec, int n, int C, int H, int W, float* work, long long work_elems,
+                       float* out, void* stream);
+
+/* patch importance scores, the total_scores input of MCM.forward (generate_scores_file.py:19-31, utils/map.py,
+ * utils/distribution.py; cv2 semantics as restated in oracle/scores_oracle.py): n grayscale uint8 images
+ * [n][H][W] -> scores [n][(size/patch)^2] f32 (device, no host round trip). */
+long long tmae_image_scores_workspace(int n, int H, int W, int size); /* bytes */
+int tmae_image_scores(const unsigned char* gray, int n, int H, int W, int size, int patch, unsigned char* work,
+                      long long work_bytes, float* scores, void* stream);
+
 /* ================================================================ training (MCM.forward backward,
  * driven by utils/engine.py:75-91: loss.backward(), clip_grad_norm_, Adam, aux Adam)
  * Every gradient is f32; GEMM operands are in `dtype` like the forward. */

@@ -311,3 +311,34 @@ class SSIM(nn.Module):
 
     def forward(self, x, y):
         return ssim(x, y, self.data_range, self.win_size, self.win_sigma, self.K)
+
+
+def _ssim_per_channel(x, y, win, data_range, K=(0.01, 0.03)):
+    c1 = (K[0] * data_range) ** 2
+    c2 = (K[1] * data_range) ** 2
+    mu1, mu2 = _gaussian_filter(x, win), _gaussian_filter(y, win)
+    mu1_sq, mu2_sq, mu1_mu2 = mu1.pow(2), mu2.pow(2), mu1 * mu2
+    s1 = _gaussian_filter(x * x, win) - mu1_sq
+    s2 = _gaussian_filter(y * y, win) - mu2_sq
+    s12 = _gaussian_filter(x * y, win) - mu1_mu2
+    cs_map = (2 * s12 + c2) / (s1 + s2 + c2)
+    ssim_map = ((2 * mu1_mu2 + c1) / (mu1_sq + mu2_sq + c1)) * cs_map
+    return torch.flatten(ssim_map, 2).mean(-1), torch.flatten(cs_map, 2).mean(-1)
+
+
+def ms_ssim(x, y, data_range=255, win_size=11, win_sigma=1.5, weights=None, K=(0.01, 0.03)):
+    """pytorch_msssim.ms_ssim (size_average=True; testing.py:48): five scales, relu'd per-channel cs / ssim,
+    2x2 average pooling with padding H % 2, W % 2 between scales."""
+    assert min(x.shape[-2:]) > (win_size - 1) * 2 ** 4
+    w = torch.tensor(weights or [0.0448, 0.2856, 0.3001, 0.2363, 0.1333], dtype=x.dtype)
+    win = _fspecial_gauss_1d(win_size, win_sigma, x.dtype).unsqueeze(0).repeat(x.shape[1], 1, 1, 1)
+    mcs = []
+    for i in range(w.numel()):
+        s, cs = _ssim_per_channel(x, y, win, data_range, K)
+        if i < w.numel() - 1:
+            mcs.append(torch.relu(cs))
+            pad = [d % 2 for d in x.shape[2:]]
+            x = F.avg_pool2d(x, kernel_size=2, padding=pad)
+            y = F.avg_pool2d(y, kernel_size=2, padding=pad)
+    vals = torch.stack(mcs + [torch.relu(s)], dim=0)
+    return torch.prod(vals ** w.view(-1, 1, 1), dim=0).mean()

@@ -108,6 +108,12 @@ SIGNATURES = {
     "tmae_rans_decoder_create": [P, LL, ctypes.POINTER(ctypes.c_void_p)],
     "tmae_rans_decode_with_indexes": [P, P, LL, P, I, P, P, I, P],
     "tmae_rans_decoder_destroy": [P],
+    # Kodak eval harness: Huffman side info (host), metrics and the score-map producer (device)
+    "tmae_huffman_build": [P, LL, P, P, P, I, ctypes.POINTER(I)],
+    "tmae_huffman_encode": [P, LL, P, P, P, I, P, LL, ctypes.POINTER(LL)],
+    "tmae_huffman_decode": [ctypes.c_char_p, LL, P, P, P, I, P, LL, ctypes.POINTER(LL)],
+    "tmae_image_metrics": [P, P, I, I, I, I, P, LL, P, P],
+    "tmae_image_scores": [P, I, I, I, I, I, P, LL, P, P],
     # training
     "tmae_linear_fwd_pre": [P, I, I, I, I, I, P, P, P, I, I, P, I, I, I, I, I, I, P],
     "tmae_linear_residual_out": [P, I, P, P, P, P, I, I, I, I, I, P],
@@ -140,7 +146,9 @@ SIGNATURES = {
 }
 
 # entry points that return a value rather than a status
-VALUE_FUNCS = {"tmae_wgrad_workspace": ([I, I, I, I], ctypes.c_longlong)}
+VALUE_FUNCS = {"tmae_wgrad_workspace": ([I, I, I, I], ctypes.c_longlong),
+               "tmae_metrics_workspace": ([I, I, I, I], ctypes.c_longlong),
+               "tmae_image_scores_workspace": ([I, I, I, I], ctypes.c_longlong)}
 
 _lib = None
 
