@@ -30,7 +30,7 @@ extern "C" {
 
 enum { TMAE_OK = 0, TMAE_EINVAL = 1, TMAE_EHIP = 2 };
 enum { TMAE_F32 = 0, TMAE_BF16 = 1 };
-enum { TMAE_ACT_NONE = 0, TMAE_ACT_GELU = 1 };
+enum { TMAE_ACT_NONE = 0, TMAE_ACT_GELU = 1, TMAE_ACT_RELU = 2 /* tmae_conv3x3 plain stores only (VGG16) */ };
 
 const char* tmae_last_error_string(void);
 int tmae_abi_version(void);
@@ -259,6 +259,26 @@ int tmae_image_metrics(const float* org, const float* rec, int n, int C, int H, 
 long long tmae_image_scores_workspace(int n, int H, int W, int size); /* bytes */
 int tmae_image_scores(const unsigned char* gray, int n, int H, int W, int size, int patch, unsigned char* work,
                       long long work_bytes, float* scores, void* stream);
+
+/* ---------------------------------------------------------------- VGG16 feature loss (MCM.forward_loss,
+ * models/Compression/loss/vgg.py:86-115 with common/image_utils.py:4-23).  The convolutions are tmae_conv3x3
+ * (act TMAE_ACT_RELU) and tmae_conv_dgrad; these are the glue kernels, NHWC, dtype = operand type. */
+/* de_normalize + normalize_batch: x NCHW f32 [n][C<=3][H][W] -> y NHWC [n][H][W][CP] (channels >= C zero) */
+int tmae_vgg_prep(const float* x, int n, int C, int H, int W, int CP, void* y, int dtype, void* stream);
+/* its backward: g NHWC [n][H][W][CP] -> dx NCHW f32 [n][C][H][W] */
+int tmae_vgg_prep_bwd(const void* g, int n, int C, int H, int W, int CP, float* dx, int dtype, void* stream);
+/* 2x2 / stride 2 max pool (nn.MaxPool2d(2, 2)), argmax (0..3, first maximum) into arg when non-NULL */
+int tmae_maxpool2(const void* x, int n, int H, int W, int C, void* y, unsigned char* arg, int dtype, void* stream);
+/* dx [n][H][W][C] = scatter of dy to the argmax (+ add when non-NULL) */
+int tmae_maxpool2_bwd(const void* dy, const unsigned char* arg, int n, int H, int W, int C, void* dx, const void* add,
+                      int dtype, void* stream);
+/* g *= (y > 0)  (ReLU backward from the ReLU output) */
+int tmae_relu_mask(void* g, const void* y, long long n, int dtype, void* stream);
+/* out[0] (accumulate ? += : =) mean((a - b)^2) (nn.MSELoss); part >= 1024 doubles */
+int tmae_mse(const void* a, const void* b, long long n, double* part, float* out, int accumulate, int dtype,
+             void* stream);
+/* da = g[0] * 2 (a - b) / n */
+int tmae_mse_bwd(const void* a, const void* b, long long n, const float* g, void* da, int dtype, void* stream);
 
 /* ================================================================ training (MCM.forward backward,
  * driven by utils/engine.py:75-91: loss.backward(), clip_grad_norm_, Adam, aux Adam)

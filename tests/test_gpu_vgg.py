@@ -1,0 +1,106 @@
+"""VGG16 feature loss on the MI355X against the plain-PyTorch restatement
+(oracle/vgg_oracle.py) with a seeded VGG16 state_dict in torchvision's layout (the pretrained weights
+need a download: parity with them is unpinned, the arithmetic is what is checked).
+
+Tolerance: f32 operands max|a-b|/max|b| <= 1e-4 on the loss and <= 1e-3 on its gradient w.r.t. the
+prediction; bf16 operands relative error <= 3e-2 (loss) and relative L2 <= 5e-2 (gradient)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.vgg_oracle import feature_loss, make_vgg_state_dict
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(n=2, H=48, W=40, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    imgs = torch.rand(n, 3, H, W, generator=g) * 2 - 1
+    preds = (imgs + 0.2 * torch.randn(n, 3, H, W, generator=g)).clamp(-1.2, 1.2)
+    return preds, imgs
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_feature_loss_and_grad_vs_oracle(tmae, dt):
+    from textmae_amd.vgg import Vgg16Features, cal_features_loss
+
+    sd = make_vgg_state_dict(1)
+    preds, imgs = _inputs()
+    pr = preds.double().requires_grad_(True)
+    sd64 = {k: v.double() for k, v in sd.items()}
+    ref = feature_loss(pr, imgs.double(), sd64)
+    ref.backward()
+    net = Vgg16Features(sd, "cuda", dt)
+    p = preds.cuda().requires_grad_(True)
+    loss = cal_features_loss(p, imgs.cuda(), net)
+    loss.backward()
+    torch.cuda.synchronize()
+    rl = abs(float(loss) - float(ref)) / abs(float(ref))
+    g, gr = p.grad.double().cpu(), pr.grad
+    if dt == torch.float32:
+        assert rl < 1e-4, rl
+        assert float((g - gr).abs().max() / gr.abs().max()) < 1e-3
+    else:
+        assert rl < 3e-2, rl
+        assert float((g - gr).norm() / gr.norm()) < 5e-2
+
+
+def test_maxpool_ties_first_max_and_odd_error(tmae):
+    """nn.MaxPool2d(2, 2) backward routes to the FIRST maximum of a tied window (torch semantics)"""
+    from textmae_amd import _lib
+    from textmae_amd.ops import _stream
+
+    x = torch.zeros(1, 2, 2, 8, device="cuda")          # NHWC, all equal: argmax = window position 0
+    y = torch.empty(1, 1, 1, 8, device="cuda")
+    arg = torch.empty(8, dtype=torch.uint8, device="cuda")
+    _lib.call("tmae_maxpool2", x.data_ptr(), 1, 2, 2, 8, y.data_ptr(), arg.data_ptr(), 0, _stream())
+    dy = torch.ones(1, 1, 1, 8, device="cuda")
+    dx = torch.empty_like(x)
+    _lib.call("tmae_maxpool2_bwd", dy.data_ptr(), arg.data_ptr(), 1, 2, 2, 8, dx.data_ptr(), None, 0, _stream())
+    torch.cuda.synchronize()
+    assert (arg == 0).all() and float(dx[0, 0, 0].sum()) == 8 and float(dx.sum()) == 8
+    with pytest.raises(ValueError):
+        _lib.call("tmae_maxpool2", x.data_ptr(), 1, 3, 2, 8, y.data_ptr(), None, 0, _stream())
+
+
+def test_mcm_forward_loss_with_local_vgg(tmae, tmp_path):
+    """MCM.forward_loss's third term with weights from a local file (load_vgg16), and the training step's
+    RateDistortionLoss carrying lmbda * 0.1 * vgg (rd_loss.py:26-27); its gradient reaches x_hat"""
+    from oracle.mcm_oracle import MCMConfig, make_state_dict
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    cfg = MCMConfig(img_size=64, patch_size=16, encoder_embed_dim=64, encoder_depth=1, encoder_num_heads=2,
+                    decoder_embed_dim=64, decoder_depth=1, decoder_num_heads=2, latent_depth=192, hyperprior_depth=96,
+                    num_keep_patches=16)
+    m = tmae.MCM(**cfg.kwargs())
+    full = m.state_dict()
+    full.update(make_state_dict(cfg, 3))
+    m.load_state_dict(full)
+    m = m.cuda().train()
+    keys = set(m.state_dict())
+    sd = make_vgg_state_dict(2)
+    path = tmp_path / "vgg16.pth"
+    torch.save(sd, path)
+    m.load_vgg16(str(path))
+    assert set(m.state_dict()) == keys  # the feature network is not part of MCM's state
+    g = torch.Generator().manual_seed(4)
+    imgs = torch.rand(2, 3, 64, 64, generator=g)
+    scores = torch.rand(2, 16, generator=g)
+    zn = torch.rand(2, 96, 1, 1, generator=g) - 0.5
+    yn = torch.rand(2, 192, 4, 4, generator=g) - 0.5
+    out = m(imgs.cuda(), scores.cuda(), noise=(zn.cuda(), yn.cuda()))
+    vgg = out["loss"][2]
+    ref = feature_loss(out["x_hat"].detach().cpu().double(), imgs.double(), {k: v.double() for k, v in sd.items()})
+    assert abs(float(vgg) - float(ref)) <= 1e-4 * abs(float(ref))
+    rd = RateDistortionLoss(lmbda=1e-2)(out, imgs.cuda())
+    expect = 1e-2 * (0.25 * float(rd["ssim_loss"]) + 10 * float(rd["L1_loss"]) + 0.1 * float(vgg)) + float(rd["bpp_loss"])
+    assert float(rd["loss"]) == pytest.approx(expect, rel=1e-5)
+    m.zero_grad(set_to_none=True)
+    rd["loss"].backward()
+    torch.cuda.synchronize()
+    grads = [p.grad for p in m.parameters() if p.requires_grad]
+    assert all(gr is not None and torch.isfinite(gr).all() for gr in grads)
+    # without weights the term is 0 (and the training path warns once)
+    m2 = tmae.MCM(**cfg.kwargs()).cuda().eval()
+    with torch.no_grad():
+        assert float(m2(imgs.cuda(), scores.cuda())["loss"][2]) == 0.0

@@ -12,7 +12,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libtmae.so")
 
 TMAE_F32, TMAE_BF16 = 0, 1
-ACT_NONE, ACT_GELU = 0, 1
+ACT_NONE, ACT_GELU, ACT_RELU = 0, 1, 2
 
 P, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 
@@ -114,6 +114,14 @@ SIGNATURES = {
     "tmae_huffman_decode": [ctypes.c_char_p, LL, P, P, P, I, P, LL, ctypes.POINTER(LL)],
     "tmae_image_metrics": [P, P, I, I, I, I, P, LL, P, P],
     "tmae_image_scores": [P, I, I, I, I, I, P, LL, P, P],
+    # VGG16 feature loss glue
+    "tmae_vgg_prep": [P, I, I, I, I, I, P, I, P],
+    "tmae_vgg_prep_bwd": [P, I, I, I, I, I, P, I, P],
+    "tmae_maxpool2": [P, I, I, I, I, P, P, I, P],
+    "tmae_maxpool2_bwd": [P, P, I, I, I, I, P, P, I, P],
+    "tmae_relu_mask": [P, P, LL, I, P],
+    "tmae_mse": [P, P, LL, P, P, I, I, P],
+    "tmae_mse_bwd": [P, P, LL, P, P, I, P],
     # training
     "tmae_linear_fwd_pre": [P, I, I, I, I, I, P, P, P, I, I, P, I, I, I, I, I, I, P],
     "tmae_linear_residual_out": [P, I, P, P, P, P, I, I, I, I, I, P],

@@ -133,6 +133,7 @@ static int conv_t(const tmae_conv_args& a, hipStream_t st) {
                "tmae_conv3x3: channel counts (%d + %d -> %d) must be multiples of %d", a.c1, a.c2, a.cout, e);
   TMAE_REQUIRE(a.stride == 1 || a.stride == 2, "tmae_conv3x3: stride %d", a.stride);
   TMAE_REQUIRE(!(a.pixel_shuffle && a.lrp_src), "tmae_conv3x3: pixel_shuffle and lrp are exclusive");
+  TMAE_REQUIRE(a.act != TMAE_ACT_RELU || (!a.pixel_shuffle && !a.lrp_src), "tmae_conv3x3: ReLU on a plain store only");
   TMAE_REQUIRE(a.nb1 >= 1 && a.nb2 >= 1, "tmae_conv3x3: batch %d x %d", a.nb1, a.nb2);
   ConvSrc<T> xs;
   xs.x1 = (const T*)a.x1; xs.x2 = (const T*)a.x2; xs.c1 = a.c1; xs.ld1 = a.ld1; xs.ld2 = a.ld2;
@@ -166,6 +167,19 @@ static int conv_t(const tmae_conv_args& a, hipStream_t st) {
     EpiLRP<T> r{a.lrp_src, a.ld_src, (T*)a.y, a.ldy, (T*)a.y2, a.ldy2, a.bias, {a.src_s1, a.src_s2},
                 {a.y_s1, a.y_s2}, {a.y2_s1, a.y2_s2}, {a.b_s1, a.b_s2}, (float*)a.pre, a.ldp, {a.pre_s1, a.pre_s2}};
     TMAE_GO(r);
+  }
+  if (a.act == TMAE_ACT_RELU) {  // VGG16 (loss/vgg.py): plain conv + ReLU, no addend / copies
+    TMAE_REQUIRE(!a.addend && !a.y32 && !a.pre, "tmae_conv3x3: ReLU supports plain stores only");
+    if (a.y_f32) {
+      auto r = make_store<float, TMAE_ACT_RELU>((float*)a.y, a.ldy, a.bias);
+      r.so = BStride{a.y_s1, a.y_s2};
+      r.sb = BStride{a.b_s1, a.b_s2};
+      return launch_gemm<true, T>(nm, W, a.w_s1, a.w_s2, N, K, xs, r, M, a.nb1, a.nb2, st);
+    }
+    auto r = make_store<T, TMAE_ACT_RELU>((T*)a.y, a.ldy, a.bias);
+    r.so = BStride{a.y_s1, a.y_s2};
+    r.sb = BStride{a.b_s1, a.b_s2};
+    return launch_gemm<true, T>(nm, W, a.w_s1, a.w_s2, N, K, xs, r, M, a.nb1, a.nb2, st);
   }
   if (a.y_f32) {
     auto g = make_store<float, 1>((float*)a.y, a.ldy, a.bias);

@@ -966,6 +966,10 @@ template <typename OT, int ACT> struct EpiStore {
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = gelu_for<OT>(v[j]);
     }
+    if (ACT == TMAE_ACT_RELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.0f);
+    }
     store4(out + (size_t)m * ldo + n, v);
     if (out32) store4(out32 + (size_t)m * ld32 + n, v);
   }
@@ -988,6 +992,10 @@ template <typename OT, int ACT> struct EpiStore {
     if (ACT == TMAE_ACT_GELU) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) { lo[j] = gelu_for<OT>(lo[j]); hi[j] = gelu_for<OT>(hi[j]); }
+    }
+    if (ACT == TMAE_ACT_RELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { lo[j] = fmaxf(lo[j], 0.0f); hi[j] = fmaxf(hi[j], 0.0f); }
     }
     store8(out + (size_t)m * ldo + n, lo, hi);
     if (out32) store8(out32 + (size_t)m * ld32 + n, lo, hi);

@@ -223,12 +223,47 @@ class MCM(CompressionModel):
         return {"loss": loss, "likelihoods": {"y": ylik, "z": zlik}, "x_hat": x_hat}
 
     def forward_loss(self, imgs, x_hat):
-        """MCM.forward_loss (MCM.py:690-712): (1 - SSIM, L1, VGG feature loss).  The VGG term needs
-        torchvision's pretrained VGG16 (a network download in the reference, vgg.py:14) and is 0 here."""
+        """MCM.forward_loss (MCM.py:690-712): (1 - SSIM, L1, VGG16 feature loss).  The reference downloads
+        torchvision's pretrained VGG16 on every call (vgg.py:14, 99); here the feature loss runs once local
+        weights are given (load_vgg16, or the TMAE_VGG16_WEIGHTS file) and is 0 (with a one-time warning in
+        training) without them."""
+        from . import vgg
         from .distortion import ssim_l1_loss
 
         s, l1 = ssim_l1_loss(x_hat, imgs)
-        return s, l1, torch.zeros((), device=imgs.device)
+        net = self._vgg_net(imgs.device)
+        if net is None:
+            if self.training:
+                vgg.warn_missing_once()
+            return s, l1, torch.zeros((), device=imgs.device)
+        return s, l1, vgg.cal_features_loss(x_hat, imgs, net)
+
+    def load_vgg16(self, weights):
+        """local VGG16 weights for the feature loss: a torchvision vgg16 state_dict (or the reference Vgg16
+        module's) or a path to one (loaded with weights_only=True).  Not part of MCM's state_dict, as in the
+        reference, where the network is frozen and rebuilt inside the loss."""
+        from .vgg import load_vgg16_state_dict
+
+        sd = load_vgg16_state_dict(weights) if isinstance(weights, (str, os.PathLike)) else weights
+        self.__dict__["_vgg_sd"] = {k: v.detach().cpu() for k, v in sd.items() if torch.is_tensor(v)}
+        self.__dict__["_vgg"] = None
+
+    def _vgg_net(self, device):
+        from .vgg import Vgg16Features
+
+        if self.__dict__.get("_vgg_sd") is None:
+            path = os.environ.get("TMAE_VGG16_WEIGHTS")
+            if not path:
+                return None
+            self.load_vgg16(path)
+        dt = self.compute_dtype
+        if torch.is_autocast_enabled() and dt == torch.float32:
+            dt = torch.bfloat16
+        net = self.__dict__.get("_vgg")
+        if net is None or net.device != torch.device(device) or net.dtype != dt:
+            net = Vgg16Features(self.__dict__["_vgg_sd"], device, dt)
+            self.__dict__["_vgg"] = net
+        return net
 
     def aux_loss(self):
         return self.entropy_bottleneck.loss()
