@@ -195,53 +195,16 @@ template <> struct AttnTr<32> { static constexpr int LDV = 32; };
 typedef __attribute__((ext_vector_type(4))) short attn_s4;
 typedef __attribute__((address_space(3))) attn_s4 attn_lds_s4;
 
+// one (image, head) item of the bf16 forward: this wave's 32 queries against the K / V tiles staged in
+// LDS (Ks row-major [Tpad][DH + 8], Vs row-major [Tpad][LDV]); writes O (and the base-2 LSE when lse)
 template <int DH>
-__global__ void __launch_bounds__(1024)
-mha_fwd_bf16_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int Tn, int H,
-                    int Tpad, float scale_log2e) {
-  constexpr int KPAD = 8, NDT = DH / 32, CPR = DH / 8, LDV = AttnTr<DH>::LDV;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__device__ __forceinline__ void mha_bf16_item(const bf16* Ks, const bf16* Vs, const bf16x8 (&qf)[DH / 16], int Tn,
+                                              int Tpad, float scale_log2e, int lane, int q0, float* lse, bf16* obase,
+                                              int D) {
+  constexpr int KPAD = 8, NDT = DH / 32, LDV = AttnTr<DH>::LDV;
   constexpr int ldk = DH + KPAD;
-  bf16* Ks = reinterpret_cast<bf16*>(smem);
-  bf16* Vs = Ks + (size_t)Tpad * ldk;
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
-  const int D = H * DH, ld = 3 * D;
-  const bf16* base = qkv + (size_t)b * Tn * ld + h * DH;
-  const int tid = threadIdx.x, nthr = blockDim.x;
-  // K and V row-major, 16-B chunks; every load of a thread issued before its first LDS store
-  constexpr int MAXC = 8;  // chunks per thread per operand (Tpad * CPR <= nthr * MAXC)
-  uint4 kv[MAXC], vv[MAXC];
-#pragma unroll
-  for (int u = 0; u < MAXC; ++u) {
-    const int i = tid + u * nthr;
-    const int r = i / CPR, c = i - r * CPR;
-    kv[u] = vv[u] = uint4{0, 0, 0, 0};
-    if (r < Tn && i < Tpad * CPR) {
-      kv[u] = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + D + c * 8);
-      vv[u] = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + 2 * D + c * 8);
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < MAXC; ++u) {
-    const int i = tid + u * nthr;
-    if (i < Tpad * CPR) {
-      const int r = i / CPR, c = i - r * CPR;
-      *reinterpret_cast<uint4*>(Ks + (size_t)r * ldk + c * 8) = kv[u];
-      *reinterpret_cast<uint4*>(Vs + (size_t)r * LDV + c * 8) = vv[u];
-    }
-  }
-  __syncthreads();
-
-  const int lane = tid & 63, wave = tid >> 6;
-  const int q0 = wave * 32;
-  if (q0 >= Tn) return;  // whole wave: EXEC stays all-ones for the transposed reads below
   const int col = lane & 31, hh = lane >> 5;
   const int q = q0 + col;
-  const int qc = q < Tn ? q : Tn - 1;
-  const bf16* qrow = base + (size_t)qc * ld;
-  bf16x8 qf[DH / 16];
-#pragma unroll
-  for (int s2 = 0; s2 < DH / 16; ++s2) qf[s2] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s2 + 8 * hh);
   // transposed-read lane roles: group g = lane >> 4 reads keys k0 + 4*(g>>1) + qq, d columns 16*(g&1) + 4*pp
   const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
   const int trow = 4 * (g >> 1) + qq, tcol = 16 * (g & 1) + 4 * pp;
@@ -315,9 +278,9 @@ mha_fwd_bf16_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
   }
   l_run += __shfl_xor(l_run, 32);
   if (q >= Tn) return;
-  if (lse && hh == 0) lse[(size_t)bh * Tn + q] = m_run * c + log2f(l_run);
+  if (lse && hh == 0) lse[q] = m_run * c + log2f(l_run);
   const float inv_l = 1.0f / l_run;
-  bf16* orow = out + ((size_t)b * Tn + q) * D + h * DH;
+  bf16* orow = obase + (size_t)q * D;
 #pragma unroll
   for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
@@ -326,6 +289,55 @@ mha_fwd_bf16_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
       f32x4 v{O[dt][4 * gg] * inv_l, O[dt][4 * gg + 1] * inv_l, O[dt][4 * gg + 2] * inv_l, O[dt][4 * gg + 3] * inv_l};
       store4(orow + d, v);
     }
+}
+
+
+template <int DH>
+__global__ void __launch_bounds__(1024)
+mha_fwd_bf16_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int Tn, int H,
+                    int Tpad, float scale_log2e) {
+  constexpr int KPAD = 8, CPR = DH / 8, LDV = AttnTr<DH>::LDV;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int ldk = DH + KPAD;
+  bf16* Ks = reinterpret_cast<bf16*>(smem);
+  bf16* Vs = Ks + (size_t)Tpad * ldk;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int D = H * DH, ld = 3 * D;
+  const bf16* base = qkv + (size_t)b * Tn * ld + h * DH;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  // K and V row-major, 16-B chunks; every load of a thread issued before its first LDS store
+  constexpr int MAXC = 8;  // chunks per thread per operand (Tpad * CPR <= nthr * MAXC)
+  uint4 kv[MAXC], vv[MAXC];
+#pragma unroll
+  for (int u = 0; u < MAXC; ++u) {
+    const int i = tid + u * nthr;
+    const int r = i / CPR, c = i - r * CPR;
+    kv[u] = vv[u] = uint4{0, 0, 0, 0};
+    if (r < Tn && i < Tpad * CPR) {
+      kv[u] = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + D + c * 8);
+      vv[u] = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + 2 * D + c * 8);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < MAXC; ++u) {
+    const int i = tid + u * nthr;
+    if (i < Tpad * CPR) {
+      const int r = i / CPR, c = i - r * CPR;
+      *reinterpret_cast<uint4*>(Ks + (size_t)r * ldk + c * 8) = kv[u];
+      *reinterpret_cast<uint4*>(Vs + (size_t)r * LDV + c * 8) = vv[u];
+    }
+  }
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6;
+  const int q0 = wave * 32;
+  if (q0 >= Tn) return;  // whole wave: EXEC stays all-ones for the transposed reads below
+  // (Q issued with the K / V loads instead, one HBM round trip for both, measured 5-10 % slower)
+  const bf16* qrow = base + (size_t)min(q0 + (lane & 31), Tn - 1) * ld;
+  bf16x8 qf[DH / 16];
+#pragma unroll
+  for (int s2 = 0; s2 < DH / 16; ++s2) qf[s2] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s2 + 8 * (lane >> 5));
+  mha_bf16_item<DH>(Ks, Vs, qf, Tn, Tpad, scale_log2e, lane, q0, lse ? lse + (size_t)bh * Tn : nullptr,
+                    out + (size_t)b * Tn * D + h * DH, D);
 }
 
 template <typename T, int DH>

@@ -169,7 +169,7 @@ static int conv_t(const tmae_conv_args& a, hipStream_t st) {
     TMAE_GO(r);
   }
   if (a.act == TMAE_ACT_RELU) {  // VGG16 (loss/vgg.py): plain conv + ReLU, no addend / copies
-    TMAE_REQUIRE(!a.addend && !a.y32 && !a.pre, "tmae_conv3x3: ReLU supports plain stores only");
+    TMAE_REQUIRE(!a.addend && !a.pre, "tmae_conv3x3: ReLU supports plain stores (+ an f32 copy) only");
     if (a.y_f32) {
       auto r = make_store<float, TMAE_ACT_RELU>((float*)a.y, a.ldy, a.bias);
       r.so = BStride{a.y_s1, a.y_s2};
@@ -179,6 +179,9 @@ static int conv_t(const tmae_conv_args& a, hipStream_t st) {
     auto r = make_store<T, TMAE_ACT_RELU>((T*)a.y, a.ldy, a.bias);
     r.so = BStride{a.y_s1, a.y_s2};
     r.sb = BStride{a.b_s1, a.b_s2};
+    r.out32 = a.y32;
+    r.ld32 = a.ld32;
+    r.s32 = BStride{a.y32_s1, a.y32_s2};
     return launch_gemm<true, T>(nm, W, a.w_s1, a.w_s2, N, K, xs, r, M, a.nb1, a.nb2, st);
   }
   if (a.y_f32) {

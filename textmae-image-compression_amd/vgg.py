@@ -74,15 +74,19 @@ class Vgg16Features:
         _lib.call("tmae_vgg_prep", x.data_ptr(), n, C, H, W, CIN_PAD, h.data_ptr(), code, _stream())
         saved = {"shape": (n, C, H, W), "acts": [], "args": []}
         cur, hh, ww = h, H, W
-        r22 = None
+        feats = []
         for j, (cin, cout) in enumerate(self.ch):
             y = self._e(n * hh * ww, cout)
+            # relu2_2 / relu3_3 feed the MSE: kept in f32 as well on the bf16 path (their difference is
+            # small next to their magnitude)
+            y32 = None
+            if j in (3, 6):
+                y32 = y if dt == torch.float32 else self._e(n * hh * ww, cout, dtype=torch.float32)
+                feats.append(y32)
             ops.conv3x3(cur, cin, cin, n, hh, ww, self.w[j], self.b[j], y, cout, cout, dt, act=ACT_RELU,
-                        y_f32=(dt == torch.float32))
+                        y_f32=(dt == torch.float32), y32=None if y32 is y else y32, ld32=cout)
             saved["acts"].append((y, hh, ww))
             cur = y
-            if j == 3:
-                r22 = y
             if CONVS[j] in POOL_AFTER:
                 p = self._e(n * (hh // 2) * (ww // 2), cout)
                 arg = torch.empty(p.numel(), dtype=torch.uint8, device=self.device) if keep else None
@@ -90,12 +94,15 @@ class Vgg16Features:
                           None if arg is None else arg.data_ptr(), code, _stream())
                 saved["args"].append(arg)
                 cur, hh, ww = p, hh // 2, ww // 2
-        return r22, cur, (saved if keep else None)
+        return feats[0], feats[1], (saved if keep else None)
 
     def backward(self, saved, g22, g33):
-        """d loss / d x (NCHW f32) from the gradients at relu2_2 and relu3_3 (operand dtype, NHWC)"""
+        """d loss / d x (NCHW f32) from the f32 gradients at relu2_2 and relu3_3 (NHWC)"""
         n, C, H, W = saved["shape"]
         dt, code = self.dtype, ops.dtype_code(self.dtype)
+        if dt != torch.float32:  # the data gradients run in the operand dtype
+            g22 = T.relayout(g22, torch.empty(g22.shape, dtype=dt, device=self.device), (g22.numel(),), (1,))
+            g33 = T.relayout(g33, torch.empty(g33.shape, dtype=dt, device=self.device), (g33.numel(),), (1,))
         acts, args = saved["acts"], list(saved["args"])
         g = g33
         for j in reversed(range(len(self.ch))):
@@ -135,7 +142,7 @@ class FeatureLossFn(torch.autograd.Function):
         need = ctx.needs_input_grad[0]
         p22, p33, saved = net.forward(preds, keep=need)
         t22, t33, _ = net.forward(imgs, keep=False)
-        code = ops.dtype_code(net.dtype)
+        code = ops.dtype_code(torch.float32)  # the features reach the MSE in f32
         out = torch.empty((), dtype=torch.float32, device=net.device)
         part = _part(net.device)
         _lib.call("tmae_mse", p22.data_ptr(), t22.data_ptr(), p22.numel(), part.data_ptr(), out.data_ptr(), 0, code,
@@ -151,7 +158,7 @@ class FeatureLossFn(torch.autograd.Function):
     def backward(ctx, g):
         net = ctx.net
         p22, t22, p33, t33 = ctx.feats
-        code = ops.dtype_code(net.dtype)
+        code = ops.dtype_code(torch.float32)
         g = g.float().contiguous().reshape(1)
         g22, g33 = torch.empty_like(p22), torch.empty_like(p33)
         _lib.call("tmae_mse_bwd", p22.data_ptr(), t22.data_ptr(), p22.numel(), g.data_ptr(), g22.data_ptr(), code,
