@@ -132,6 +132,7 @@ SIGNATURES = {
     "tmae_dgrad_linear": [P, I, I, I, I, P, I, I, I, P, I, I, P, I, P, I, I, P],
     "tmae_conv_dgrad": [ctypes.POINTER(ConvDgradArgs), I, P],
     "tmae_relayout": [P, P, I, I, I, I, I, LL, LL, LL, LL, P],
+    "tmae_relayout_multi": [P, I, LL, P],
     "tmae_colsum": [P, I, I, I, I, I, I, I, P, LL, P, I, P],
     "tmae_layernorm_bwd": [P, P, P, P, P, P, I, I, I, I, I, I, F, P, LL, P, P, P, I, P],
     "tmae_unshuffle_bwd": [P, I, I, P, I, P, I, I, I, I, I, P],

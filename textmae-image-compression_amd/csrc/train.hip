@@ -313,6 +313,44 @@ extern "C" int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0,
   TMAE_LAUNCH_CHECK("tmae_relayout");
 }
 
+// multi-tensor form: table[t] = {src, dst, dst_dtype, d1, d2, d3, s0, s1, s2, s3, total, first_chunk} (int64);
+// 2048-element chunks, a block finds its tensor by binary search over first_chunk.  One launch re-lays out
+// every weight whose version moved (the optimizer step), instead of one launch per weight and layout.
+__global__ void __launch_bounds__(256)
+relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
+  const long long b = blockIdx.x;
+  int lo = 0, hi = nt - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[12 * mid + 11] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const long long* e = tab + 12 * lo;
+  const float* src = (const float*)e[0];
+  const int d1 = (int)e[3], d2 = (int)e[4], d3 = (int)e[5];
+  const long long s0 = e[6], s1 = e[7], s2 = e[8], s3 = e[9], total = e[10];
+  const long long base = (b - e[11]) * 2048;
+  for (int k = threadIdx.x; k < 2048; k += 256) {
+    const long long i = base + k;
+    if (i >= total) break;
+    long long r = i;
+    const int i3 = (int)(r % d3); r /= d3;
+    const int i2 = (int)(r % d2); r /= d2;
+    const int i1 = (int)(r % d1);
+    const long long i0 = r / d1;
+    const float v = src[i0 * s0 + i1 * s1 + i2 * s2 + i3 * s3];
+    if (e[2] == TMAE_BF16) ((bf16*)e[1])[i] = (bf16)v;
+    else ((float*)e[1])[i] = v;
+  }
+}
+
+extern "C" int tmae_relayout_multi(const long long* table, int ntensors, long long nchunks, void* stream) {
+  TMAE_REQUIRE(table && ntensors > 0, "tmae_relayout_multi: bad arguments");
+  if (nchunks <= 0) return TMAE_OK;
+  hipLaunchKernelGGL(relayout_multi_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, table, ntensors);
+  TMAE_LAUNCH_CHECK("tmae_relayout_multi");
+}
+
 // ================================================================== column sums (bias gradients)
 // part[split][c] = sum over this split's rows r of x[src_row(r)][c]; src_row = (r / G) * Gs + off + r % G
 template <typename T>
@@ -328,6 +366,27 @@ colsum_partial_kernel(const T* __restrict__ x, int ld, int rows, int C, int G, i
     s += (float)x[(size_t)sr * ld + c];
   }
   part[(size_t)blockIdx.y * C + c] = s;
+}
+
+// vector form: a thread owns 8 consecutive columns (one 16-B bf16 load per row, two for f32) and walks its
+// rows with an incremental row-group map (no division per row); needs C, ld multiples of 8
+template <typename T>
+__global__ void __launch_bounds__(256)
+colsum_partial8_kernel(const T* __restrict__ x, int ld, int rows, int C, int G, int Gs, int off, int rows_per_split,
+                       float* __restrict__ part) {
+  const int c = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c >= C) return;
+  const int r0 = blockIdx.y * rows_per_split, r1 = min(rows, r0 + rows_per_split);
+  f32x4 s0{0.f, 0.f, 0.f, 0.f}, s1{0.f, 0.f, 0.f, 0.f};
+  int q = r0 / G, rem = r0 - (r0 / G) * G;
+  for (int r = r0; r < r1; ++r) {
+    f32x4 lo, hi;
+    load8f(x + (size_t)(q * Gs + off + rem) * ld + c, lo, hi);
+    s0 += lo;
+    s1 += hi;
+    if (++rem == G) { rem = 0; ++q; }
+  }
+  store8(part + (size_t)blockIdx.y * C + c, s0, s1);
 }
 
 // fold [rows][C] partials over rows: 64 columns x 16 row-lanes per block, fixed-order LDS tree
@@ -369,6 +428,17 @@ extern "C" int tmae_colsum(const void* x, int x_dtype, int ld, int rows, int C, 
   while ((long long)splits * C > work_elems && splits > 1) splits /= 2;
   TMAE_REQUIRE((long long)splits * C <= work_elems, "tmae_colsum: workspace too small");
   const int rps = ceil_div(std::max(rows, 1), splits);
+  if (C % 8 == 0 && ld % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)work & 15) == 0) {
+    const dim3 grid8(ceil_div(C / 8, 256), splits);
+    if (x_dtype == TMAE_BF16)
+      hipLaunchKernelGGL(colsum_partial8_kernel<bf16>, grid8, dim3(256), 0, st, (const bf16*)x, ld, rows, C, row_group,
+                         group_stride, row_offset, rps, work);
+    else
+      hipLaunchKernelGGL(colsum_partial8_kernel<float>, grid8, dim3(256), 0, st, (const float*)x, ld, rows, C,
+                         row_group, group_stride, row_offset, rps, work);
+    fold_rows(work, splits, C, out, out, C, accumulate, st);
+    TMAE_LAUNCH_CHECK("tmae_colsum");
+  }
   const dim3 grid(ceil_div(C, 256), splits);
   if (x_dtype == TMAE_BF16)
     hipLaunchKernelGGL(colsum_partial_kernel<bf16>, grid, dim3(256), 0, st, (const bf16*)x, ld, rows, C, row_group,

@@ -22,7 +22,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import _lib, ops
 from . import train_ops as T
 from .ops import ACT_GELU, ACT_NONE
 
@@ -32,63 +32,99 @@ def _convs(seq):
 
 
 class _Weights:
-    """Kernel-layout copies of the f32 parameters, rebuilt when a parameter's version changes
-    (once per optimizer step)."""
+    """Kernel-layout copies of the f32 parameters, rebuilt when a parameter's version changes (once per
+    optimizer step).  The first build of each (parameter, layout) is lazy; afterwards ``refresh()`` re-lays
+    out every stale copy in ONE multi-tensor launch (tmae_relayout_multi), plain transposes excepted (their
+    LDS-tiled kernel, one launch each)."""
 
     def __init__(self, dtype):
         self.dtype = dtype
-        self.cache = {}
+        self.cache = {}   # (id(p), kind) -> [sig, tensor, p, job]; job = (dims, strides) or None (a view)
+        self._tab = None
 
-    def _get(self, p, kind, build):
+    def _get(self, p, kind, make):
         key = (id(p), kind)
         sig = (p.data_ptr(), p._version)
         hit = self.cache.get(key)
         if hit is not None and hit[0] == sig:
             return hit[1]
-        t = build(p.detach())
-        self.cache[key] = (sig, t)
-        return t
+        w = p.detach()
+        dst, job = make(w)
+        if job is not None:
+            T.relayout(w, dst, *job)
+        self.cache[key] = [sig, dst, p, job]
+        return dst
+
+    @staticmethod
+    def _is_transpose(dims, strides):
+        d = list(dims) + [1] * (4 - len(dims))
+        st = list(strides) + [0] * (4 - len(strides))
+        return d[1] == 1 and d[2] == 1 and st[0] == 1 and st[3] >= d[0]
+
+    def refresh(self):
+        """re-lay out every cached copy whose parameter moved since it was built"""
+        stale = [e for e in self.cache.values() if e[0] != (e[2].data_ptr(), e[2]._version)]
+        if not stale:
+            return
+        rows, chunk, ptrs = [], 0, []
+        for e in stale:
+            sig, dst, p, job = e
+            e[0] = (p.data_ptr(), p._version)
+            if job is None:
+                continue
+            dims, strides = job
+            if self._is_transpose(dims, strides):
+                T.relayout(p.detach(), dst, dims, strides)
+                continue
+            d = list(dims) + [1] * (4 - len(dims))
+            st = list(strides) + [0] * (4 - len(strides))
+            total = d[0] * d[1] * d[2] * d[3]
+            rows.append([p.data_ptr(), dst.data_ptr(), ops.dtype_code(dst.dtype), d[1], d[2], d[3], *st, total, chunk])
+            ptrs.append((p.data_ptr(), dst.data_ptr()))
+            chunk += (total + 2047) // 2048
+        if not rows:
+            return
+        key = tuple(ptrs)
+        if self._tab is None or self._tab[0] != key:
+            dev = stale[0][1].device
+            self._tab = (key, torch.tensor(rows, dtype=torch.int64).to(dev), chunk)
+        _lib.call("tmae_relayout_multi", self._tab[1].data_ptr(), len(rows), self._tab[2],
+                  torch.cuda.current_stream().cuda_stream)
+
+    def _cast_same(self, w2):
+        if self.dtype == torch.float32:
+            return w2.contiguous(), None
+        return torch.empty(w2.shape, dtype=self.dtype, device=w2.device), ((w2.numel(),), (1,))
 
     def nt(self, p, rows=None):
         """nn.Linear / 1x1 conv weight as [N][K] in the operand dtype"""
-        def b(w):
-            w2 = w.reshape(w.shape[0], -1) if rows is None else w.reshape(rows, -1)
-            if self.dtype == torch.float32:
-                return w2.contiguous()
-            return T.relayout(w2, torch.empty(w2.shape, dtype=self.dtype, device=w.device), (w2.numel(),), (1,))
-        return self._get(p, "nt", b)
+        return self._get(p, "nt", lambda w: self._cast_same(w.reshape(w.shape[0], -1) if rows is None
+                                                            else w.reshape(rows, -1)))
 
     def t(self, p, rows=None):
         """transposed [K][N] (the data-gradient operand of y = x W^T)"""
         def b(w):
             w2 = w.reshape(w.shape[0], -1) if rows is None else w.reshape(rows, -1)
             N, K = w2.shape
-            return T.relayout(w2, torch.empty((K, N), dtype=self.dtype, device=w.device), (K, 1, 1, N), (1, 0, 0, K))
+            return torch.empty((K, N), dtype=self.dtype, device=w.device), ((K, 1, 1, N), (1, 0, 0, K))
         return self._get(p, "t", b)
 
     def raw(self, p):
         """the weight as stored ([cin][cout] for ConvTranspose2d 1x1), cast"""
-        def b(w):
-            w2 = w.reshape(w.shape[0], -1)
-            if self.dtype == torch.float32:
-                return w2.contiguous()
-            return T.relayout(w2, torch.empty(w2.shape, dtype=self.dtype, device=w.device), (w2.numel(),), (1,))
-        return self._get(p, "raw", b)
+        return self._get(p, "raw", lambda w: self._cast_same(w.reshape(w.shape[0], -1)))
 
     def conv(self, p):
         """Conv2d 3x3 weight [Cout][Cin][3][3] -> [Cout][3][3][Cin] (forward implicit GEMM)"""
         def b(w):
             co, ci = w.shape[:2]
-            return T.relayout(w, torch.empty((co, 9 * ci), dtype=self.dtype, device=w.device), (co, 3, 3, ci),
-                              (ci * 9, 3, 1, 9))
+            return torch.empty((co, 9 * ci), dtype=self.dtype, device=w.device), ((co, 3, 3, ci), (ci * 9, 3, 1, 9))
         return self._get(p, "conv", b)
 
     def conv_dg(self, p):
         """-> [Cin][3][3][Cout] (transposed-conv data gradient)"""
         def b(w):
             co, ci = w.shape[:2]
-            return T.relayout(w, torch.empty((ci, 9 * co), dtype=self.dtype, device=w.device), (ci, 3, 3, co),
-                              (9, 3, 1, ci * 9))
+            return torch.empty((ci, 9 * co), dtype=self.dtype, device=w.device), ((ci, 3, 3, co), (9, 3, 1, ci * 9))
         return self._get(p, "conv_dg", b)
 
 
@@ -185,6 +221,7 @@ class TrainExec:
         if imgs.shape[1:] != (m.encoder_embed.proj.in_channels, self.img, self.img):
             raise ValueError(f"Input image size {tuple(imgs.shape[2:])} doesn't match model ({self.img})")
         self.imgs = imgs
+        self.w.refresh()  # one launch for every weight copy the last optimizer step made stale
         if noise is not None:
             self.z_noise, self.y_noise = (t.float().contiguous() for t in noise)
         elif not m.training:  # eval semantics: round(x - median) + median / round(y - mu) + mu
