@@ -351,3 +351,36 @@ def test_mcm_train_vitb_step_runs():
         losses.append(loss.item())
     assert all(math.isfinite(v) for v in losses)
     assert all(torch.isfinite(p).all() for p in m.parameters())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_relayout_multi_dense_and_strided(T, dt):
+    """tmae_relayout_multi (the weight cache's one launch per optimizer step): plain casts (vector path,
+    ragged tails, an unaligned destination) and strided permutes in one table, exact against torch"""
+    from textmae_amd import _lib, ops
+
+    dev = "cuda"
+    srcs = [_rnd(5000, seed=1), _rnd(64, 3, 3, 40, seed=2), _rnd(4096, seed=3), _rnd(96, 130, seed=4),
+            _rnd(2048 * 3 + 7, seed=5)]
+    srcs = [s.to(dev) for s in srcs]
+    big = torch.empty(2048 * 3 + 8, dtype=dt, device=dev)
+    jobs = [  # (source, destination, dims, element strides)
+        (srcs[0], torch.empty(5000, dtype=dt, device=dev), (5000,), (1,)),
+        (srcs[1], torch.empty(64, 40, 3, 3, dtype=dt, device=dev), (64, 40, 3, 3), (360, 1, 120, 40)),
+        (srcs[2], torch.empty(4096, dtype=dt, device=dev), (4096,), (1,)),
+        (srcs[3], torch.empty(130, 96, dtype=dt, device=dev), (130, 96), (1, 130)),
+        (srcs[4], big[1:], (2048 * 3 + 7,), (1,)),   # destination 2 or 4 B past a 16-B boundary
+    ]
+    rows, chunk = [], 0
+    for s, d, dims, st in jobs:
+        dd = list(dims) + [1] * (4 - len(dims))
+        ss = list(st) + [0] * (4 - len(st))
+        total = dd[0] * dd[1] * dd[2] * dd[3]
+        rows.append([s.data_ptr(), d.data_ptr(), ops.dtype_code(dt), dd[1], dd[2], dd[3], *ss, total, chunk])
+        chunk += (total + 2047) // 2048
+    tab = torch.tensor(rows, dtype=torch.int64).to(dev)
+    _lib.call("tmae_relayout_multi", tab.data_ptr(), len(rows), chunk, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for s, d, dims, st in jobs:
+        ref = torch.as_strided(s, dims, st).to(dt)
+        assert torch.equal(d.reshape(dims), ref)

@@ -9,7 +9,7 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libtmae.so")
+LIB_PATH = os.environ.get("TMAE_LIB") or os.path.join(PKG_DIR, "lib", "libtmae.so")  # TMAE_LIB: A/B builds
 
 TMAE_F32, TMAE_BF16 = 0, 1
 ACT_NONE, ACT_GELU, ACT_RELU = 0, 1, 2

@@ -22,6 +22,9 @@ CXX = os.environ.get("CXX", "g++")
 
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}", "-Wno-unused-result"]
 HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"-I{INCLUDE}", "-Wall"]
+# per-source extras.  attention.hip: the softmax max trees take MFMA results through loop phis, where IEEE-mode
+# fmaxf would first quiet each operand (one v_max_f32 x, x per score); scores are finite or the -inf mask.
+EXTRA = {"attention.hip": ["-fno-honor-nans"]}
 
 
 def _sources():
@@ -42,7 +45,7 @@ def _compile(src: str, hdr_mtime: float, verbose: bool) -> str:
     if src.endswith(".cpp"):
         cmd = [CXX, *HOST_FLAGS, "-c", src, "-o", obj]
     else:
-        cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+        cmd = [HIPCC, *FLAGS, *EXTRA.get(os.path.basename(src), []), "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

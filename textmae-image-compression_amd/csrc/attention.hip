@@ -195,8 +195,25 @@ template <> struct AttnTr<32> { static constexpr int LDV = 32; };
 typedef __attribute__((ext_vector_type(4))) short attn_s4;
 typedef __attribute__((address_space(3))) attn_s4 attn_lds_s4;
 
+typedef __attribute__((ext_vector_type(2))) float attn_f2;
+
+// max / sum over the two lane halves (lane l <-> l ^ 32) without an LDS round trip: v_permlane32_swap with
+// the value in both operands returns {own, partner} in lanes 0-31 and {partner, own} in lanes 32-63
+__device__ __forceinline__ float attn_xhalf_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float attn_xhalf_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // one (image, head) item of the bf16 forward: this wave's 32 queries against the K / V tiles staged in
-// LDS (Ks row-major [Tpad][DH + 8], Vs row-major [Tpad][LDV]); writes O (and the base-2 LSE when lse)
+// LDS (Ks row-major [Tpad][DH + 8], Vs row-major [Tpad][LDV]); writes O (and the base-2 LSE when lse).
+// Software pipeline: the S^T MFMAs of key tile kt+1 are issued before the softmax of tile kt, so they run
+// under its VALU work instead of stalling the max reduction.  The softmax runs on packed pairs
+// (v_pk_fma_f32 / v_pk_add_f32), the cross-half reductions on v_permlane32_swap, and only the last key
+// tile carries the ragged-length mask (peeled out of the loop).
 template <int DH>
 __device__ __forceinline__ void mha_bf16_item(const bf16* Ks, const bf16* Vs, const bf16x8 (&qf)[DH / 16], int Tn,
                                               int Tpad, float scale_log2e, int lane, int q0, float* lse, bf16* obase,
@@ -216,10 +233,12 @@ __device__ __forceinline__ void mha_bf16_item(const bf16* Ks, const bf16* Vs, co
     for (int r = 0; r < 16; ++r) O[dt][r] = 0.0f;
   const float c = scale_log2e;
   const float thr = 8.0f / c;  // 8 in log2 units, in raw-score units
-  float m_run = -INFINITY, l_run = 0.0f;
+  float m_run = -INFINITY;
+  attn_f2 l2 = {0.0f, 0.0f};
   const int ntiles = Tpad / 32;
   const bool ragged = (Tn & 31) != 0;
-  for (int kt = 0; kt < ntiles; ++kt) {
+
+  auto qk = [&](int kt) {
     f32x16 S;
 #pragma unroll
     for (int r = 0; r < 16; ++r) S[r] = 0.0f;
@@ -229,7 +248,10 @@ __device__ __forceinline__ void mha_bf16_item(const bf16* Ks, const bf16* Vs, co
       const bf16x8 a = *reinterpret_cast<const bf16x8*>(krow + 16 * s2);
       S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s2], S, 0, 0, 0);
     }
-    if (ragged && kt == ntiles - 1) {
+    return S;
+  };
+  auto step = [&](f32x16 S, int kt, bool mask) {
+    if (mask) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
@@ -239,28 +261,31 @@ __device__ __forceinline__ void mha_bf16_item(const bf16* Ks, const bf16* Vs, co
     float t0 = fmaxf(fmaxf(S[0], S[1]), S[2]), t1 = fmaxf(fmaxf(S[3], S[4]), S[5]);
     float t2 = fmaxf(fmaxf(S[6], S[7]), S[8]), t3 = fmaxf(fmaxf(S[9], S[10]), S[11]);
     float t4 = fmaxf(fmaxf(S[12], S[13]), S[14]);
-    float tmax = fmaxf(fmaxf(fmaxf(t0, t1), fmaxf(t2, t3)), fmaxf(t4, S[15]));
-    tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+    const float tmax = attn_xhalf_max(fmaxf(fmaxf(fmaxf(t0, t1), fmaxf(t2, t3)), fmaxf(t4, S[15])));
     const bool grow = tmax > m_run + thr;
     if (__builtin_amdgcn_ballot_w64(grow)) {
       const float m_new = grow ? tmax : m_run;
       const float alpha = exp2f((m_run - m_new) * c);
-      l_run *= alpha;
+      l2 *= alpha;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) O[dt] *= alpha;
       m_run = m_new;
     }
-    const float mc = -m_run * c;
+    const attn_f2 c2 = {c, c}, mc2 = {-m_run * c, -m_run * c};
+    float P[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      S[r] = __builtin_amdgcn_exp2f(fmaf(S[r], c, mc));
-      l_run += S[r];
+    for (int r = 0; r < 16; r += 2) {
+      const attn_f2 e = __builtin_elementwise_fma((attn_f2){S[r], S[r + 1]}, c2, mc2);
+      const attn_f2 p = {__builtin_amdgcn_exp2f(e.x), __builtin_amdgcn_exp2f(e.y)};
+      l2 += p;
+      P[r] = p.x;
+      P[r + 1] = p.y;
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       bf16x8 pb;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) pb[j] = (bf16)S[8 * s2 + j];
+      for (int j = 0; j < 8; ++j) pb[j] = (bf16)P[8 * s2 + j];
       const int k0 = 32 * kt + 16 * s2;
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
@@ -275,8 +300,24 @@ __device__ __forceinline__ void mha_bf16_item(const bf16* Ks, const bf16* Vs, co
         O[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<bf16x8*>(&av), pb, O[dt], 0, 0, 0);
       }
     }
+  };
+  // two tiles per trip so the look-ahead scores alternate between two register sets (no copies)
+  f32x16 S0 = qk(0);
+  int kt = 0;
+  for (; kt + 2 < ntiles; kt += 2) {
+    const f32x16 S1 = qk(kt + 1);
+    step(S0, kt, false);
+    S0 = qk(kt + 2);
+    step(S1, kt + 1, false);
   }
-  l_run += __shfl_xor(l_run, 32);
+  if (kt + 1 < ntiles) {
+    const f32x16 S1 = qk(kt + 1);
+    step(S0, kt, false);
+    step(S1, kt + 1, ragged);
+  } else {
+    step(S0, kt, ragged);
+  }
+  const float l_run = attn_xhalf_sum(l2.x + l2.y);
   if (q >= Tn) return;
   if (lse && hh == 0) lse[q] = m_run * c + log2f(l_run);
   const float inv_l = 1.0f / l_run;

@@ -70,6 +70,24 @@ __device__ __forceinline__ float gelu_bf16out(float x) {
   const float z = xc * fmaf(fmaf(1.0142631e-3f, x2, -0.10677572f), x2, -2.3011213f);  // -log2e (a + b x2 + c x4)
   return x * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(z));
 }
+// the same on two values with packed f32 math (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32: two lanes' worth of
+// FMA-class work per issue; bitwise equal to gelu_bf16out, same operations in the same order)
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+__device__ __forceinline__ f32x2 gelu2_bf16out(f32x2 x) {
+  const f32x2 xc = {__builtin_amdgcn_fmed3f(x.x, -10.0f, 10.0f), __builtin_amdgcn_fmed3f(x.y, -10.0f, 10.0f)};
+  const f32x2 x2 = xc * xc;
+  f32x2 p = __builtin_elementwise_fma((f32x2){1.0142631e-3f, 1.0142631e-3f}, x2, (f32x2){-0.10677572f, -0.10677572f});
+  p = __builtin_elementwise_fma(p, x2, (f32x2){-2.3011213f, -2.3011213f});
+  const f32x2 z = xc * p;
+  const f32x2 d = (f32x2){1.0f, 1.0f} + (f32x2){__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)};
+  return x * (f32x2){__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+__device__ __forceinline__ void gelu8_bf16out(f32x4& lo, f32x4& hi) {
+  lo.xy = gelu2_bf16out(lo.xy);
+  lo.zw = gelu2_bf16out(lo.zw);
+  hi.xy = gelu2_bf16out(hi.xy);
+  hi.zw = gelu2_bf16out(hi.zw);
+}
 // the GELU an epilogue storing OT applies
 template <typename OT> __device__ __forceinline__ float gelu_for(float x) {
   if constexpr (sizeof(OT) == 2) return gelu_bf16out(x);

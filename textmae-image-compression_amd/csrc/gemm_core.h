@@ -990,8 +990,12 @@ template <typename OT, int ACT> struct EpiStore {
     if (addend) { lo += p.a0; hi += p.a1; }
     if (pre) store8(pre + (size_t)m * ldp + n, lo, hi);
     if (ACT == TMAE_ACT_GELU) {
+      if constexpr (sizeof(OT) == 2) {
+        gelu8_bf16out(lo, hi);
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { lo[j] = gelu_for<OT>(lo[j]); hi[j] = gelu_for<OT>(hi[j]); }
+        for (int j = 0; j < 4; ++j) { lo[j] = gelu_for<OT>(lo[j]); hi[j] = gelu_for<OT>(hi[j]); }
+      }
     }
     if (ACT == TMAE_ACT_RELU) {
 #pragma unroll

@@ -327,19 +327,34 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
   }
   const long long* e = tab + 12 * lo;
   const float* src = (const float*)e[0];
-  const int d1 = (int)e[3], d2 = (int)e[4], d3 = (int)e[5];
-  const long long s0 = e[6], s1 = e[7], s2 = e[8], s3 = e[9], total = e[10];
-  const long long base = (b - e[11]) * 2048;
-  for (int k = threadIdx.x; k < 2048; k += 256) {
-    const long long i = base + k;
+  const unsigned d1 = (unsigned)e[3], d2 = (unsigned)e[4], d3 = (unsigned)e[5];
+  const long long s0 = e[6], s1 = e[7], s2 = e[8], s3 = e[9];
+  const unsigned total = (unsigned)e[10];  // < 2^31 (host check)
+  const unsigned base = (unsigned)(b - e[11]) * 2048u;
+  const bool to_bf16 = e[2] == TMAE_BF16;
+  // a plain cast (contiguous source, 16-B aligned ends): 8 elements per thread, vector loads and stores
+  const bool dense = (d3 == 1 || s3 == 1) && (d2 == 1 || s2 == (long long)d3) && (d1 == 1 || s1 == (long long)d2 * d3) &&
+                     s0 == (long long)d1 * d2 * d3 &&
+                     ((((unsigned long long)src) | ((unsigned long long)e[1])) & 15) == 0;
+  if (dense && base + 2048u <= total) {
+    const unsigned i = base + 8u * threadIdx.x;
+    f32x4 lo, hi;
+    load8f(src + i, lo, hi);
+    if (to_bf16) store8((bf16*)e[1] + i, lo, hi);
+    else store8((float*)e[1] + i, lo, hi);
+    return;
+  }
+  // general strided gather: 32-bit index arithmetic (64-bit division is a long VALU sequence)
+  for (unsigned k = threadIdx.x; k < 2048u; k += 256u) {
+    const unsigned i = base + k;
     if (i >= total) break;
-    long long r = i;
-    const int i3 = (int)(r % d3); r /= d3;
-    const int i2 = (int)(r % d2); r /= d2;
-    const int i1 = (int)(r % d1);
-    const long long i0 = r / d1;
-    const float v = src[i0 * s0 + i1 * s1 + i2 * s2 + i3 * s3];
-    if (e[2] == TMAE_BF16) ((bf16*)e[1])[i] = (bf16)v;
+    unsigned r = i;
+    const unsigned i3 = r % d3; r /= d3;
+    const unsigned i2 = r % d2; r /= d2;
+    const unsigned i1 = r % d1;
+    const unsigned i0 = r / d1;
+    const float v = src[(long long)i0 * s0 + (long long)i1 * s1 + (long long)i2 * s2 + (long long)i3 * s3];
+    if (to_bf16) ((bf16*)e[1])[i] = (bf16)v;
     else ((float*)e[1])[i] = v;
   }
 }

@@ -79,6 +79,8 @@ class _Weights:
             d = list(dims) + [1] * (4 - len(dims))
             st = list(strides) + [0] * (4 - len(strides))
             total = d[0] * d[1] * d[2] * d[3]
+            if total >= 1 << 31:
+                raise ValueError(f"weight relayout of {total} elements exceeds the 32-bit index range")
             rows.append([p.data_ptr(), dst.data_ptr(), ops.dtype_code(dst.dtype), d[1], d[2], d[3], *st, total, chunk])
             ptrs.append((p.data_ptr(), dst.data_ptr()))
             chunk += (total + 2047) // 2048
