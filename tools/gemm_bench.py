@@ -19,11 +19,20 @@ SHAPES = {  # name: (M, N, K, act)
 
 
 def ev_time(fn, reps):
-    fn()
+    """GPU time per call: reps calls captured in one HIP graph, replayed (not the host's launch rate)"""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        fn()
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(reps):
-        fn()
+    g.replay()
     e.record()
     e.synchronize()
     return s.elapsed_time(e) / reps * 1e-3
