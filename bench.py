@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--dump-launches", default=None, help="write every launch of one forward with its family and shape")
     ap.add_argument("--train-steps", type=int, default=10, help="training steps timed after the inference run")
     ap.add_argument("--train-warmup", type=int, default=3)
     ap.add_argument("--train-batch", type=int, default=64)
@@ -180,6 +181,20 @@ class LaunchTimer:
             return "layernorm", 0.0
         return "other:" + name, 0.0
 
+    def describe(self, name, a):
+        """the shape a launch was classified on (the shape -> family mapping, written out by --dump-launches)"""
+        if name == "tmae_linear_fwd":
+            return {"M": a[13], "N": a[14], "K": a[15]}
+        if name == "tmae_linear_residual_fwd":
+            return {"M": a[6], "N": a[7], "K": a[8]}
+        if name == "tmae_mha_fwd":
+            return {"B": a[2], "T": a[3], "H": a[4], "dh": a[5]}
+        if name == "tmae_conv3x3":
+            c = a[0]._obj
+            return {"n": c.n, "H": c.H, "W": c.W, "cin": c.c1 + c.c2, "cout": c.cout, "problems": c.nb1 * c.nb2,
+                    "stride": c.stride, "out_f32": bool(c.y_f32), "addend": bool(c.addend)}
+        return {}
+
     def run(self, fn):
         orig = self._lib.call
         calls = self.calls
@@ -223,10 +238,15 @@ class LaunchTimer:
         return out
 
 
-def roofline_report(m, imgs, scores, batch):
+def roofline_report(m, imgs, scores, batch, dump=None):
     lt = LaunchTimer(m, batch)
     with torch.no_grad():
         fam = lt.run(lambda: m(imgs, scores))
+    if dump:
+        rows = [{"i": i, "entry": name, "family": f, "gflop": round(fl / 1e9, 4), "shape": lt.describe(name, args)}
+                for i, (f, fl, name, args) in enumerate(lt.calls)]
+        with open(dump, "w") as fh:
+            json.dump({"batch": batch, "launches": rows}, fh, indent=0)
     mf = {k: v for k, v in fam.items() if v[2] > 0}
     agg = {"token_gemm": [k for k in mf if k.split("_")[-1] in ("qkv", "proj", "fc1", "fc2")],
            "lic_conv3x3": ["lic_conv3x3"]}
@@ -443,7 +463,7 @@ def main():
         el = max_over_ranks(time.perf_counter() - t0, world, dev, args.backend)
     roof = None
     if rank == 0 and not args.no_roofline:
-        roof = roofline_report(model, imgs, scores, args.batch)
+        roof = roofline_report(model, imgs, scores, args.batch, dump=args.dump_launches)
     graph = None
 
     train = None

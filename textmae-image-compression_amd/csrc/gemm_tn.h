@@ -246,7 +246,10 @@ static inline TnPlan tn_plan(int M, int N, int K, bool bf) {
   const int tiles = ceil_div(N, p.bn) * ceil_div(M, p.bm);
   const int slots = p.nw == 8 ? 256 : 512;
   const int kmin = bf ? 256 : 128;
-  int s = ceil_div(slots, tiles);
+  // splits: as many as fit ONE round of the slots (floor): with the ceiling, tiles * splits overshot the
+  // 256 slots of the 8-wave tile on every encoder weight gradient (qkv 270, fc1 / fc2 288, proj 261
+  // workgroups), and the few workgroups of the second round took a whole round of time
+  int s = std::max(1, slots / tiles);
   s = std::max(1, std::min(s, std::max(1, K / kmin)));
   s = std::min(s, 64);
   const int step = bf ? 64 : 32;

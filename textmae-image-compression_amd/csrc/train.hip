@@ -24,6 +24,26 @@ __device__ __forceinline__ float gelu_grad(float x) {
   return cdf + x * e * 0.39894228040143267794f;
 }
 
+// gelu_grad on two values with packed f32 math (v_pk_fma / v_pk_mul): the same approximation as the scalar
+// form, ~12 VALU issues per element instead of ~19; the data-gradient epilogues apply it to every fc1 / conv
+// element
+__device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) {
+  const f32x2 z = (f32x2){fabsf(x.x), fabsf(x.y)} * 0.70710678118654752440f;
+  const f32x2 d = __builtin_elementwise_fma((f32x2){0.3275911f, 0.3275911f}, z, (f32x2){1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = __builtin_elementwise_fma((f32x2){1.061405429f, 1.061405429f}, t, (f32x2){-1.453152027f, -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, (f32x2){1.421413741f, 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, (f32x2){-0.284496736f, -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, (f32x2){0.254829592f, 0.254829592f});
+  p *= t;
+  const f32x2 a = -z * z * 1.44269504088896341f;
+  const f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  const f32x2 erf_abs = __builtin_elementwise_fma(-p, e, (f32x2){1.0f, 1.0f});
+  const f32x2 pos = 0.5f + 0.5f * erf_abs, neg = 0.5f * p * e;
+  const f32x2 cdf = {x.x >= 0.0f ? pos.x : neg.x, x.y >= 0.0f ? pos.y : neg.y};
+  return cdf + x * e * 0.39894228040143267794f;
+}
+
 // ================================================================== weight gradients (split-K TN GEMM)
 template <typename T>
 static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
@@ -125,7 +145,10 @@ template <typename OT, typename PT> struct EpiDgrad {
   __device__ void wide(int m, int n, f32x4 lo, f32x4 hi, const Pre& q) const {
     if (pre) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) { lo[j] *= gelu_grad(q.p0[j]); hi[j] *= gelu_grad(q.p1[j]); }
+      for (int j = 0; j < 4; j += 2) {
+        const f32x2 gl = gelu_grad2((f32x2){q.p0[j], q.p0[j + 1]}), gh = gelu_grad2((f32x2){q.p1[j], q.p1[j + 1]});
+        lo[j] *= gl.x; lo[j + 1] *= gl.y; hi[j] *= gh.x; hi[j + 1] *= gh.y;
+      }
     }
     if (out) store8(out + (size_t)m * ldo + n, lo, hi);
     if (acc) store8(acc + (size_t)m * lda + n, q.a0 + lo, q.a1 + hi);
