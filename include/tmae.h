@@ -124,6 +124,34 @@ typedef struct tmae_conv_args {
 } tmae_conv_args;
 int tmae_conv3x3(const tmae_conv_args* args, int dtype, void* stream);
 
+/* A whole slice-transform stack -- cc_transform_mean / cc_transform_scale / lrp_transform[i]
+ * (MCM.py:165-293 applied at MCM.py:761-784): `nlayers` 3x3 convs with GELU between them -- for
+ * nb1 x nb2 problems x n images over a G x G grid (G*G <= 144), bf16 operands, one workgroup per
+ * (problem, image) with the activations resident in LDS (every intermediate <= 224 channels).
+ * Layer-0 input: channels [0, c1) of x1 and [c1, c1 + c2) of x2 (NHWC rows ld1 / ld2 apart).
+ * w[l]: weights packed by the caller in MFMA fragment order [tap 9][k-step round32(cin)/32][cout
+ * fragment round16(cout)/16][lane 64][8], zero-padded (textmae_amd.ops.pack_lic_stack_weight);
+ * bias[l]: f32 [cout].  addend (optional, f32, rows ld_add apart) is added to layer 0's output before
+ * its GELU (the latent-channel partial sums).  Last layer: y = acc + bias (f32 if y_f32, else bf16),
+ * or with lrp_src: y (and y2 if set) = lrp_src + 0.5 tanh(acc + bias) in bf16.  Every operand has
+ * per-problem element strides {s1, s2} for problem (b1, b2). */
+#define TMAE_LIC_STACK_MAXL 5
+typedef struct tmae_lic_stack_args {
+  int n, G, nb1, nb2, nlayers;
+  const void* x1; int c1, ld1; long long x1_s[2];
+  const void* x2; int c2, ld2; long long x2_s[2];
+  const void* w[TMAE_LIC_STACK_MAXL]; long long w_s[TMAE_LIC_STACK_MAXL][2];
+  const float* bias[TMAE_LIC_STACK_MAXL]; long long b_s[TMAE_LIC_STACK_MAXL][2];
+  int cout[TMAE_LIC_STACK_MAXL];
+  const float* addend; int ld_add; long long a_s[2];
+  void* y; int y_f32, ldy; long long y_s[2];
+  const float* lrp_src; int ld_src; long long src_s[2];
+  void* y2; int ldy2; long long y2_s[2];
+  int flags; /* TMAE_LIC_STACK_WARM_L2: touch the problem's weights into each XCD's L2 up front */
+} tmae_lic_stack_args;
+#define TMAE_LIC_STACK_WARM_L2 1
+int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream);
+
 /* GaussianConditional likelihood + y_hat quantisation for `nslices` consecutive slices of width sw
  * (MCM.py:767-776): lik[NCHW channel yoff + j*sw + c] = GC(y~, max(sigma, .11), mu), LowerBound 1e-9;
  * yhat (dtype yhat_dtype) and yhat32 (f32, optional) [pixel][channel] = round(y - mu) + mu.

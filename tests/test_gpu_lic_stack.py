@@ -1,0 +1,159 @@
+"""tmae_lic_stack (csrc/lic_stack.hip): a whole slice-transform stack (cc_transform_mean / _scale /
+lrp_transform, MCM.py:165-293 applied at MCM.py:761-784) per workgroup.
+
+* the kernel against a plain PyTorch fp32 restatement of the same stack (conv2d + GELU chain over
+  bf16-rounded operands, activations rounded to bf16 between layers as the kernel stores them in LDS):
+  two input sources (torch.cat without a copy), the layer-0 addend, batched problems with strides, the
+  f32 (mu / sigma) and the lrp (y_hat_pre + 0.5 tanh) outputs, the 12x12 and 8x8 grids, an empty
+  layer-0 input (slice 0's mean / scale stacks);
+* the MCM eval forward with the fused stacks against the layer-by-layer launches (TMAE_LIC_STACK=0) on
+  the same weights, bf16, at the benched geometry.
+Tolerance: bf16 operands, f32 accumulation -> max|a-b| / max|b| <= 2e-2 per output.
+"""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+MID = [224, 176, 128, 80, 32]
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _ref_stack(x, ws, bs, G, addend=None, lrp_src=None):
+    """x [P][n*G*G][cin0] f32 (bf16 values); ws[l] [P][Cout][Cin][3][3]; returns [P][n*G*G][Cout_last]"""
+    P, rows, cin0 = x.shape
+    n = rows // (G * G)
+    outs = []
+    for p in range(P):
+        h = x[p].view(n, G, G, cin0).permute(0, 3, 1, 2)
+        for l, (w, b) in enumerate(zip(ws, bs)):
+            h = F.conv2d(h, w[p], b[p], padding=1) if w[p].shape[1] else b[p].view(1, -1, 1, 1).expand(n, -1, G, G)
+            if l == 0 and addend is not None:
+                h = h + addend[p].view(n, G, G, -1).permute(0, 3, 1, 2)
+            if l + 1 < len(ws):
+                h = _bf(F.gelu(h))
+        h = h.permute(0, 2, 3, 1).reshape(rows, -1)
+        if lrp_src is not None:
+            h = lrp_src[p] + 0.5 * torch.tanh(h)
+        outs.append(h)
+    return torch.stack(outs)
+
+
+def _maxrel(a, b):
+    return float((a.double() - b.double()).abs().max() / b.double().abs().max())
+
+
+@pytest.mark.parametrize("G,c1,c2,nb,mode", [
+    (12, 64, 32, (2, 3), "f32"),
+    (12, 160, 0, (2, 1), "f32"),
+    (12, 0, 0, (2, 1), "f32"),
+    (12, 192, 32, (1, 2), "lrp"),
+    (8, 96, 0, (1, 1), "lrp"),
+])
+def test_lic_stack_vs_torch(tmae, G, c1, c2, nb, mode):
+    from textmae_amd import ops
+
+    torch.manual_seed(G * 1000 + c1 + c2)
+    n, P = 5, nb[0] * nb[1]
+    rows = n * G * G
+    cin0 = c1 + c2
+    ld1, ld2 = c1 + 16, c2 + 8
+    x1 = torch.randn(rows, ld1).to(torch.bfloat16).to(DEV)
+    x2 = torch.randn(P, rows, ld2).to(torch.bfloat16).to(DEV)  # one slab per problem (s2 for b2, s1 for b1)
+    chans = [cin0] + MID
+    ws = [_bf(torch.randn(P, chans[l + 1], chans[l], 3, 3) / (3.0 * max(chans[l], 1) ** 0.5)) for l in range(5)]
+    bs = [torch.randn(P, c) * 0.1 for c in MID]
+    add = torch.randn(P, rows, 240) * 0.5
+    packed = [torch.stack([ops.pack_lic_stack_weight(w[p]) for p in range(P)]).to(DEV) for w in ws]
+    bias = [b.contiguous().to(DEV) for b in bs]
+    addd = add.to(DEV)
+    st = {"x2": (nb[1] * rows * ld2, rows * ld2), "a": (nb[1] * rows * 240, rows * 240)}
+    for l in range(5):
+        sz = packed[l][0].numel()
+        st[f"w{l}"] = (nb[1] * sz, sz)
+        st[f"b{l}"] = (nb[1] * MID[l], MID[l])
+    x_in = torch.cat([x1[:, :c1].float().cpu().expand(P, -1, -1), x2[:, :, :c2].float().cpu()], dim=2)
+    if mode == "f32":
+        y = torch.zeros(P, rows, 40, device=DEV)
+        st["y"] = (nb[1] * rows * 40, rows * 40)
+        ops.lic_stack(n, G, x1, c1, ld1, packed, bias, MID, y, 40, True, x2=x2 if c2 else None, c2=c2, ld2=ld2,
+                      addend=addd, ld_add=240, nb=nb, strides=st)
+        ref = _ref_stack(x_in, ws, bs, G, addend=add[:, :, :224])
+        got = y[:, :, :32].cpu()
+    else:
+        src = torch.randn(P, rows, 48)
+        y = torch.zeros(P, rows, 48, dtype=torch.bfloat16, device=DEV)
+        y2 = torch.zeros_like(y)
+        st.update({"y": (nb[1] * rows * 48, rows * 48), "src": (nb[1] * rows * 48, rows * 48),
+                   "y2": (nb[1] * rows * 48, rows * 48)})
+        ops.lic_stack(n, G, x1, c1, ld1, packed, bias, MID, y, 48, False, x2=x2 if c2 else None, c2=c2, ld2=ld2,
+                      addend=addd, ld_add=240, lrp_src=src.to(DEV), ld_src=48, y2=y2, ldy2=48, nb=nb, strides=st)
+        ref = _ref_stack(x_in, ws, bs, G, addend=add[:, :, :224], lrp_src=src[:, :, :32])
+        got = y[:, :, :32].float().cpu()
+        assert torch.equal(y, y2)
+        assert float(y[:, :, 32:].float().abs().max()) == 0.0  # nothing outside the 32 output channels
+    torch.cuda.synchronize()
+    err = _maxrel(got, ref)
+    print(f"G={G} cin={c1}+{c2} nb={nb} {mode}: max rel err {err:.2e}")
+    assert err < 2e-2
+
+
+def test_lic_stack_rejects_oversized(tmae):
+    from textmae_amd import ops
+
+    x = torch.zeros(144, 256, dtype=torch.bfloat16, device=DEV)
+    w = [torch.zeros(1, dtype=torch.bfloat16, device=DEV)] * 5
+    b = [torch.zeros(256, device=DEV)] * 5
+    y = torch.zeros(144, 32, device=DEV)
+    with pytest.raises(ValueError, match="input channels"):
+        ops.lic_stack(1, 12, x, 256, 256, w, b, MID, y, 32, True)
+    with pytest.raises(ValueError, match="grid"):
+        ops.lic_stack(1, 13, x, 32, 256, w, b, MID, y, 32, True)
+
+
+def test_mcm_fused_stacks_match_layerwise(tmae):
+    """MCM eval forward, bf16, ViT-B 256^2 K=144 at batch 8: fused slice stacks vs the per-layer launches"""
+    torch.manual_seed(3)
+    m = tmae.MCM(img_size=256, num_keep_patches=144).to(DEV).eval()
+    m.compute_dtype = torch.bfloat16
+    m.distortion = "none"
+    imgs = torch.randn(8, 3, 256, 256, device=DEV)
+    scores = torch.rand(8, 256, device=DEV)
+    outs = {}
+    old = os.environ.get("TMAE_LIC_STACK")
+    try:
+        for flag in ("1", "0"):
+            os.environ["TMAE_LIC_STACK"] = flag
+            m._exec = None
+            with torch.no_grad():
+                o = m(imgs, scores)
+            assert (m._exec.lstk is not None) == (flag == "1")
+            ex = m._exec
+            # MUSIG holds mu / sigma of the batched slices 6..11; YH - YPRE = 0.5 tanh(lrp) of every slice
+            outs[flag] = {"x_hat": o["x_hat"].clone(), "y": o["likelihoods"]["y"].clone(),
+                          "yh": ex.YH.float().clone(), "musig": ex.MUSIG.clone(),
+                          "lrp": (ex.YH.float() - ex.YPRE).clone()}
+    finally:
+        if old is None:
+            os.environ.pop("TMAE_LIC_STACK", None)
+        else:
+            os.environ["TMAE_LIC_STACK"] = old
+        m._exec = None
+    a, b = outs["1"], outs["0"]
+    flips = int(((a["yh"] - b["yh"]).abs() > 0.5).sum())
+    xr = float((a["x_hat"] - b["x_hat"]).norm() / b["x_hat"].norm())
+    ly = (a["y"].double().log() - b["y"].double().log()).abs()
+    print(f"fused vs layerwise: y_hat flips {flips} of {a['yh'].numel()}, x_hat rel L2 {xr:.2e}, "
+          f"log y-lik max diff {float(ly.max()):.2e} mean {float(ly.mean()):.2e}")
+    e_ms, e_lrp = _maxrel(a["musig"], b["musig"]), _maxrel(a["lrp"], b["lrp"])
+    print(f"  mu/sigma (slices 6..11) max rel {e_ms:.2e}; 0.5 tanh(lrp) max rel {e_lrp:.2e}")
+    assert e_ms < 2e-2 and e_lrp < 5e-2
+    assert flips <= 1e-3 * a["yh"].numel()
+    assert xr < 2e-2
+    assert float(ly.mean()) < 2e-2

@@ -62,6 +62,26 @@ class ConvDgradArgs(ctypes.Structure):
     ]
 
 
+LSTK_MAXL = 5
+
+
+class LicStackArgs(ctypes.Structure):
+    """mirror of tmae_lic_stack_args"""
+    _fields_ = [
+        ("n", I), ("G", I), ("nb1", I), ("nb2", I), ("nlayers", I),
+        ("x1", P), ("c1", I), ("ld1", I), ("x1_s", LL * 2),
+        ("x2", P), ("c2", I), ("ld2", I), ("x2_s", LL * 2),
+        ("w", P * LSTK_MAXL), ("w_s", (LL * 2) * LSTK_MAXL),
+        ("bias", P * LSTK_MAXL), ("b_s", (LL * 2) * LSTK_MAXL),
+        ("cout", I * LSTK_MAXL),
+        ("addend", P), ("ld_add", I), ("a_s", LL * 2),
+        ("y", P), ("y_f32", I), ("ldy", I), ("y_s", LL * 2),
+        ("lrp_src", P), ("ld_src", I), ("src_s", LL * 2),
+        ("y2", P), ("ldy2", I), ("y2_s", LL * 2),
+        ("flags", I),
+    ]
+
+
 class EBParams(ctypes.Structure):
     _fields_ = [("matrix", ctypes.c_void_p * 5), ("bias", ctypes.c_void_p * 5), ("factor", ctypes.c_void_p * 4),
                 ("quantiles", ctypes.c_void_p)]
@@ -82,6 +102,7 @@ SIGNATURES = {
     "tmae_decoder_pred_fwd": [P, P, P, P, I, I, I, I, I, I, I, I, P],
     "tmae_decoder_pred_cp_fwd": [P, P, P, P, I, I, I, I, I, I, I, I, P],
     "tmae_conv3x3": [ctypes.POINTER(ConvArgs), I, P],
+    "tmae_lic_stack": [ctypes.POINTER(LicStackArgs), P],
     "tmae_gc_slices_fwd": [P, I, I, P, P, LL, I, P, P, I, P, I, I, P, I, I, I, I, I, P],
     "tmae_eb_likelihood_fwd": [P, ctypes.POINTER(EBParams), P, P, P, I, P, I, I, I, P],
     "tmae_eb_aux_loss": [ctypes.POINTER(EBParams), P, P, P, I, P],

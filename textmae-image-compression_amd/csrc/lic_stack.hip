@@ -1,0 +1,346 @@
+// One whole slice-transform stack per workgroup, activations resident in LDS (bf16).
+//
+// cc_transform_mean[i] / cc_transform_scale[i] / lrp_transform[i] (MCM.py:165-293, applied at
+// MCM.py:761-784) are five 3x3 convs (224 -> 176 -> 128 -> 80 -> 32 channels at the default config)
+// with GELU between them, over the 12x12 latent grid.  Run layer by layer (conv_halo.h) every layer is
+// a separate launch of 64-256 workgroups whose ~0.7 us per (chunk, tap) step chain, not the MFMA rate,
+// sets the time, and the serial slice chain (slices 0..5) is a row of such launches.  Here ONE
+// workgroup owns one (problem, image) and runs the whole stack:
+//   * the layer-0 input (y_hat slices, MCM.py:756-760, torch.cat of two sources without a copy) goes
+//     global -> LDS once; every layer's output stays in LDS (two ping-pong buffers, 144 rows of up to
+//     224 channels each) and is the next layer's input -- no HBM round trip between layers;
+//   * weights never touch LDS: they are pre-packed in MFMA fragment order ([tap][k32][cout16][lane][8])
+//     so every A-fragment is one coalesced 1-KiB wave load from L2 (all images of a problem share them),
+//     prefetched four K-steps ahead into VGPRs; so the K loop has NO workgroup barrier at all, only the
+//     one between layers;
+//   * pixel fragments are 16 consecutive pixels; tap (dy, dx) shifts the LDS row by dy*G + dx, pixels
+//     whose tap falls outside the grid read a zero row.  Row pitch = 2 * round32(C) + 32 bytes, so every
+//     fragment read is bank-conflict-free for every tap shift.
+// Work split: 8 waves (two per SIMD); a wave item = one or two 16-channel output fragments x all 9 pixel
+// fragments (x 5 for the narrow last layers), items dealt round-robin to the waves.
+// MFMA v_mfma_f32_16x16x32_bf16 issued swapped (A = weights 16 couts x 32 k, B = 32 k x 16 pixels):
+// each lane ends with 4 consecutive output channels of one pixel (one 8-B LDS store per fragment).
+// The first layer's epilogue adds the latent-channel partial sums (the P buffer of mcm.py _slices) and
+// the last layer's writes mu / sigma (f32) or, for lrp, y_hat = y_hat_pre + 0.5 tanh(.) (MCM.py:779-784).
+#include "gemm_core.h"
+
+namespace lstk {
+constexpr int NW = 8;                       // waves per workgroup (two per SIMD: 256 VGPRs each)
+constexpr int MAXC = 224;                   // widest resident activation (channels, padded to 32)
+constexpr int MAXPITCH = 2 * MAXC + 32;     // bytes
+constexpr int MAXPIX = 144;                 // 12 x 12
+constexpr int BUF = MAXPIX * MAXPITCH;      // one activation buffer
+constexpr int ZOFF = 2 * BUF;               // zero row
+constexpr int DUMP = 2 * BUF + MAXPITCH;     // 1 KiB landing area of the L2 warm-up DMA (never read)
+constexpr int TMASK = DUMP + 1024;          // per-pixel 9-bit tap-validity masks (u16, 160 pixel slots)
+constexpr int LDS_BYTES = TMASK + 320;
+__host__ __device__ constexpr int pad32(int c) { return (c + 31) & ~31; }
+// row pitch: 32 B past the channels makes every ds_read_b128 fragment read (16 consecutive rows, the
+// gfx950 lane groups {0-3,12-15,20-27} / {4-11,16-19,28-31} mixing two k-chunks) conflict-free for every
+// tap shift; 16 B left them 2-way conflicted
+__host__ __device__ constexpr int pitch(int c) { return 2 * pad32(c) + 32; }
+}  // namespace lstk
+
+struct LstkLayer {
+  const bf16* w;
+  const float* b;
+  int cin, cout;
+};
+
+// per-workgroup outputs of the last layer / the layer-0 addend, problem offsets applied
+struct LstkOut {
+  const float* add;
+  int ld_add;
+  void* y;
+  int ldy, y_f32;
+  const float* src;
+  int ld_src;
+  void* y2;
+  int ldy2;
+};
+
+__device__ __forceinline__ bf16x8 lstk_lds8(const unsigned char* lb, unsigned off) {
+  return *reinterpret_cast<const bf16x8*>(lb + off);
+}
+
+// One wave item: NF output fragments (channels 16 f0 .. 16 (f0 + NF) - 1) x MF pixel fragments
+// j0 .. j0 + MF - 1, NKC = K-steps of 32 input channels per tap.  Every B fragment read from LDS feeds NF
+// MFMAs (at NF = 1 one 1-KiB read per 16-cycle MFMA on each SIMD is exactly the LDS array's 256 B/clk).
+// All 9 x NKC K-steps are unrolled: A fragments stream through a static register ring D steps ahead,
+// B fragments are read one step ahead.
+template <int NF, int MF, int NKC>
+__device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool last, const LstkOut& o, int img,
+                                          int f0, int j0, unsigned char* lb, unsigned in_off, unsigned out_off,
+                                          int npix, int G, int lane) {
+  using namespace lstk;
+  // opaque per item: keeps the per-fragment pixel / address math inside the item (hoisted out of the
+  // layer loop it was ~70 VGPRs of 64-bit epilogue addresses, all spilled)
+  asm volatile("" : "+v"(lane));
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nfr = (L.cout + 15) >> 4;
+  f32x4 acc[NF][MF];
+#pragma unroll
+  for (int i = 0; i < NF; ++i)
+#pragma unroll
+    for (int j = 0; j < MF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if constexpr (NKC > 0) {
+    const int pin = pitch(L.cin);
+    // A fragment of step s = tap * NKC + kc, output fragment f at w + ((s * nfr + f) * 64 + lane) * 8;
+    // fragments past nfr (odd nfr at NF = 2) re-read fragment nfr - 1 and are dropped in the epilogue
+    const bf16* wp[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) wp[i] = L.w + ((size_t)min(f0 + i, nfr - 1) * 64 + lane) * 8;
+    const unsigned sstride = (unsigned)nfr * 512u;
+    // A ring: step s's fragments in slot s % D, the load of step s + D issued right after slot s is read;
+    // all 9 x NKC steps are unrolled so the slots are static registers (a rolled tap loop needed copies
+    // of the in-flight loads at its back edge, i.e. a vmcnt(0) at the end of every tap)
+    constexpr int NS = 9 * NKC, D = NF == 2 ? 4 : 6;
+    bf16x8 ar[D][NF];
+    const bf16* wl[NF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      wl[i] = wp[i];
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        if (d < NS) {
+          ar[d][i] = *reinterpret_cast<const bf16x8*>(wl[i]);
+          wl[i] += sstride;
+        }
+    }
+    // per pixel fragment: bit t set when tap t of this lane's pixel lies inside the grid (table built once
+    // per workgroup in LDS; 0 for pixels past the grid)
+    unsigned tmask[MF];
+#pragma unroll
+    for (int j = 0; j < MF; ++j) tmask[j] = *reinterpret_cast<const unsigned short*>(lb + TMASK + 2 * (16 * (j0 + j) + fr));
+    auto row = [&](int t, int j) -> unsigned {
+      const int p = 16 * (j0 + j) + fr, sh = (t / 3 - 1) * G + (t % 3 - 1);
+      return ((tmask[j] >> t) & 1u ? in_off + (unsigned)((p + sh) * pin) : (unsigned)ZOFF) + 16u * fq;
+    };
+    // B fragments double-buffered: step s+1's reads are issued before step s's MFMAs; the sched barrier
+    // keeps the scheduler from hoisting later steps' reads
+    bf16x8 bv[2][MF];
+#pragma unroll
+    for (int j = 0; j < MF; ++j) bv[0][j] = lstk_lds8(lb, row(0, j));
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s + 1 < NS) {
+        const int t1 = (s + 1) / NKC, k1 = (s + 1) - t1 * NKC;
+#pragma unroll
+        for (int j = 0; j < MF; ++j) bv[(s + 1) & 1][j] = lstk_lds8(lb, row(t1, j) + 64u * k1);
+      }
+      bf16x8 a0[NF];
+#pragma unroll
+      for (int i = 0; i < NF; ++i) {
+        a0[i] = ar[s % D][i];
+        if (s + D < NS) {
+          ar[s % D][i] = *reinterpret_cast<const bf16x8*>(wl[i]);
+          wl[i] += sstride;  // one pointer bump per load (per-step constant offsets spilled ~280 SGPRs)
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < MF; ++j)
+#pragma unroll
+        for (int i = 0; i < NF; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], bv[s & 1][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+
+  // epilogue: lane holds channels c..c+3 of pixel 16 (j0 + j) + fr
+  const int pout = pitch(L.cout);
+#pragma unroll
+  for (int i = 0; i < NF; ++i) {
+    const int c = 16 * (f0 + i) + 4 * fq;
+    if (c >= L.cout) continue;
+    const f32x4 bias = load4f(L.b + c);
+#pragma unroll
+    for (int j = 0; j < MF; ++j) {
+      const int p = 16 * (j0 + j) + fr;
+      if (p >= npix) continue;
+      const size_t row = (size_t)img * npix + p;
+      f32x4 v = acc[i][j] + bias;
+      if (first && o.add) v += load4f(o.add + row * o.ld_add + c);
+      if (!last) {
+        const f32x2 lo = gelu2_bf16out(v.xy), hi = gelu2_bf16out(v.zw);
+        bf16x4 q;
+        q[0] = (bf16)lo.x; q[1] = (bf16)lo.y; q[2] = (bf16)hi.x; q[3] = (bf16)hi.y;
+        *reinterpret_cast<bf16x4*>(lb + out_off + p * pout + 2 * c) = q;
+      } else if (o.src) {  // lrp: y_hat = y_hat_pre + 0.5 tanh(lrp)
+        f32x4 r = load4f(o.src + row * o.ld_src + c);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) r[e] += 0.5f * tanhf(v[e]);
+        store4(reinterpret_cast<bf16*>(o.y) + row * o.ldy + c, r);
+        if (o.y2) store4(reinterpret_cast<bf16*>(o.y2) + row * o.ldy2 + c, r);
+      } else if (o.y_f32) {
+        store4(reinterpret_cast<float*>(o.y) + row * o.ldy + c, v);
+      } else {
+        store4(reinterpret_cast<bf16*>(o.y) + row * o.ldy + c, v);
+      }
+    }
+  }
+}
+
+template <int NF, int MF>
+__device__ __forceinline__ void lstk_dispatch(int nkc, const LstkLayer& L, bool first, bool last, const LstkOut& o,
+                                              int img, int f0, int j0, unsigned char* lb, unsigned in_off,
+                                              unsigned out_off, int npix, int G, int lane) {
+#define LSTK_CASE(K) \
+  case K: lstk_item<NF, MF, K>(L, first, last, o, img, f0, j0, lb, in_off, out_off, npix, G, lane); break;
+  switch (nkc) {
+    LSTK_CASE(0) LSTK_CASE(1) LSTK_CASE(2) LSTK_CASE(3) LSTK_CASE(4) LSTK_CASE(5) LSTK_CASE(6) LSTK_CASE(7)
+    default: break;
+  }
+#undef LSTK_CASE
+}
+
+// the argument block is read in place from the kernarg segment (scalar loads, layer fields indexed at
+// run time): a by-value copy indexed by the layer number would live in scratch
+typedef const __attribute__((address_space(4))) tmae_lic_stack_args LstkArgs;
+
+__global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack_args) {
+  using namespace lstk;
+  LstkArgs* a = (LstkArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+  __shared__ __attribute__((aligned(16))) uint4 lds[LDS_BYTES / 16];
+  unsigned char* lb = reinterpret_cast<unsigned char*>(lds);
+  const int n = a->n, G = a->G, npix = G * G, nmf = (npix + 15) >> 4, nb2 = a->nb2;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);  // each XCD's L2 serves a contiguous run of problems
+  const int prob = t / n, img = t - prob * n;
+  const long long b1 = prob / nb2, b2 = prob - (prob / nb2) * nb2;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // zero row + layer-0 input -> buffer 0 (channels [0, c1) from x1, [c1, cin0) from x2, pad zeros)
+  for (int i = tid; i < MAXPITCH / 16; i += NW * 64) reinterpret_cast<uint4*>(lds)[ZOFF / 16 + i] = uint4{0, 0, 0, 0};
+  for (int p = tid; p < 160; p += NW * 64) {
+    unsigned m = 0;
+    if (p < npix) {
+      const int py = p / G, px = p - py * G;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int yy = py + t / 3 - 1, xx = px + t % 3 - 1;
+        m |= ((unsigned)yy < (unsigned)G && (unsigned)xx < (unsigned)G) ? (1u << t) : 0u;
+      }
+    }
+    *reinterpret_cast<unsigned short*>(lb + TMASK + 2 * p) = (unsigned short)m;
+  }
+  const int c1 = a->c1, cin0 = a->c1 + a->c2;
+  const int nl = a->nlayers;
+  const int pol = a->flags & 2;  // experiment knob: item policy B
+  if (a->flags & TMAE_LIC_STACK_WARM_L2) {
+    // L2 warm-up: the workgroups of one XCD (a contiguous run of t, one problem) each touch 1/16 of the
+    // problem's packed weights up front (LDS-DMA into a dump area: no registers, many in flight), so the
+    // per-tap A-fragment loads hit L2 instead of each paying a miss one tap ahead
+    const unsigned dump = (unsigned)(size_t)(lds_void_t*)lds + DUMP;
+    const long long part = t & 15;
+    int ci = cin0;
+    for (int l = 0; l < nl; ++l) {
+      const int co = a->cout[l];
+      const long long nchunk = 9LL * (pad32(ci) >> 5) * ((co + 15) >> 4) * 64;  // 16-B pieces
+      const char* w = reinterpret_cast<const char*>(a->w[l]) + 2 * (b1 * a->w_s[l][0] + b2 * a->w_s[l][1]);
+      for (long long c = (part * NW + wave) * 64 + lane; c < nchunk; c += 16LL * NW * 64) glds16(w + 16 * c, dump);
+      ci = co;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  {
+    const bf16* x1 = reinterpret_cast<const bf16*>(a->x1) + b1 * a->x1_s[0] + b2 * a->x1_s[1];
+    const bf16* x2 = a->x2 ? reinterpret_cast<const bf16*>(a->x2) + b1 * a->x2_s[0] + b2 * a->x2_s[1] : nullptr;
+    const int ld1 = a->ld1, ld2 = a->ld2;
+    const int q = pad32(cin0) >> 3, pin = pitch(cin0);
+    for (int i = tid; i < npix * q; i += NW * 64) {
+      const int p = i / q, ch = 8 * (i - p * q);
+      const size_t row = (size_t)img * npix + p;
+      uint4 v = uint4{0, 0, 0, 0};
+      if (ch < c1) v = *reinterpret_cast<const uint4*>(x1 + row * ld1 + ch);
+      else if (ch < cin0) v = *reinterpret_cast<const uint4*>(x2 + row * ld2 + (ch - c1));
+      *reinterpret_cast<uint4*>(lb + p * pin + 2 * ch) = v;
+    }
+  }
+  __syncthreads();
+
+  LstkOut o;
+  o.add = a->addend ? a->addend + b1 * a->a_s[0] + b2 * a->a_s[1] : nullptr;
+  o.ld_add = a->ld_add;
+  o.y_f32 = a->y_f32;
+  o.y = o.y_f32 ? (void*)(reinterpret_cast<float*>(a->y) + b1 * a->y_s[0] + b2 * a->y_s[1])
+                : (void*)(reinterpret_cast<bf16*>(a->y) + b1 * a->y_s[0] + b2 * a->y_s[1]);
+  o.ldy = a->ldy;
+  o.src = a->lrp_src ? a->lrp_src + b1 * a->src_s[0] + b2 * a->src_s[1] : nullptr;
+  o.ld_src = a->ld_src;
+  o.y2 = a->y2 ? (void*)(reinterpret_cast<bf16*>(a->y2) + b1 * a->y2_s[0] + b2 * a->y2_s[1]) : nullptr;
+  o.ldy2 = a->ldy2;
+
+  int cin = cin0;
+  for (int l = 0; l < nl; ++l) {
+    LstkLayer L;
+    L.w = reinterpret_cast<const bf16*>(a->w[l]) + b1 * a->w_s[l][0] + b2 * a->w_s[l][1];
+    L.b = a->bias[l] + b1 * a->b_s[l][0] + b2 * a->b_s[l][1];
+    L.cin = cin;
+    L.cout = a->cout[l];
+    const bool first = l == 0, last = l + 1 == nl;
+    const unsigned in_off = (l & 1) ? (unsigned)BUF : 0u, out_off = (l & 1) ? 0u : (unsigned)BUF;
+    const int nfr = (L.cout + 15) >> 4;
+    const int nkc = pad32(L.cin) >> 5;
+    // wave items (each A fragment is loaded by ONE wave unless the pixel set is split):
+    //   >= 12 output fragments (224): two fragments x all pixel fragments (B reads shared by both);
+    //   8..11 (176, 128): one fragment x all pixel fragments (enough items for two per SIMD);
+    //   < 8 (80, 32): one fragment x half the pixel fragments (more items for the waves)
+    if (pol && nfr >= 8) {  // policy B: fragment pairs x pixel halves for every wide layer
+      const int nh = (nmf + 4) / 5, ng = (nfr + 1) >> 1;
+      for (int it = wave; it < ng * nh; it += NW) {
+        const int g = it / nh, h = it - g * nh;
+        lstk_dispatch<2, 5>(nkc, L, first, last, o, img, 2 * g, 5 * h, lb, in_off, out_off, npix, G, lane);
+      }
+    } else if (nfr >= 12) {
+      for (int it = wave; it < (nfr + 1) >> 1; it += NW)
+        lstk_dispatch<2, 9>(nkc, L, first, last, o, img, 2 * it, 0, lb, in_off, out_off, npix, G, lane);
+    } else if (nfr >= 8) {
+      for (int it = wave; it < nfr; it += NW)
+        lstk_dispatch<1, 9>(nkc, L, first, last, o, img, it, 0, lb, in_off, out_off, npix, G, lane);
+    } else {
+      const int nh = (nmf + 4) / 5;
+      for (int it = wave; it < nfr * nh; it += NW) {
+        const int g = it / nh, h = it - g * nh;
+        lstk_dispatch<1, 5>(nkc, L, first, last, o, img, g, 5 * h, lb, in_off, out_off, npix, G, lane);
+      }
+    }
+    if (!last) {
+      // zero the channel padding [cout, pad32(cout)) the next layer's 32-wide K steps read
+      const int cp = pad32(L.cout), pz = pitch(L.cout);
+      const int q = (cp - L.cout) >> 3;  // 16-B pieces per row (cout is a multiple of 8)
+      if (q > 0)
+        for (int i = tid; i < npix * q; i += NW * 64) {
+          const int p = i / q, ch = L.cout + 8 * (i - p * q);
+          *reinterpret_cast<uint4*>(lb + out_off + p * pz + 2 * ch) = uint4{0, 0, 0, 0};
+        }
+    }
+    cin = L.cout;
+    __syncthreads();
+  }
+}
+
+extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
+  using namespace lstk;
+  TMAE_REQUIRE(args != nullptr, "tmae_lic_stack: args is NULL");
+  const tmae_lic_stack_args& a = *args;
+  TMAE_REQUIRE(a.G >= 1 && a.G * a.G <= MAXPIX, "tmae_lic_stack: grid %dx%d exceeds %d pixels", a.G, a.G, MAXPIX);
+  TMAE_REQUIRE(a.nlayers >= 1 && a.nlayers <= TMAE_LIC_STACK_MAXL, "tmae_lic_stack: %d layers", a.nlayers);
+  TMAE_REQUIRE(a.nb1 >= 1 && a.nb2 >= 1 && a.n >= 1, "tmae_lic_stack: batch %d x %d, n %d", a.nb1, a.nb2, a.n);
+  TMAE_REQUIRE(a.x1 != nullptr && a.y != nullptr, "tmae_lic_stack: x1 / y required");
+  TMAE_REQUIRE(a.c1 >= 0 && a.c2 >= 0 && (a.c2 == 0 || a.x2 != nullptr), "tmae_lic_stack: channels %d + %d", a.c1, a.c2);
+  TMAE_REQUIRE(a.c1 % 8 == 0 && a.c2 % 8 == 0 && a.ld1 % 8 == 0 && (a.c2 == 0 || a.ld2 % 8 == 0),
+               "tmae_lic_stack: input channels / strides must be multiples of 8");
+  TMAE_REQUIRE(pad32(a.c1 + a.c2) <= MAXC, "tmae_lic_stack: %d input channels exceed %d", a.c1 + a.c2, MAXC);
+  for (int l = 0; l < a.nlayers; ++l) {
+    TMAE_REQUIRE((a.w[l] != nullptr || (l == 0 && a.c1 + a.c2 == 0)) && a.bias[l] != nullptr,
+                 "tmae_lic_stack: layer %d weights", l);
+    TMAE_REQUIRE(a.cout[l] >= 4 && a.cout[l] % 8 == 0, "tmae_lic_stack: layer %d cout %d (multiple of 8)", l, a.cout[l]);
+    TMAE_REQUIRE(l + 1 == a.nlayers || pad32(a.cout[l]) <= MAXC, "tmae_lic_stack: layer %d cout %d exceeds %d", l,
+                 a.cout[l], MAXC);
+  }
+  TMAE_REQUIRE(!a.lrp_src || !a.y_f32, "tmae_lic_stack: lrp output is bf16");
+  if (a.addend) TMAE_REQUIRE(a.ld_add % 4 == 0, "tmae_lic_stack: addend stride %d", a.ld_add);
+  const int nwg = a.n * a.nb1 * a.nb2;
+  hipLaunchKernelGGL(lic_stack_kernel, dim3(nwg), dim3(NW * 64), 0, (hipStream_t)stream, a);
+  TMAE_LAUNCH_CHECK("tmae_lic_stack");
+}

@@ -468,6 +468,30 @@ class _Executor:
                             torch.stack([lrp[i][0].bias for i in bs]).detach().contiguous())
         self.b_lrp_layers = [(cast(torch.stack([cw(lrp[i][j].weight) for i in bs])),
                               torch.stack([lrp[i][j].bias for i in bs]).detach().contiguous()) for j in range(1, 5)]
+        # fused slice-transform stacks (lic_stack.hip): every layer packed in MFMA fragment order, problems
+        # stacked like the per-layer launches above; bf16 only, shapes that fit one workgroup's LDS
+        self.lstk = None
+        if (dt == torch.bfloat16 and os.environ.get("TMAE_LIC_STACK", "1") != "0" and sw % 8 == 0
+                and ops.lic_stack_fits(self.g, sw * (ms + 1), self.mid)):
+            pk = ops.pack_lic_stack_weight
+
+            def packs(convs, lo=None, hi=None):  # [layer] -> packed weights of one stack
+                return [pk(c.weight[:, lo:hi] if j == 0 else c.weight) for j, c in enumerate(convs)]
+
+            def stk(ts):  # stack problems' packed weights per layer
+                return [torch.stack(list(layer)).contiguous() for layer in zip(*ts)]
+
+            L = {"ms": [], "lrp": []}
+            for i in range(ms):
+                ny = sw * i
+                L["ms"].append(stk([packs(mean[i], M, M + ny), packs(scale[i], M, M + ny)]))
+                L["lrp"].append(packs(lrp[i], M, M + ny + sw))
+            if S > ms:
+                ny = sw * ms
+                L["b_ms"] = [torch.stack([a_, b_]).contiguous() for a_, b_ in
+                             zip(stk([packs(mean[i], M, M + ny) for i in bs]), stk([packs(scale[i], M, M + ny) for i in bs]))]
+                L["b_lrp"] = stk([packs(lrp[i], M, M + ny + sw) for i in bs])
+            self.lstk = L
         self.w_de = cast(m.decoder_embed.weight)
         # decoder_pred rows in channel-planar order: the unpatchify epilogue stores whole pixel runs
         pp = m.encoder_embed.patch_size[0]
@@ -756,6 +780,37 @@ class _Executor:
                             strides={"x1": (cm_s1[j], Mp * cin), "w": (w[0].numel(), w[0][0].numel() if nbs > 1 else 0),
                                      "b": (b[0].numel(), cout if nbs > 1 else 0), "y": (ys1, Mp * cout)})
 
+        def ms_fused(i0, nbs):
+            """mean+scale stacks of slices i0.. as ONE tmae_lic_stack launch (2 x nbs problems) -> MUSIG"""
+            ws = self.lstk["b_ms"] if nbs > 1 else self.lstk["ms"][i0]
+            first, layers = (self.b_ms_first, self.b_ms_layers) if nbs > 1 else (self.ms_first[i0], self.ms_layers[i0])
+            bs_ = [first[1]] + [b for _, b in layers]
+            st = {"a": (off_scale - off_mean, c0), "y": (ms_s1, Mp * sw)}
+            for l, (w, b) in enumerate(zip(ws, bs_)):
+                st[f"w{l}"] = (w[0].numel(), w[0][0].numel() if nbs > 1 else 0)
+                st[f"b{l}"] = (b[0].numel(), b.shape[-1] if nbs > 1 else 0)
+            ops.lic_stack(B, g, supy, sw * (ms if nbs > 1 else i0), M, ws, bs_, mid, musig, sw, True,
+                          addend=pbase + (off_mean + i0 * c0) * eP, ld_add=Pw, nb=(2, nbs), strides=st)
+
+        def lrp_fused(i0, nbs):
+            """lrp stack(s) of slices i0.. as one tmae_lic_stack launch: y_hat = y_hat_pre + 0.5 tanh(lrp) -> YH"""
+            ws = self.lstk["b_lrp"] if nbs > 1 else self.lstk["lrp"][i0]
+            first, layers = (self.b_lrp_first, self.b_lrp_layers) if nbs > 1 else (self.lrp_first[i0], self.lrp_layers[i0])
+            bs_ = [first[1]] + [b for _, b in layers]
+            st = {"a": (0, c0), "y": (0, sw), "src": (0, sw), "x2": (0, sw)}
+            for l, (w, b) in enumerate(zip(ws, bs_)):
+                st[f"w{l}"] = (0, w[0].numel() if nbs > 1 else 0)
+                st[f"b{l}"] = (0, b.shape[-1] if nbs > 1 else 0)
+            if nbs > 1:  # shared slots 0..ms-1 + own pre-LRP slot
+                x = dict(x2=supy + ms * sw * esz, c2=sw, ld2=M)
+                c1 = sw * ms
+            else:        # y_hat slots 0..i0 (contiguous); also the support slot
+                x = dict(y2=supy + i0 * sw * esz, ldy2=M)
+                c1 = sw * (i0 + 1)
+            ops.lic_stack(B, g, supy, c1, M, ws, bs_, mid, yh + i0 * sw * esz, M, False,
+                          addend=pbase + (off_lrp + i0 * c0) * eP, ld_add=Pw, lrp_src=ypre + i0 * sw * e4, ld_src=M,
+                          nb=(1, nbs), strides=st, **x)
+
         def lrp_stack(first, layers, i0, nbs, x2=None):
             w, b = first
             if x2 is None:  # single slice i0: input = y_hat slots 0..i0 (contiguous)
@@ -781,16 +836,29 @@ class _Executor:
                                          "y2": (0, sw)})
 
         # slices 0..ms-1: serial (slice i conditions on y_hat 0..i-1)
+        fused = self.lstk is not None
         for i in range(ms):
             wait_pre(i)
-            ms_stack(self.ms_first[i], self.ms_layers[i], supy, sw * i, i, 1)
+            if fused:
+                ms_fused(i, 1)
+            else:
+                ms_stack(self.ms_first[i], self.ms_layers[i], supy, sw * i, i, 1)
             gc_step(i, 1, musig, musig + ms_s1 * e4, Mp * sw)
-            lrp_stack(self.lrp_first[i], self.lrp_layers[i], i, 1)
+            if fused:
+                lrp_fused(i, 1)
+            else:
+                lrp_stack(self.lrp_first[i], self.lrp_layers[i], i, 1)
         # slices ms..S-1: batched on the fixed support y_hat 0..ms-1
         if nb > 0:
             wait_pre(ms)
-            ms_stack(self.b_ms_first, self.b_ms_layers, supy, sw * ms, ms, nb)
+            if fused:
+                ms_fused(ms, nb)
+            else:
+                ms_stack(self.b_ms_first, self.b_ms_layers, supy, sw * ms, ms, nb)
             gc_step(ms, nb, musig, musig + ms_s1 * e4, Mp * sw)
-            lrp_stack(self.b_lrp_first, self.b_lrp_layers, ms, nb, x2=supy + ms * sw * esz)
+            if fused:
+                lrp_fused(ms, nb)
+            else:
+                lrp_stack(self.b_lrp_first, self.b_lrp_layers, ms, nb, x2=supy + ms * sw * esz)
         for k in list(ready):  # join the side stream in every case
             wait_pre(k)

@@ -7,15 +7,16 @@ the library never allocates) unless an `out=` buffer is passed.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
 from . import _lib
-from ._lib import ACT_GELU, ACT_NONE, TMAE_BF16, TMAE_F32, ConvArgs, EBParams
+from ._lib import ACT_GELU, ACT_NONE, TMAE_BF16, TMAE_F32, ConvArgs, EBParams, LicStackArgs
 
 __all__ = [
     "ids_shuffle", "layernorm", "linear", "linear_residual", "patch_embed", "cls_rows", "mha", "decoder_embed",
-    "mask_rows", "decoder_pred", "conv3x3", "gc_slices", "eb_likelihood", "eb_aux_loss",
+    "mask_rows", "decoder_pred", "conv3x3", "lic_stack", "pack_lic_stack_weight", "lic_stack_fits", "gc_slices", "eb_likelihood", "eb_aux_loss",
     "gc_likelihood", "nhwc_to_nchw", "bpp", "gemm_plan", "dtype_code", "gc_slices_code", "gc_indexes",
     "gc_dequantize", "gc_pmf", "eb_pmf", "eb_symbols", "eb_dequantize", "invert_permutation", "mae_masking",
     "mae_loss", "TMAE_F32", "TMAE_BF16", "ACT_NONE", "ACT_GELU",
@@ -186,6 +187,61 @@ def conv3x3(x1, c1, ld1, n, H, W, w, b, y, ldy, cout, dtype, stride=1, act=ACT_N
         setattr(a, f"{name}_s1", s1)
         setattr(a, f"{name}_s2", s2)
     _lib.call("tmae_conv3x3", ctypes.byref(a), dtype_code(dtype), _stream())
+
+
+LSTK_MAXC, LSTK_MAXPIX = 224, 144  # lic_stack.hip: widest resident activation, pixels per workgroup
+LSTK_FLAGS = int(os.environ.get("TMAE_LSTK_FLAGS", "1"))  # bit 0: L2 warm-up of the stack's weights
+
+
+def _pad(c, m):
+    return (c + m - 1) // m * m
+
+
+def lic_stack_fits(G, cin0, couts):
+    """True when tmae_lic_stack takes a stack of this shape (grid G x G, layer-0 input cin0 channels,
+    output channels per layer): bf16 operands, activations resident in one workgroup's LDS"""
+    return (G * G <= LSTK_MAXPIX and cin0 % 8 == 0 and _pad(cin0, 32) <= LSTK_MAXC and 1 <= len(couts) <= 5
+            and all(c % 8 == 0 for c in couts) and all(_pad(c, 32) <= LSTK_MAXC for c in couts[:-1]))
+
+
+def pack_lic_stack_weight(w: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    """Conv weight [Cout][Cin][3][3] -> tmae_lic_stack's MFMA fragment order
+    [tap 9][k-step Cin/32][cout fragment Cout/16][lane 64][8] (lane = 16 * k-group + cout row), zero-padded
+    to multiples of 32 input / 16 output channels (flat, `dtype`)"""
+    w = w.detach()
+    co, ci = w.shape[:2]
+    cip, cop = _pad(ci, 32), _pad(co, 16)
+    t = torch.zeros(9, cop, cip, dtype=torch.float32, device=w.device)
+    if ci:
+        t[:, :co, :ci] = w.float().permute(2, 3, 0, 1).reshape(9, co, ci)
+    nkc, nfr = cip // 32, cop // 16
+    t = t.view(9, nfr, 16, nkc, 4, 8).permute(0, 3, 1, 4, 2, 5).contiguous()
+    return t.view(-1).to(dtype)
+
+
+def lic_stack(n, G, x1, c1, ld1, weights, biases, couts, y, ldy, y_f32, x2=None, c2=0, ld2=0, addend=None, ld_add=0,
+              lrp_src=None, ld_src=0, y2=None, ldy2=0, nb=(1, 1), strides=None):
+    """One slice-transform stack per (problem, image) (tmae_lic_stack).  weights: packed per layer
+    (pack_lic_stack_weight, problems stacked); `strides` maps operand (x1, x2, w0..w4, b0..b4, a, y, src, y2)
+    -> (s1, s2) element strides of the nb[0] x nb[1] problems.  Pointers: tensors or raw addresses."""
+    a = LicStackArgs()
+    a.n, a.G, a.nlayers = n, G, len(couts)
+    a.nb1, a.nb2 = nb
+    a.x1, a.c1, a.ld1 = _p(x1), c1, ld1
+    a.x2, a.c2, a.ld2 = _p(x2), c2, ld2
+    for l, (w, b, c) in enumerate(zip(weights, biases, couts)):
+        a.w[l], a.bias[l], a.cout[l] = _p(w), _p(b), c
+    a.addend, a.ld_add = _p(addend), ld_add
+    a.y, a.y_f32, a.ldy = _p(y), int(y_f32), ldy
+    a.lrp_src, a.ld_src = _p(lrp_src), ld_src
+    a.y2, a.ldy2 = _p(y2), ldy2
+    a.flags = LSTK_FLAGS
+    for name, (s1, s2) in (strides or {}).items():
+        if name[0] in "wb" and name[1:].isdigit():
+            getattr(a, f"{name[0]}_s")[int(name[1:])][:] = (s1, s2)
+        else:
+            getattr(a, f"{name}_s")[:] = (s1, s2)
+    _lib.call("tmae_lic_stack", ctypes.byref(a), _stream())
 
 
 def gc_slices(y, ldy, yoff, mu, sigma, ms_stride, ld_ms, noise, lik, Mtot, yhat, yhat_dtype, ld_yhat, yhat32, ld32, n,
