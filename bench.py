@@ -142,6 +142,7 @@ class LaunchTimer:
         self.Te, self.Td = m.num_keep_patches + 1, m.encoder_embed.num_patches + 1
         self.calls = []
         self.conv_bytes = 0
+        self.stack_bytes = 0
 
     def classify(self, name, a):
         B, E, Dd, Te, Td = self.B, self.E, self.Dd, self.Te, self.Td
@@ -171,6 +172,16 @@ class LaunchTimer:
             self.conv_bytes += nb * (c.n * c.H * c.W * cin * es + c.cout * 9 * cin * es
                                      + c.n * Ho * Wo * c.cout * ((4 if c.y_f32 else 2) + (4 if c.addend else 0)))
             return "lic_conv3x3", 2.0 * nb * c.n * Ho * Wo * c.cout * 9 * cin
+        if name == "tmae_lic_stack":
+            c = a[0]._obj
+            P, px = c.nb1 * c.nb2, c.n * c.G * c.G
+            ch = [c.c1 + c.c2] + [c.cout[l] for l in range(c.nlayers)]
+            fl = 2.0 * P * px * 9 * sum(ch[l] * ch[l + 1] for l in range(c.nlayers))
+            # algorithmic bytes: layer-0 input, every layer's weights, the addend, the output (+ lrp source)
+            self.stack_bytes += P * (px * ch[0] * 2 + sum(9 * ch[l] * ch[l + 1] * 2 for l in range(c.nlayers))
+                                     + (px * ch[1] * 4 if c.addend else 0)
+                                     + px * ch[-1] * ((4 if c.y_f32 else 2) + (4 if c.lrp_src else 0)))
+            return "lic_stack", fl
         if name == "tmae_patch_embed_fwd":
             return "patch_embed", 2.0 * a[6] * a[13] * a[11] * a[7] * a[10] * a[10]
         if name == "tmae_decoder_embed_fwd":
@@ -189,6 +200,10 @@ class LaunchTimer:
             return {"M": a[6], "N": a[7], "K": a[8]}
         if name == "tmae_mha_fwd":
             return {"B": a[2], "T": a[3], "H": a[4], "dh": a[5]}
+        if name == "tmae_lic_stack":
+            c = a[0]._obj
+            return {"n": c.n, "G": c.G, "cin": c.c1 + c.c2, "couts": [c.cout[l] for l in range(c.nlayers)],
+                    "problems": c.nb1 * c.nb2, "addend": bool(c.addend), "lrp": bool(c.lrp_src)}
         if name == "tmae_conv3x3":
             c = a[0]._obj
             return {"n": c.n, "H": c.H, "W": c.W, "cin": c.c1 + c.c2, "cout": c.cout, "problems": c.nb1 * c.nb2,
@@ -249,7 +264,7 @@ def roofline_report(m, imgs, scores, batch, dump=None):
             json.dump({"batch": batch, "launches": rows}, fh, indent=0)
     mf = {k: v for k, v in fam.items() if v[2] > 0}
     agg = {"token_gemm": [k for k in mf if k.split("_")[-1] in ("qkv", "proj", "fc1", "fc2")],
-           "lic_conv3x3": ["lic_conv3x3"]}
+           "lic_conv3x3": ["lic_conv3x3"], "lic_3x3_all": ["lic_conv3x3", "lic_stack"]}
 
     def stat(keys):
         n = sum(fam[k][0] for k in keys if k in fam)
@@ -263,8 +278,11 @@ def roofline_report(m, imgs, scores, batch, dump=None):
     total_t = sum(v[1] for v in fam.values())  # replayed families only (entropy models / ids excluded)
     dom = max(fam, key=lambda k: fam[k][1] if fam[k][2] > 0 else -1)
     d = stat([dom])
-    roof = {"kernel": dom + (" (conv_halo_kernel + conv-source GEMM tiles, every 3x3 conv of h_a / h_s / "
-                             "cc_transform / lrp_transform)" if dom == "lic_conv3x3" else ""),
+    desc = {"lic_conv3x3": " (conv_halo_kernel + conv-source GEMM tiles: h_a / h_s and the slice stacks' "
+                           "latent-channel partial sums)",
+            "lic_stack": " (lic_stack_kernel: whole cc_transform_mean/scale and lrp_transform stacks, one "
+                         "workgroup per problem x image)"}
+    roof = {"kernel": dom + desc.get(dom, ""),
             "bound": "mfma", "achieved": d["achieved"], "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
             "frac": d["frac"], "traffic": None, "launches_per_step": d["launches"],
             "avg_launch_us": round(d["time_us"] / max(d["launches"], 1), 2),
@@ -276,8 +294,9 @@ def roofline_report(m, imgs, scores, batch, dump=None):
         roof[f"attention_core_{side}"] = stat([f"{side}_attn_core"])
     roof["families"] = per
     roof["aggregates"] = {k: stat(v) for k, v in agg.items()}
-    if dom == "lic_conv3x3":
-        roof["algorithmic_bytes_per_launch"] = int(lt.conv_bytes / max(d["launches"], 1))
+    if dom in ("lic_conv3x3", "lic_stack"):
+        roof["algorithmic_bytes_per_launch"] = int((lt.conv_bytes if dom == "lic_conv3x3" else lt.stack_bytes)
+                                                   / max(d["launches"], 1))
     pmc = os.path.join(ROOT, "profiles", "r02", "pmc_dominant.json")
     if os.path.exists(pmc):
         try:

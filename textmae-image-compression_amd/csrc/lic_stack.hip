@@ -30,8 +30,8 @@ constexpr int MAXC = 224;                   // widest resident activation (chann
 constexpr int MAXPITCH = 2 * MAXC + 32;     // bytes
 constexpr int MAXPIX = 144;                 // 12 x 12
 constexpr int BUF = MAXPIX * MAXPITCH;      // one activation buffer
-constexpr int ZOFF = 2 * BUF;               // zero row
-constexpr int DUMP = 2 * BUF + MAXPITCH;     // 1 KiB landing area of the L2 warm-up DMA (never read)
+constexpr int ZOFF = 2 * BUF;               // zero block: 16 rows, read by taps that fall outside the grid
+constexpr int DUMP = 2 * BUF + 16 * MAXPITCH;  // 1 KiB landing area of the L2 warm-up DMA (never read)
 constexpr int TMASK = DUMP + 1024;          // per-pixel 9-bit tap-validity masks (u16, 160 pixel slots)
 constexpr int LDS_BYTES = TMASK + 320;
 __host__ __device__ constexpr int pad32(int c) { return (c + 31) & ~31; }
@@ -59,8 +59,19 @@ struct LstkOut {
   int ldy2;
 };
 
+#ifndef LSTK_DIAG
+#define LSTK_DIAG 0  // phase isolation builds (tools/lstk_diag.sh): 4 = no MFMA, 8 = no B reads, 16 = no A loads,
+                     // 32 = no epilogue
+#endif
+
 __device__ __forceinline__ bf16x8 lstk_lds8(const unsigned char* lb, unsigned off) {
+#if LSTK_DIAG & 8
+  bf16x8 v;
+  asm volatile("; no B read %0" : "=v"(v) : "v"(off));
+  return v;
+#else
   return *reinterpret_cast<const bf16x8*>(lb + off);
+#endif
 }
 
 // One wave item: NF output fragments (channels 16 f0 .. 16 (f0 + NF) - 1) x MF pixel fragments
@@ -115,7 +126,10 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
     for (int j = 0; j < MF; ++j) tmask[j] = *reinterpret_cast<const unsigned short*>(lb + TMASK + 2 * (16 * (j0 + j) + fr));
     auto row = [&](int t, int j) -> unsigned {
       const int p = 16 * (j0 + j) + fr, sh = (t / 3 - 1) * G + (t % 3 - 1);
-      return ((tmask[j] >> t) & 1u ? in_off + (unsigned)((p + sh) * pin) : (unsigned)ZOFF) + 16u * fq;
+      // an outside tap reads zero row (p + sh) mod 16 of the zero block: the same bank quad as an inside
+      // row would give, so border fragments stay conflict-free
+      const unsigned r = (unsigned)(p + sh);
+      return ((tmask[j] >> t) & 1u ? in_off + r * pin : (unsigned)ZOFF + (r & 15u) * pin) + 16u * fq;
     };
     // B fragments double-buffered: step s+1's reads are issued before step s's MFMAs; the sched barrier
     // keeps the scheduler from hoisting later steps' reads
@@ -133,51 +147,102 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
 #pragma unroll
       for (int i = 0; i < NF; ++i) {
         a0[i] = ar[s % D][i];
-        if (s + D < NS) {
+        if (s + D < NS && !(LSTK_DIAG & 16)) {
           ar[s % D][i] = *reinterpret_cast<const bf16x8*>(wl[i]);
           wl[i] += sstride;  // one pointer bump per load (per-step constant offsets spilled ~280 SGPRs)
         }
       }
+#if LSTK_DIAG & 4  // phase isolation: no MFMA (operands consumed by an empty asm)
+#pragma unroll
+      for (int j = 0; j < MF; ++j) asm volatile("" ::"v"(bv[s & 1][j]));
+#pragma unroll
+      for (int i = 0; i < NF; ++i) asm volatile("" ::"v"(a0[i]));
+#else
 #pragma unroll
       for (int j = 0; j < MF; ++j)
 #pragma unroll
         for (int i = 0; i < NF; ++i)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], bv[s & 1][j], acc[i][j], 0, 0, 0);
+#endif
       __builtin_amdgcn_sched_barrier(0);
     }
   }
 
   // epilogue: lane holds channels c..c+3 of pixel 16 (j0 + j) + fr
+#if LSTK_DIAG & 32  // phase isolation: no epilogue (keep the accumulators alive)
+#pragma unroll
+  for (int i = 0; i < NF; ++i)
+#pragma unroll
+    for (int j = 0; j < MF; ++j) asm volatile("" ::"v"(acc[i][j]));
+  return;
+#endif
+  // Every global operand of the epilogue (the layer-0 addend, the lrp source) is loaded for all
+  // fragments first, then the math runs: fetched per fragment, each load was its own exposed round trip
+  // (vmcnt(0) per fragment).  Lanes past cout / npix use a clamped address and drop their result.
   const int pout = pitch(L.cout);
+  int cc[NF];
+  bool okc[NF];
+  f32x4 bias[NF];
 #pragma unroll
   for (int i = 0; i < NF; ++i) {
-    const int c = 16 * (f0 + i) + 4 * fq;
-    if (c >= L.cout) continue;
-    const f32x4 bias = load4f(L.b + c);
+    cc[i] = 16 * (f0 + i) + 4 * fq;
+    okc[i] = cc[i] < L.cout;
+    bias[i] = load4f(L.b + (okc[i] ? cc[i] : 0));
+  }
+  auto pix = [&](int j) { return 16 * (j0 + j) + fr; };
+  auto grow = [&](int j) { return (size_t)img * npix + (size_t)min(pix(j), npix - 1); };
+  if (!last) {
+    if (first && o.add) {
+      f32x4 ad[NF][MF];
 #pragma unroll
-    for (int j = 0; j < MF; ++j) {
-      const int p = 16 * (j0 + j) + fr;
-      if (p >= npix) continue;
-      const size_t row = (size_t)img * npix + p;
-      f32x4 v = acc[i][j] + bias;
-      if (first && o.add) v += load4f(o.add + row * o.ld_add + c);
-      if (!last) {
+      for (int i = 0; i < NF; ++i)
+#pragma unroll
+        for (int j = 0; j < MF; ++j) ad[i][j] = load4f(o.add + grow(j) * o.ld_add + (okc[i] ? cc[i] : 0));
+#pragma unroll
+      for (int i = 0; i < NF; ++i)
+#pragma unroll
+        for (int j = 0; j < MF; ++j) acc[i][j] += ad[i][j];
+    }
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int j = 0; j < MF; ++j) {
+        const f32x4 v = acc[i][j] + bias[i];
         const f32x2 lo = gelu2_bf16out(v.xy), hi = gelu2_bf16out(v.zw);
         bf16x4 q;
         q[0] = (bf16)lo.x; q[1] = (bf16)lo.y; q[2] = (bf16)hi.x; q[3] = (bf16)hi.y;
-        *reinterpret_cast<bf16x4*>(lb + out_off + p * pout + 2 * c) = q;
-      } else if (o.src) {  // lrp: y_hat = y_hat_pre + 0.5 tanh(lrp)
-        f32x4 r = load4f(o.src + row * o.ld_src + c);
+        if (okc[i] && pix(j) < npix) *reinterpret_cast<bf16x4*>(lb + out_off + pix(j) * pout + 2 * cc[i]) = q;
+      }
+  } else if (o.src) {  // lrp: y_hat = y_hat_pre + 0.5 tanh(lrp)
+    f32x4 sv[NF][MF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int j = 0; j < MF; ++j) sv[i][j] = load4f(o.src + grow(j) * o.ld_src + (okc[i] ? cc[i] : 0));
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int j = 0; j < MF; ++j) {
+        const f32x4 v = acc[i][j] + bias[i];
+        f32x4 r = sv[i][j];
 #pragma unroll
         for (int e = 0; e < 4; ++e) r[e] += 0.5f * tanhf(v[e]);
-        store4(reinterpret_cast<bf16*>(o.y) + row * o.ldy + c, r);
-        if (o.y2) store4(reinterpret_cast<bf16*>(o.y2) + row * o.ldy2 + c, r);
-      } else if (o.y_f32) {
-        store4(reinterpret_cast<float*>(o.y) + row * o.ldy + c, v);
-      } else {
-        store4(reinterpret_cast<bf16*>(o.y) + row * o.ldy + c, v);
+        if (okc[i] && pix(j) < npix) {
+          store4(reinterpret_cast<bf16*>(o.y) + grow(j) * o.ldy + cc[i], r);
+          if (o.y2) store4(reinterpret_cast<bf16*>(o.y2) + grow(j) * o.ldy2 + cc[i], r);
+        }
       }
-    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int j = 0; j < MF; ++j) {
+        const f32x4 v = acc[i][j] + bias[i];
+        if (okc[i] && pix(j) < npix) {
+          if (o.y_f32) store4(reinterpret_cast<float*>(o.y) + grow(j) * o.ldy + cc[i], v);
+          else store4(reinterpret_cast<bf16*>(o.y) + grow(j) * o.ldy + cc[i], v);
+        }
+      }
   }
 }
 
@@ -210,7 +275,7 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
   // zero row + layer-0 input -> buffer 0 (channels [0, c1) from x1, [c1, cin0) from x2, pad zeros)
-  for (int i = tid; i < MAXPITCH / 16; i += NW * 64) reinterpret_cast<uint4*>(lds)[ZOFF / 16 + i] = uint4{0, 0, 0, 0};
+  for (int i = tid; i < 16 * MAXPITCH / 16; i += NW * 64) reinterpret_cast<uint4*>(lds)[ZOFF / 16 + i] = uint4{0, 0, 0, 0};
   for (int p = tid; p < 160; p += NW * 64) {
     unsigned m = 0;
     if (p < npix) {
@@ -225,7 +290,6 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
   }
   const int c1 = a->c1, cin0 = a->c1 + a->c2;
   const int nl = a->nlayers;
-  const int pol = a->flags & 2;  // experiment knob: item policy B
   if (a->flags & TMAE_LIC_STACK_WARM_L2) {
     // L2 warm-up: the workgroups of one XCD (a contiguous run of t, one problem) each touch 1/16 of the
     // problem's packed weights up front (LDS-DMA into a dump area: no registers, many in flight), so the
@@ -239,6 +303,17 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
       const char* w = reinterpret_cast<const char*>(a->w[l]) + 2 * (b1 * a->w_s[l][0] + b2 * a->w_s[l][1]);
       for (long long c = (part * NW + wave) * 64 + lane; c < nchunk; c += 16LL * NW * 64) glds16(w + 16 * c, dump);
       ci = co;
+    }
+    // and this image's rows of the layer-0 addend / the lrp source (f32, otherwise first read from HBM
+    // inside the epilogues, one exposed round trip per item)
+    const float* ad = a->addend ? a->addend + b1 * a->a_s[0] + b2 * a->a_s[1] : nullptr;
+    const float* sr = a->lrp_src ? a->lrp_src + b1 * a->src_s[0] + b2 * a->src_s[1] : nullptr;
+    const int qa = ad ? a->cout[0] >> 2 : 0, qs = sr ? a->cout[nl - 1] >> 2 : 0;  // 16-B pieces per row
+    for (int i = tid; i < npix * (qa + qs); i += NW * 64) {
+      const int p = i / (qa + qs), k = i - p * (qa + qs);
+      const size_t row = (size_t)img * npix + p;
+      glds16(k < qa ? (const void*)(ad + row * a->ld_add + 4 * k) : (const void*)(sr + row * a->ld_src + 4 * (k - qa)),
+             dump);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -281,27 +356,33 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
     const unsigned in_off = (l & 1) ? (unsigned)BUF : 0u, out_off = (l & 1) ? 0u : (unsigned)BUF;
     const int nfr = (L.cout + 15) >> 4;
     const int nkc = pad32(L.cin) >> 5;
-    // wave items (each A fragment is loaded by ONE wave unless the pixel set is split):
-    //   >= 12 output fragments (224): two fragments x all pixel fragments (B reads shared by both);
-    //   8..11 (176, 128): one fragment x all pixel fragments (enough items for two per SIMD);
-    //   < 8 (80, 32): one fragment x half the pixel fragments (more items for the waves)
-    if (pol && nfr >= 8) {  // policy B: fragment pairs x pixel halves for every wide layer
-      const int nh = (nmf + 4) / 5, ng = (nfr + 1) >> 1;
-      for (int it = wave; it < ng * nh; it += NW) {
-        const int g = it / nh, h = it - g * nh;
-        lstk_dispatch<2, 5>(nkc, L, first, last, o, img, 2 * g, 5 * h, lb, in_off, out_off, npix, G, lane);
+    // wave items.  LDS bandwidth binds first: one 1-KiB B read per 16-cycle MFMA on every SIMD is the whole
+    // 256 B/clk array, so every wide layer shares each B read between two output fragments (NF = 2); the
+    // pixel fragments are split in halves (5 + 4) where that balances the four SIMDs better:
+    //   >= 14 output fragments (224): fragment pairs x all pixel fragments (7 items);
+    //   8..13 (176, 128): fragment pairs x pixel halves, all first halves dealt before the second ones;
+    //   < 8 (80, 32): single fragments x pixel halves.
+    const bool halves = nmf > 5;
+    if (nfr >= 8) {
+      const int ng = (nfr + 1) >> 1;
+      if (nfr >= 14 || !halves) {
+        for (int it = wave; it < ng; it += NW)
+          lstk_dispatch<2, 9>(nkc, L, first, last, o, img, 2 * it, 0, lb, in_off, out_off, npix, G, lane);
+      } else {
+        for (int it = wave; it < 2 * ng; it += NW) {
+          const int g = it < ng ? it : it - ng;
+          if (it < ng) lstk_dispatch<2, 5>(nkc, L, first, last, o, img, 2 * g, 0, lb, in_off, out_off, npix, G, lane);
+          else lstk_dispatch<2, 4>(nkc, L, first, last, o, img, 2 * g, 5, lb, in_off, out_off, npix, G, lane);
+        }
       }
-    } else if (nfr >= 12) {
-      for (int it = wave; it < (nfr + 1) >> 1; it += NW)
-        lstk_dispatch<2, 9>(nkc, L, first, last, o, img, 2 * it, 0, lb, in_off, out_off, npix, G, lane);
-    } else if (nfr >= 8) {
+    } else if (!halves) {
       for (int it = wave; it < nfr; it += NW)
-        lstk_dispatch<1, 9>(nkc, L, first, last, o, img, it, 0, lb, in_off, out_off, npix, G, lane);
+        lstk_dispatch<1, 5>(nkc, L, first, last, o, img, it, 0, lb, in_off, out_off, npix, G, lane);
     } else {
-      const int nh = (nmf + 4) / 5;
-      for (int it = wave; it < nfr * nh; it += NW) {
-        const int g = it / nh, h = it - g * nh;
-        lstk_dispatch<1, 5>(nkc, L, first, last, o, img, g, 5 * h, lb, in_off, out_off, npix, G, lane);
+      for (int it = wave; it < 2 * nfr; it += NW) {
+        const int f = it < nfr ? it : it - nfr;
+        if (it < nfr) lstk_dispatch<1, 5>(nkc, L, first, last, o, img, f, 0, lb, in_off, out_off, npix, G, lane);
+        else lstk_dispatch<1, 4>(nkc, L, first, last, o, img, f, 5, lb, in_off, out_off, npix, G, lane);
       }
     }
     if (!last) {

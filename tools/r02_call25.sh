@@ -1,0 +1,15 @@
+#!/bin/bash
+# round-2 call 25: fused stacks: NF=2 pairs with balanced pixel halves, addend / lrp-source L2 warm-up
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+L=$PWD/textmae-image-compression_amd/lib
+B="python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-roofline --no-train"
+P2="SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU"
+bash tools/gpu_session.sh \
+  "pytest_lstk:300:python -u -m pytest tests/test_gpu_lic_stack.py -q --timeout 120 --timeout-method thread -p no:cacheprovider" \
+  "lstk:200:python -u tools/lstk_bench.py" \
+  "lstk_d4:200:TMAE_LIB=$L/libtmae_d4.so python -u tools/lstk_bench.py ms_3 lrp_3 b_ms" \
+  "lstk_d32:200:TMAE_LIB=$L/libtmae_d32.so python -u tools/lstk_bench.py ms_3 lrp_3 b_ms" \
+  "pmc2:90:timeout -s KILL 80 rocprofv3 --kernel-trace --pmc $P2 -f csv -d gpurun_out/pmc2 -o p -- python3 tools/lstk_bench.py ms_3" \
+  "bench_new:200:$B" \
+  "bench_old:200:TMAE_LIC_STACK=0 $B"
