@@ -190,7 +190,7 @@ def conv3x3(x1, c1, ld1, n, H, W, w, b, y, ldy, cout, dtype, stride=1, act=ACT_N
 
 
 LSTK_MAXC, LSTK_MAXPIX = 224, 144  # lic_stack.hip: widest resident activation, pixels per workgroup
-LSTK_FLAGS = int(os.environ.get("TMAE_LSTK_FLAGS", "1"))  # bit 0: L2 warm-up of the stack's weights
+LSTK_FLAGS = int(os.environ.get("TMAE_LSTK_FLAGS", "0"))  # bit 0: L2 warm-up (measured: costs 3-5 us per stack)
 
 
 def _pad(c, m):
