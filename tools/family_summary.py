@@ -22,6 +22,8 @@ from collections import defaultdict
 
 
 def family(name):
+    if "lic_stack_kernel" in name:
+        return "lic_stack"
     if "conv_halo_kernel" in name or ("gemm" in name and "ConvSrc" in name):
         return "lic_conv3x3"
     if "mha_fwd" in name:
