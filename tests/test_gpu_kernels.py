@@ -168,6 +168,31 @@ def test_conv3x3_batched_addend(tmae, dtype):
             assert rel(y[i, j], ref) < tol(dtype), (i, j)
 
 
+@pytest.mark.parametrize("n", [5, 64])
+def test_conv_halo_two_images_bitwise(tmae, n, monkeypatch):
+    """the halo-staged conv with two images per workgroup (TMAE_CONV_HALO_IMG=2) against one image per
+    workgroup: same per-output accumulation order, so bitwise equal -- odd batch (a half-empty last pair),
+    two input segments, 2 problems with an addend, cin not a multiple of 64"""
+    torch.manual_seed(n)
+    H, c1, c2, cout, nb = 12, 160, 32, 224, 2
+    xa = torch.randn(n * H * H, c1).to(torch.bfloat16).to(DEV)
+    xb = torch.randn(n * H * H, c2).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(nb, cout, 9 * (c1 + c2)) / (9 * (c1 + c2)) ** 0.5).to(torch.bfloat16).to(DEV)
+    b = torch.randn(nb, cout, device=DEV)
+    add = torch.randn(n * H * H, 2 * cout, device=DEV)
+    outs = []
+    for im in ("1", "2"):
+        monkeypatch.setenv("TMAE_CONV_HALO_IMG", im)
+        y = torch.full((nb, n * H * H, cout), float("nan"), device=DEV, dtype=torch.bfloat16)
+        tmae.ops.conv3x3(xa, c1, c1, n, H, H, w, b, y, cout, cout, torch.bfloat16, act=1, x2=xb, c2=c2, ld2=c2,
+                         addend=add, ld_add=2 * cout, nb=(1, nb),
+                         strides={"w": (0, w[0].numel()), "b": (0, cout), "a": (0, cout), "y": (0, n * H * H * cout)})
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert not torch.isnan(outs[1].float()).any()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 def test_conv3x3_lrp_epilogue(tmae, dtype):
     torch.manual_seed(12)
