@@ -147,9 +147,22 @@ typedef struct tmae_lic_stack_args {
   void* y; int y_f32, ldy; long long y_s[2];
   const float* lrp_src; int ld_src; long long src_s[2];
   void* y2; int ldy2; long long y2_s[2];
-  int flags; /* TMAE_LIC_STACK_WARM_L2: touch the problem's weights into each XCD's L2 up front */
+  int flags; /* TMAE_LIC_STACK_CHAIN */
+  /* TMAE_LIC_STACK_CHAIN: problem (0, 0) of the nb1 x nb2 = 2 x 1 launch (a slice's mean stack; problem
+   * (1, 0) is its scale stack) goes on with that slice's lrp stack in the same workgroup (MCM.py:771-784):
+   * y_hat_pre = round(y - mu) + mu from yv (f32, rows ldyv apart) and the mean stack's f32 output mu, also
+   * written to csrc (f32, rows cld_src apart); lrp input = [cx1 channels 0..cc1 | y_hat_pre];
+   * cy (and cy2, optional) = y_hat_pre + 0.5 tanh(lrp), bf16.  cw / cb / ccout: the lrp layers (packed as w),
+   * cadd: its layer-0 addend.  The Gaussian likelihood of the slice is left to the caller. */
+  int cn; const void* cw[TMAE_LIC_STACK_MAXL]; const float* cb[TMAE_LIC_STACK_MAXL]; int ccout[TMAE_LIC_STACK_MAXL];
+  const void* cx1; int cc1, cld1;
+  const float* yv; int ldyv;
+  const float* cadd; int cld_add;
+  float* csrc; int cld_src;
+  void* cy; int cldy;
+  void* cy2; int cldy2;
 } tmae_lic_stack_args;
-#define TMAE_LIC_STACK_WARM_L2 1
+#define TMAE_LIC_STACK_CHAIN 1
 int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream);
 
 /* GaussianConditional likelihood + y_hat quantisation for `nslices` consecutive slices of width sw

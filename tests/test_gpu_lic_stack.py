@@ -157,3 +157,37 @@ def test_mcm_fused_stacks_match_layerwise(tmae):
     assert flips <= 1e-3 * a["yh"].numel()
     assert xr < 2e-2
     assert float(ly.mean()) < 2e-2
+
+
+@pytest.mark.parametrize("training", [False, True])
+def test_mcm_chained_slices_bitwise(tmae, training):
+    """serial slices chained (mean stack -> y_hat_pre -> lrp stack in one launch, likelihoods deferred) against
+    the separate mean/scale, Gaussian and lrp launches: the same arithmetic in the same order, so x_hat, both
+    likelihoods and y_hat are bitwise equal (eval, and train-mode quantisation noise injected)"""
+    torch.manual_seed(4)
+    m = tmae.MCM(img_size=256, num_keep_patches=144).to(DEV).eval()
+    m.compute_dtype = torch.bfloat16
+    m.distortion = "none"
+    imgs = torch.randn(6, 3, 256, 256, device=DEV)
+    scores = torch.rand(6, 256, device=DEV)
+    noise = (torch.rand(6, 192, 3, 3, device=DEV) - 0.5, torch.rand(6, 384, 12, 12, device=DEV) - 0.5)
+    outs = {}
+    old = os.environ.get("TMAE_LIC_CHAIN")
+    try:
+        for flag in ("1", "0"):
+            os.environ["TMAE_LIC_CHAIN"] = flag
+            m._exec = None
+            m.train(training)
+            with torch.no_grad():
+                o = m(imgs, scores, noise=noise) if training else m(imgs, scores)
+            outs[flag] = (o["x_hat"].clone(), o["likelihoods"]["y"].clone(), o["likelihoods"]["z"].clone(),
+                          m._exec.YH.clone())
+    finally:
+        if old is None:
+            os.environ.pop("TMAE_LIC_CHAIN", None)
+        else:
+            os.environ["TMAE_LIC_CHAIN"] = old
+        m._exec = None
+        m.eval()
+    for a, b in zip(outs["1"], outs["0"]):
+        assert torch.equal(a, b)

@@ -79,6 +79,13 @@ class LicStackArgs(ctypes.Structure):
         ("lrp_src", P), ("ld_src", I), ("src_s", LL * 2),
         ("y2", P), ("ldy2", I), ("y2_s", LL * 2),
         ("flags", I),
+        ("cn", I), ("cw", P * LSTK_MAXL), ("cb", P * LSTK_MAXL), ("ccout", I * LSTK_MAXL),
+        ("cx1", P), ("cc1", I), ("cld1", I),
+        ("yv", P), ("ldyv", I),
+        ("cadd", P), ("cld_add", I),
+        ("csrc", P), ("cld_src", I),
+        ("cy", P), ("cldy", I),
+        ("cy2", P), ("cldy2", I),
     ]
 
 

@@ -31,8 +31,7 @@ constexpr int MAXPITCH = 2 * MAXC + 32;     // bytes
 constexpr int MAXPIX = 144;                 // 12 x 12
 constexpr int BUF = MAXPIX * MAXPITCH;      // one activation buffer
 constexpr int ZOFF = 2 * BUF;               // zero block: 16 rows, read by taps that fall outside the grid
-constexpr int DUMP = 2 * BUF + 16 * MAXPITCH;  // 1 KiB landing area of the L2 warm-up DMA (never read)
-constexpr int TMASK = DUMP + 1024;          // per-pixel 9-bit tap-validity masks (u16, 160 pixel slots)
+constexpr int TMASK = 2 * BUF + 16 * MAXPITCH;  // per-pixel 9-bit tap-validity masks (u16, 160 pixel slots)
 constexpr int LDS_BYTES = TMASK + 320;
 __host__ __device__ constexpr int pad32(int c) { return (c + 31) & ~31; }
 // row pitch: 32 B past the channels makes every ds_read_b128 fragment read (16 consecutive rows, the
@@ -290,33 +289,6 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
   }
   const int c1 = a->c1, cin0 = a->c1 + a->c2;
   const int nl = a->nlayers;
-  if (a->flags & TMAE_LIC_STACK_WARM_L2) {
-    // L2 warm-up: the workgroups of one XCD (a contiguous run of t, one problem) each touch 1/16 of the
-    // problem's packed weights up front (LDS-DMA into a dump area: no registers, many in flight), so the
-    // per-tap A-fragment loads hit L2 instead of each paying a miss one tap ahead
-    const unsigned dump = (unsigned)(size_t)(lds_void_t*)lds + DUMP;
-    const long long part = t & 15;
-    int ci = cin0;
-    for (int l = 0; l < nl; ++l) {
-      const int co = a->cout[l];
-      const long long nchunk = 9LL * (pad32(ci) >> 5) * ((co + 15) >> 4) * 64;  // 16-B pieces
-      const char* w = reinterpret_cast<const char*>(a->w[l]) + 2 * (b1 * a->w_s[l][0] + b2 * a->w_s[l][1]);
-      for (long long c = (part * NW + wave) * 64 + lane; c < nchunk; c += 16LL * NW * 64) glds16(w + 16 * c, dump);
-      ci = co;
-    }
-    // and this image's rows of the layer-0 addend / the lrp source (f32, otherwise first read from HBM
-    // inside the epilogues, one exposed round trip per item)
-    const float* ad = a->addend ? a->addend + b1 * a->a_s[0] + b2 * a->a_s[1] : nullptr;
-    const float* sr = a->lrp_src ? a->lrp_src + b1 * a->src_s[0] + b2 * a->src_s[1] : nullptr;
-    const int qa = ad ? a->cout[0] >> 2 : 0, qs = sr ? a->cout[nl - 1] >> 2 : 0;  // 16-B pieces per row
-    for (int i = tid; i < npix * (qa + qs); i += NW * 64) {
-      const int p = i / (qa + qs), k = i - p * (qa + qs);
-      const size_t row = (size_t)img * npix + p;
-      glds16(k < qa ? (const void*)(ad + row * a->ld_add + 4 * k) : (const void*)(sr + row * a->ld_src + 4 * (k - qa)),
-             dump);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
   {
     const bf16* x1 = reinterpret_cast<const bf16*>(a->x1) + b1 * a->x1_s[0] + b2 * a->x1_s[1];
     const bf16* x2 = a->x2 ? reinterpret_cast<const bf16*>(a->x2) + b1 * a->x2_s[0] + b2 * a->x2_s[1] : nullptr;
@@ -333,70 +305,126 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
   }
   __syncthreads();
 
-  LstkOut o;
-  o.add = a->addend ? a->addend + b1 * a->a_s[0] + b2 * a->a_s[1] : nullptr;
-  o.ld_add = a->ld_add;
-  o.y_f32 = a->y_f32;
-  o.y = o.y_f32 ? (void*)(reinterpret_cast<float*>(a->y) + b1 * a->y_s[0] + b2 * a->y_s[1])
-                : (void*)(reinterpret_cast<bf16*>(a->y) + b1 * a->y_s[0] + b2 * a->y_s[1]);
-  o.ldy = a->ldy;
-  o.src = a->lrp_src ? a->lrp_src + b1 * a->src_s[0] + b2 * a->src_s[1] : nullptr;
-  o.ld_src = a->ld_src;
-  o.y2 = a->y2 ? (void*)(reinterpret_cast<bf16*>(a->y2) + b1 * a->y2_s[0] + b2 * a->y2_s[1]) : nullptr;
-  o.ldy2 = a->ldy2;
-
+  // pass 0: the stack of this problem; pass 1 (TMAE_LIC_STACK_CHAIN, problem (0, 0) = a slice's mean stack):
+  // that slice's lrp stack, same workgroup, its input built from the mean stack's output
+  const bool chain = (a->flags & TMAE_LIC_STACK_CHAIN) && b1 == 0 && b2 == 0;
   int cin = cin0;
-  for (int l = 0; l < nl; ++l) {
-    LstkLayer L;
-    L.w = reinterpret_cast<const bf16*>(a->w[l]) + b1 * a->w_s[l][0] + b2 * a->w_s[l][1];
-    L.b = a->bias[l] + b1 * a->b_s[l][0] + b2 * a->b_s[l][1];
-    L.cin = cin;
-    L.cout = a->cout[l];
-    const bool first = l == 0, last = l + 1 == nl;
-    const unsigned in_off = (l & 1) ? (unsigned)BUF : 0u, out_off = (l & 1) ? 0u : (unsigned)BUF;
-    const int nfr = (L.cout + 15) >> 4;
-    const int nkc = pad32(L.cin) >> 5;
-    // wave items.  LDS bandwidth binds first: one 1-KiB B read per 16-cycle MFMA on every SIMD is the whole
-    // 256 B/clk array, so every wide layer shares each B read between two output fragments (NF = 2); the
-    // pixel fragments are split in halves (5 + 4) where that balances the four SIMDs better:
-    //   >= 14 output fragments (224): fragment pairs x all pixel fragments (7 items);
-    //   8..13 (176, 128): fragment pairs x pixel halves, all first halves dealt before the second ones;
-    //   < 8 (80, 32): single fragments x pixel halves.
-    const bool halves = nmf > 5;
-    if (nfr >= 8) {
-      const int ng = (nfr + 1) >> 1;
-      if (nfr >= 14 || !halves) {
-        for (int it = wave; it < ng; it += NW)
-          lstk_dispatch<2, 9>(nkc, L, first, last, o, img, 2 * it, 0, lb, in_off, out_off, npix, G, lane);
-      } else {
-        for (int it = wave; it < 2 * ng; it += NW) {
-          const int g = it < ng ? it : it - ng;
-          if (it < ng) lstk_dispatch<2, 5>(nkc, L, first, last, o, img, 2 * g, 0, lb, in_off, out_off, npix, G, lane);
-          else lstk_dispatch<2, 4>(nkc, L, first, last, o, img, 2 * g, 5, lb, in_off, out_off, npix, G, lane);
-        }
-      }
-    } else if (!halves) {
-      for (int it = wave; it < nfr; it += NW)
-        lstk_dispatch<1, 5>(nkc, L, first, last, o, img, it, 0, lb, in_off, out_off, npix, G, lane);
+  for (int pass = 0; pass < (chain ? 2 : 1); ++pass) {
+    LstkOut o;
+    if (pass == 0) {
+      o.add = a->addend ? a->addend + b1 * a->a_s[0] + b2 * a->a_s[1] : nullptr;
+      o.ld_add = a->ld_add;
+      o.y_f32 = a->y_f32;
+      o.y = o.y_f32 ? (void*)(reinterpret_cast<float*>(a->y) + b1 * a->y_s[0] + b2 * a->y_s[1])
+                    : (void*)(reinterpret_cast<bf16*>(a->y) + b1 * a->y_s[0] + b2 * a->y_s[1]);
+      o.ldy = a->ldy;
+      o.src = a->lrp_src ? a->lrp_src + b1 * a->src_s[0] + b2 * a->src_s[1] : nullptr;
+      o.ld_src = a->ld_src;
+      o.y2 = a->y2 ? (void*)(reinterpret_cast<bf16*>(a->y2) + b1 * a->y2_s[0] + b2 * a->y2_s[1]) : nullptr;
+      o.ldy2 = a->ldy2;
     } else {
-      for (int it = wave; it < 2 * nfr; it += NW) {
-        const int f = it < nfr ? it : it - nfr;
-        if (it < nfr) lstk_dispatch<1, 5>(nkc, L, first, last, o, img, f, 0, lb, in_off, out_off, npix, G, lane);
-        else lstk_dispatch<1, 4>(nkc, L, first, last, o, img, f, 5, lb, in_off, out_off, npix, G, lane);
-      }
-    }
-    if (!last) {
-      // zero the channel padding [cout, pad32(cout)) the next layer's 32-wide K steps read
-      const int cp = pad32(L.cout), pz = pitch(L.cout);
-      const int q = (cp - L.cout) >> 3;  // 16-B pieces per row (cout is a multiple of 8)
-      if (q > 0)
-        for (int i = tid; i < npix * q; i += NW * 64) {
-          const int p = i / q, ch = L.cout + 8 * (i - p * q);
-          *reinterpret_cast<uint4*>(lb + out_off + p * pz + 2 * ch) = uint4{0, 0, 0, 0};
+      // lrp input (MCM.py:779-781): [y_hat slots 0..i-1 | y_hat_pre = round(y - mu) + mu] (the quantize_ste
+      // value, MCM.py:771-776); y_hat_pre also goes out in f32 (the lrp epilogue's source, read back below
+      // after the layer barriers; first touch of those lines by this CU, so no stale L1 copy)
+      const float* mu = reinterpret_cast<const float*>(a->y);  // the mean stack's output (f32), problem (0, 0)
+      const int ldmu = a->ldy, cc1 = a->cc1, sw = a->ccout[a->cn - 1];
+      const bf16* cx1 = reinterpret_cast<const bf16*>(a->cx1);
+      const float* yv = a->yv;
+      float* ypre = a->csrc;
+      const int cld1 = a->cld1, ldyv = a->ldyv, ldp = a->cld_src;
+      cin = cc1 + sw;
+      const int q = pad32(cin) >> 3, pin = pitch(cin);
+      for (int i = tid; i < npix * q; i += NW * 64) {
+        const int p = i / q, ch = 8 * (i - p * q);
+        const size_t row = (size_t)img * npix + p;
+        uint4 v = uint4{0, 0, 0, 0};
+        if (ch < cc1) {
+          v = *reinterpret_cast<const uint4*>(cx1 + row * cld1 + ch);
+        } else if (ch < cin) {
+          const int c = ch - cc1;
+          f32x4 y0, y1, m0, m1;
+          load8f(yv + row * ldyv + c, y0, y1);
+          load8f(mu + row * ldmu + c, m0, m1);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            y0[e] = rintf(y0[e] - m0[e]) + m0[e];
+            y1[e] = rintf(y1[e] - m1[e]) + m1[e];
+          }
+          store8(ypre + row * ldp + c, y0, y1);
+          v = pack8_bf16(y0, y1);
         }
+        *reinterpret_cast<uint4*>(lb + p * pin + 2 * ch) = v;
+      }
+      __syncthreads();
+      o.add = a->cadd;
+      o.ld_add = a->cld_add;
+      o.y_f32 = 0;
+      o.y = a->cy;
+      o.ldy = a->cldy;
+      o.src = ypre;
+      o.ld_src = ldp;
+      o.y2 = a->cy2;
+      o.ldy2 = a->cldy2;
     }
-    cin = L.cout;
-    __syncthreads();
+    const int nl = pass ? a->cn : a->nlayers;
+    for (int l = 0; l < nl; ++l) {
+      LstkLayer L;
+      if (pass == 0) {
+        L.w = reinterpret_cast<const bf16*>(a->w[l]) + b1 * a->w_s[l][0] + b2 * a->w_s[l][1];
+        L.b = a->bias[l] + b1 * a->b_s[l][0] + b2 * a->b_s[l][1];
+        L.cout = a->cout[l];
+      } else {
+        L.w = reinterpret_cast<const bf16*>(a->cw[l]);
+        L.b = a->cb[l];
+        L.cout = a->ccout[l];
+      }
+      L.cin = cin;
+      const bool first = l == 0, last = l + 1 == nl;
+      const unsigned in_off = (l & 1) ? (unsigned)BUF : 0u, out_off = (l & 1) ? 0u : (unsigned)BUF;
+      const int nfr = (L.cout + 15) >> 4;
+      const int nkc = pad32(L.cin) >> 5;
+      // wave items.  LDS bandwidth binds first: one 1-KiB B read per 16-cycle MFMA on every SIMD is the
+      // whole 256 B/clk array, so every wide layer shares each B read between two output fragments
+      // (NF = 2); the pixel fragments are split in halves (5 + 4) where that balances the four SIMDs better:
+      //   >= 14 output fragments (224): fragment pairs x all pixel fragments (7 items);
+      //   8..13 (176, 128): fragment pairs x pixel halves, all first halves dealt before the second ones;
+      //   < 8 (80, 32): single fragments x pixel halves.
+      const bool halves = nmf > 5;
+      if (nfr >= 8) {
+        const int ng = (nfr + 1) >> 1;
+        if (nfr >= 14 || !halves) {
+          for (int it = wave; it < ng; it += NW)
+            lstk_dispatch<2, 9>(nkc, L, first, last, o, img, 2 * it, 0, lb, in_off, out_off, npix, G, lane);
+        } else {
+          for (int it = wave; it < 2 * ng; it += NW) {
+            const int g = it < ng ? it : it - ng;
+            if (it < ng) lstk_dispatch<2, 5>(nkc, L, first, last, o, img, 2 * g, 0, lb, in_off, out_off, npix, G, lane);
+            else lstk_dispatch<2, 4>(nkc, L, first, last, o, img, 2 * g, 5, lb, in_off, out_off, npix, G, lane);
+          }
+        }
+      } else if (!halves) {
+        for (int it = wave; it < nfr; it += NW)
+          lstk_dispatch<1, 5>(nkc, L, first, last, o, img, it, 0, lb, in_off, out_off, npix, G, lane);
+      } else {
+        for (int it = wave; it < 2 * nfr; it += NW) {
+          const int f = it < nfr ? it : it - nfr;
+          if (it < nfr) lstk_dispatch<1, 5>(nkc, L, first, last, o, img, f, 0, lb, in_off, out_off, npix, G, lane);
+          else lstk_dispatch<1, 4>(nkc, L, first, last, o, img, f, 5, lb, in_off, out_off, npix, G, lane);
+        }
+      }
+      if (!last) {
+        // zero the channel padding [cout, pad32(cout)) the next layer's 32-wide K steps read
+        const int cp = pad32(L.cout), pz = pitch(L.cout);
+        const int q = (cp - L.cout) >> 3;  // 16-B pieces per row (cout is a multiple of 8)
+        if (q > 0)
+          for (int i = tid; i < npix * q; i += NW * 64) {
+            const int p = i / q, ch = L.cout + 8 * (i - p * q);
+            *reinterpret_cast<uint4*>(lb + out_off + p * pz + 2 * ch) = uint4{0, 0, 0, 0};
+          }
+      }
+      cin = L.cout;
+      __syncthreads();
+    }
   }
 }
 
@@ -420,6 +448,18 @@ extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
                  a.cout[l], MAXC);
   }
   TMAE_REQUIRE(!a.lrp_src || !a.y_f32, "tmae_lic_stack: lrp output is bf16");
+  if (a.flags & TMAE_LIC_STACK_CHAIN) {
+    TMAE_REQUIRE(a.nb1 == 2 && a.nb2 == 1 && a.y_f32 && !a.lrp_src && a.cn >= 1 && a.cn <= TMAE_LIC_STACK_MAXL,
+                 "tmae_lic_stack: chain needs the 2 x 1 mean / scale problems with f32 outputs");
+    TMAE_REQUIRE(a.ccout[a.cn - 1] == a.cout[a.nlayers - 1] && a.cx1 && a.yv && a.csrc && a.cy,
+                 "tmae_lic_stack: chain operands");
+    TMAE_REQUIRE(a.cc1 % 8 == 0 && a.cld1 % 8 == 0 && a.ldyv % 4 == 0 && a.cld_src % 4 == 0 && a.ldy % 4 == 0 &&
+                 pad32(a.cc1 + a.ccout[a.cn - 1]) <= MAXC, "tmae_lic_stack: chain channels %d + %d", a.cc1,
+                 a.ccout[a.cn - 1]);
+    for (int l = 0; l < a.cn; ++l)
+      TMAE_REQUIRE(a.cw[l] && a.cb[l] && a.ccout[l] % 8 == 0 && (l + 1 == a.cn || pad32(a.ccout[l]) <= MAXC),
+                   "tmae_lic_stack: chain layer %d", l);
+  }
   if (a.addend) TMAE_REQUIRE(a.ld_add % 4 == 0, "tmae_lic_stack: addend stride %d", a.ld_add);
   const int nwg = a.n * a.nb1 * a.nb2;
   hipLaunchKernelGGL(lic_stack_kernel, dim3(nwg), dim3(NW * 64), 0, (hipStream_t)stream, a);

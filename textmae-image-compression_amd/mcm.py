@@ -384,6 +384,9 @@ class _Executor:
         nb = self.nb
         self.CM = [z(2, nb, Mp, c, dtype=dt) for c in self.mid[:-1]]
         self.MUSIG = z(2, nb, Mp, self.sw)
+        # chained serial slices (mean stack + lrp stack in one launch): every serial slice's mu / sigma kept
+        # for the one deferred likelihood launch after the slice loop
+        self.MS_SER = z(2, self.maxsup, Mp, self.sw)
         self.CL = [z(nb, Mp, c, dtype=dt) for c in self.mid[:-1]]
         self.YLIK = z(B, M, g, g)
         gs = [l.out_channels for l in m.g_s if isinstance(l, nn.ConvTranspose2d)]
@@ -533,7 +536,7 @@ class _Executor:
         self._h_s()
 
         # ---- slice loop (MCM.py:751-787)
-        self._slices(self._gc_forward(y_noise))
+        self._slices(self._gc_forward(y_noise), chain_ok=True)
 
         x_hat = self._back(shuf, imgs.shape[1])
         return {"x_hat": x_hat, "y": self.YLIK.clone(), "z": self.ZLIK.clone(), "ids_restore": rest,
@@ -707,7 +710,7 @@ class _Executor:
                 cin = cout
             x, xs = out, out[0].numel()
 
-    def _slices(self, gc_step):
+    def _slices(self, gc_step, chain_ok=False):
         m, dt, B, g = self.m, self.dtype, self.batch, self.g
         M, S, sw, ms, nb, Mp = m.latent_depth, m.num_slices, self.sw, self.maxsup, self.nb, self.Mp
         mid = self.mid
@@ -837,8 +840,33 @@ class _Executor:
 
         # slices 0..ms-1: serial (slice i conditions on y_hat 0..i-1)
         fused = self.lstk is not None
+        # serial slices as ONE launch each (TMAE_LIC_CHAIN=0 disables): the mean stack's workgroups go on with
+        # the slice's lrp stack (y_hat_pre = round(y - mu) + mu in between), the scale stacks run beside them;
+        # the slices' Gaussian likelihoods follow the loop in one launch (nothing in the chain reads them)
+        chain = fused and chain_ok and os.environ.get("TMAE_LIC_CHAIN", "1") != "0"
+        ms_ser = self.MS_SER.data_ptr()
+        yv = self.Y32.data_ptr()
+
+        def ms_chain(i):
+            ws, (first, layers) = self.lstk["ms"][i], (self.ms_first[i], self.ms_layers[i])
+            bs_ = [first[1]] + [b for _, b in layers]
+            st = {"a": (off_scale - off_mean, c0), "y": (ms * Mp * sw, 0)}
+            for l, (w, b) in enumerate(zip(ws, bs_)):
+                st[f"w{l}"] = (w[0].numel(), 0)
+                st[f"b{l}"] = (b[0].numel(), 0)
+            lw = self.lstk["lrp"][i]
+            lb_ = [self.lrp_first[i][1]] + [b for _, b in self.lrp_layers[i]]
+            ch = dict(w=lw, b=lb_, couts=mid, x1=supy, c1=sw * i, ld1=M, y=yv + i * sw * e4, ldy=M,
+                      add=pbase + (off_lrp + i * c0) * eP, ld_add=Pw, ypre=ypre + i * sw * e4, ld_ypre=M,
+                      out=yh + i * sw * esz, ld_out=M, out2=supy + i * sw * esz, ld_out2=M)
+            ops.lic_stack(B, g, supy, sw * i, M, ws, bs_, mid, ms_ser + i * Mp * sw * e4, sw, True,
+                          addend=pbase + (off_mean + i * c0) * eP, ld_add=Pw, nb=(2, 1), strides=st, chain=ch)
+
         for i in range(ms):
             wait_pre(i)
+            if chain:
+                ms_chain(i)
+                continue
             if fused:
                 ms_fused(i, 1)
             else:
@@ -860,5 +888,7 @@ class _Executor:
                 lrp_fused(ms, nb)
             else:
                 lrp_stack(self.b_lrp_first, self.b_lrp_layers, ms, nb, x2=supy + ms * sw * esz)
+        if chain and ms > 0:  # likelihoods of the chained slices (overwrites their dead SUPY / YPRE slots)
+            gc_step(0, ms, ms_ser, ms_ser + ms * Mp * sw * e4, Mp * sw)
         for k in list(ready):  # join the side stream in every case
             wait_pre(k)

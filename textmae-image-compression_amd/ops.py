@@ -190,7 +190,6 @@ def conv3x3(x1, c1, ld1, n, H, W, w, b, y, ldy, cout, dtype, stride=1, act=ACT_N
 
 
 LSTK_MAXC, LSTK_MAXPIX = 224, 144  # lic_stack.hip: widest resident activation, pixels per workgroup
-LSTK_FLAGS = int(os.environ.get("TMAE_LSTK_FLAGS", "0"))  # bit 0: L2 warm-up (measured: costs 3-5 us per stack)
 
 
 def _pad(c, m):
@@ -220,7 +219,7 @@ def pack_lic_stack_weight(w: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor
 
 
 def lic_stack(n, G, x1, c1, ld1, weights, biases, couts, y, ldy, y_f32, x2=None, c2=0, ld2=0, addend=None, ld_add=0,
-              lrp_src=None, ld_src=0, y2=None, ldy2=0, nb=(1, 1), strides=None):
+              lrp_src=None, ld_src=0, y2=None, ldy2=0, nb=(1, 1), strides=None, chain=None):
     """One slice-transform stack per (problem, image) (tmae_lic_stack).  weights: packed per layer
     (pack_lic_stack_weight, problems stacked); `strides` maps operand (x1, x2, w0..w4, b0..b4, a, y, src, y2)
     -> (s1, s2) element strides of the nb[0] x nb[1] problems.  Pointers: tensors or raw addresses."""
@@ -235,7 +234,17 @@ def lic_stack(n, G, x1, c1, ld1, weights, biases, couts, y, ldy, y_f32, x2=None,
     a.y, a.y_f32, a.ldy = _p(y), int(y_f32), ldy
     a.lrp_src, a.ld_src = _p(lrp_src), ld_src
     a.y2, a.ldy2 = _p(y2), ldy2
-    a.flags = LSTK_FLAGS
+    if chain is not None:  # the mean problem goes on with its slice's lrp stack (TMAE_LIC_STACK_CHAIN)
+        a.flags = 1
+        a.cn = len(chain["couts"])
+        for l, (w, b, c) in enumerate(zip(chain["w"], chain["b"], chain["couts"])):
+            a.cw[l], a.cb[l], a.ccout[l] = _p(w), _p(b), c
+        a.cx1, a.cc1, a.cld1 = _p(chain["x1"]), chain["c1"], chain["ld1"]
+        a.yv, a.ldyv = _p(chain["y"]), chain["ldy"]
+        a.cadd, a.cld_add = _p(chain["add"]), chain["ld_add"]
+        a.csrc, a.cld_src = _p(chain["ypre"]), chain["ld_ypre"]
+        a.cy, a.cldy = _p(chain["out"]), chain["ld_out"]
+        a.cy2, a.cldy2 = _p(chain.get("out2")), chain.get("ld_out2", 0)
     for name, (s1, s2) in (strides or {}).items():
         if name[0] in "wb" and name[1:].isdigit():
             getattr(a, f"{name[0]}_s")[int(name[1:])][:] = (s1, s2)
