@@ -148,8 +148,8 @@ typedef struct tmae_lic_stack_args {
   const float* lrp_src; int ld_src; long long src_s[2];
   void* y2; int ldy2; long long y2_s[2];
   int flags; /* TMAE_LIC_STACK_CHAIN */
-  /* TMAE_LIC_STACK_CHAIN: problem (0, 0) of the nb1 x nb2 = 2 x 1 launch (a slice's mean stack; problem
-   * (1, 0) is its scale stack) goes on with that slice's lrp stack in the same workgroup (MCM.py:771-784):
+  /* TMAE_LIC_STACK_CHAIN: problems (0, b2) of the nb1 x nb2 = 2 x nb2 launch (slice b2's mean stack;
+   * (1, b2) its scale stack) go on with that slice's lrp stack in the same workgroup (MCM.py:771-784):
    * y_hat_pre = round(y - mu) + mu from yv (f32, rows ldyv apart) and the mean stack's f32 output mu, also
    * written to csrc (f32, rows cld_src apart); lrp input = [cx1 channels 0..cc1 | y_hat_pre];
    * cy (and cy2, optional) = y_hat_pre + 0.5 tanh(lrp), bf16.  cw / cb / ccout: the lrp layers (packed as w),
@@ -161,6 +161,8 @@ typedef struct tmae_lic_stack_args {
   float* csrc; int cld_src;
   void* cy; int cldy;
   void* cy2; int cldy2;
+  /* chain operands of problem (0, b2) are offset by b2 * these element strides (batched slices) */
+  long long cs_x1, cs_yv, cs_src, cs_add, cs_y, cs_y2, cs_w[TMAE_LIC_STACK_MAXL], cs_b[TMAE_LIC_STACK_MAXL];
 } tmae_lic_stack_args;
 #define TMAE_LIC_STACK_CHAIN 1
 int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream);

@@ -127,6 +127,8 @@ def test_mcm_fused_stacks_match_layerwise(tmae):
     scores = torch.rand(8, 256, device=DEV)
     outs = {}
     old = os.environ.get("TMAE_LIC_STACK")
+    old_chain = os.environ.get("TMAE_LIC_CHAIN")
+    os.environ["TMAE_LIC_CHAIN"] = "0"  # MUSIG holds the batched slices' mu / sigma only without the chain
     try:
         for flag in ("1", "0"):
             os.environ["TMAE_LIC_STACK"] = flag
@@ -144,6 +146,10 @@ def test_mcm_fused_stacks_match_layerwise(tmae):
             os.environ.pop("TMAE_LIC_STACK", None)
         else:
             os.environ["TMAE_LIC_STACK"] = old
+        if old_chain is None:
+            os.environ.pop("TMAE_LIC_CHAIN", None)
+        else:
+            os.environ["TMAE_LIC_CHAIN"] = old_chain
         m._exec = None
     a, b = outs["1"], outs["0"]
     flips = int(((a["yh"] - b["yh"]).abs() > 0.5).sum())
@@ -159,8 +165,8 @@ def test_mcm_fused_stacks_match_layerwise(tmae):
     assert float(ly.mean()) < 2e-2
 
 
-@pytest.mark.parametrize("training", [False, True])
-def test_mcm_chained_slices_bitwise(tmae, training):
+@pytest.mark.parametrize("training,batched", [(False, "0"), (True, "0"), (False, "1")])
+def test_mcm_chained_slices_bitwise(tmae, training, batched, monkeypatch):
     """serial slices chained (mean stack -> y_hat_pre -> lrp stack in one launch, likelihoods deferred) against
     the separate mean/scale, Gaussian and lrp launches: the same arithmetic in the same order, so x_hat, both
     likelihoods and y_hat are bitwise equal (eval, and train-mode quantisation noise injected)"""
@@ -171,6 +177,7 @@ def test_mcm_chained_slices_bitwise(tmae, training):
     imgs = torch.randn(6, 3, 256, 256, device=DEV)
     scores = torch.rand(6, 256, device=DEV)
     noise = (torch.rand(6, 192, 3, 3, device=DEV) - 0.5, torch.rand(6, 384, 12, 12, device=DEV) - 0.5)
+    monkeypatch.setenv("TMAE_LIC_CHAIN_B", batched)  # slices 6..11 chained as well
     outs = {}
     old = os.environ.get("TMAE_LIC_CHAIN")
     try:

@@ -86,6 +86,8 @@ class LicStackArgs(ctypes.Structure):
         ("csrc", P), ("cld_src", I),
         ("cy", P), ("cldy", I),
         ("cy2", P), ("cldy2", I),
+        ("cs_x1", LL), ("cs_yv", LL), ("cs_src", LL), ("cs_add", LL), ("cs_y", LL), ("cs_y2", LL),
+        ("cs_w", LL * LSTK_MAXL), ("cs_b", LL * LSTK_MAXL),
     ]
 
 

@@ -270,7 +270,10 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
   const int n = a->n, G = a->G, npix = G * G, nmf = (npix + 15) >> 4, nb2 = a->nb2;
   const int t = xcd_remap(blockIdx.x, gridDim.x);  // each XCD's L2 serves a contiguous run of problems
   const int prob = t / n, img = t - prob * n;
-  const long long b1 = prob / nb2, b2 = prob - (prob / nb2) * nb2;
+  // chained launches interleave mean (two stacks) and scale (one stack) problems, so every XCD's run of
+  // logical workgroups carries the same mix of long and short ones
+  const bool ilv = a->flags & TMAE_LIC_STACK_CHAIN;
+  const long long b1 = ilv ? prob % a->nb1 : prob / nb2, b2 = ilv ? prob / a->nb1 : prob - (prob / nb2) * nb2;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
   // zero row + layer-0 input -> buffer 0 (channels [0, c1) from x1, [c1, cin0) from x2, pad zeros)
@@ -307,7 +310,7 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
 
   // pass 0: the stack of this problem; pass 1 (TMAE_LIC_STACK_CHAIN, problem (0, 0) = a slice's mean stack):
   // that slice's lrp stack, same workgroup, its input built from the mean stack's output
-  const bool chain = (a->flags & TMAE_LIC_STACK_CHAIN) && b1 == 0 && b2 == 0;
+  const bool chain = (a->flags & TMAE_LIC_STACK_CHAIN) && b1 == 0;
   int cin = cin0;
   for (int pass = 0; pass < (chain ? 2 : 1); ++pass) {
     LstkOut o;
@@ -326,11 +329,12 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
       // lrp input (MCM.py:779-781): [y_hat slots 0..i-1 | y_hat_pre = round(y - mu) + mu] (the quantize_ste
       // value, MCM.py:771-776); y_hat_pre also goes out in f32 (the lrp epilogue's source, read back below
       // after the layer barriers; first touch of those lines by this CU, so no stale L1 copy)
-      const float* mu = reinterpret_cast<const float*>(a->y);  // the mean stack's output (f32), problem (0, 0)
+      // the mean stack's output (f32) of problem (0, b2)
+      const float* mu = reinterpret_cast<const float*>(a->y) + b2 * a->y_s[1];
       const int ldmu = a->ldy, cc1 = a->cc1, sw = a->ccout[a->cn - 1];
-      const bf16* cx1 = reinterpret_cast<const bf16*>(a->cx1);
-      const float* yv = a->yv;
-      float* ypre = a->csrc;
+      const bf16* cx1 = reinterpret_cast<const bf16*>(a->cx1) + b2 * a->cs_x1;
+      const float* yv = a->yv + b2 * a->cs_yv;
+      float* ypre = a->csrc + b2 * a->cs_src;
       const int cld1 = a->cld1, ldyv = a->ldyv, ldp = a->cld_src;
       cin = cc1 + sw;
       const int q = pad32(cin) >> 3, pin = pitch(cin);
@@ -356,14 +360,14 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
         *reinterpret_cast<uint4*>(lb + p * pin + 2 * ch) = v;
       }
       __syncthreads();
-      o.add = a->cadd;
+      o.add = a->cadd ? a->cadd + b2 * a->cs_add : nullptr;
       o.ld_add = a->cld_add;
       o.y_f32 = 0;
-      o.y = a->cy;
+      o.y = reinterpret_cast<bf16*>(a->cy) + b2 * a->cs_y;
       o.ldy = a->cldy;
       o.src = ypre;
       o.ld_src = ldp;
-      o.y2 = a->cy2;
+      o.y2 = a->cy2 ? (void*)(reinterpret_cast<bf16*>(a->cy2) + b2 * a->cs_y2) : nullptr;
       o.ldy2 = a->cldy2;
     }
     const int nl = pass ? a->cn : a->nlayers;
@@ -374,8 +378,8 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
         L.b = a->bias[l] + b1 * a->b_s[l][0] + b2 * a->b_s[l][1];
         L.cout = a->cout[l];
       } else {
-        L.w = reinterpret_cast<const bf16*>(a->cw[l]);
-        L.b = a->cb[l];
+        L.w = reinterpret_cast<const bf16*>(a->cw[l]) + b2 * a->cs_w[l];
+        L.b = a->cb[l] + b2 * a->cs_b[l];
         L.cout = a->ccout[l];
       }
       L.cin = cin;
@@ -449,8 +453,8 @@ extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
   }
   TMAE_REQUIRE(!a.lrp_src || !a.y_f32, "tmae_lic_stack: lrp output is bf16");
   if (a.flags & TMAE_LIC_STACK_CHAIN) {
-    TMAE_REQUIRE(a.nb1 == 2 && a.nb2 == 1 && a.y_f32 && !a.lrp_src && a.cn >= 1 && a.cn <= TMAE_LIC_STACK_MAXL,
-                 "tmae_lic_stack: chain needs the 2 x 1 mean / scale problems with f32 outputs");
+    TMAE_REQUIRE(a.nb1 == 2 && a.y_f32 && !a.lrp_src && a.cn >= 1 && a.cn <= TMAE_LIC_STACK_MAXL,
+                 "tmae_lic_stack: chain needs the 2 x nb2 mean / scale problems with f32 outputs");
     TMAE_REQUIRE(a.ccout[a.cn - 1] == a.cout[a.nlayers - 1] && a.cx1 && a.yv && a.csrc && a.cy,
                  "tmae_lic_stack: chain operands");
     TMAE_REQUIRE(a.cc1 % 8 == 0 && a.cld1 % 8 == 0 && a.ldyv % 4 == 0 && a.cld_src % 4 == 0 && a.ldy % 4 == 0 &&

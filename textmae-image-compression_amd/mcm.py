@@ -386,7 +386,7 @@ class _Executor:
         self.MUSIG = z(2, nb, Mp, self.sw)
         # chained serial slices (mean stack + lrp stack in one launch): every serial slice's mu / sigma kept
         # for the one deferred likelihood launch after the slice loop
-        self.MS_SER = z(2, self.maxsup, Mp, self.sw)
+        self.MS_SER = z(2, S, Mp, self.sw)
         self.CL = [z(nb, Mp, c, dtype=dt) for c in self.mid[:-1]]
         self.YLIK = z(B, M, g, g)
         gs = [l.out_channels for l in m.g_s if isinstance(l, nn.ConvTranspose2d)]
@@ -850,7 +850,7 @@ class _Executor:
         def ms_chain(i):
             ws, (first, layers) = self.lstk["ms"][i], (self.ms_first[i], self.ms_layers[i])
             bs_ = [first[1]] + [b for _, b in layers]
-            st = {"a": (off_scale - off_mean, c0), "y": (ms * Mp * sw, 0)}
+            st = {"a": (off_scale - off_mean, c0), "y": (S * Mp * sw, 0)}
             for l, (w, b) in enumerate(zip(ws, bs_)):
                 st[f"w{l}"] = (w[0].numel(), 0)
                 st[f"b{l}"] = (b[0].numel(), 0)
@@ -877,7 +877,26 @@ class _Executor:
             else:
                 lrp_stack(self.lrp_first[i], self.lrp_layers[i], i, 1)
         # slices ms..S-1: batched on the fixed support y_hat 0..ms-1
-        if nb > 0:
+        chain_b = chain and os.environ.get("TMAE_LIC_CHAIN_B", "0") != "0"
+        if nb > 0 and chain_b:  # 2 x nb problems, the mean ones chained into their lrp stacks
+            wait_pre(ms)
+            bw, (first, layers) = self.lstk["b_ms"], (self.b_ms_first, self.b_ms_layers)
+            bs_ = [first[1]] + [b for _, b in layers]
+            st = {"a": (off_scale - off_mean, c0), "y": (S * Mp * sw, Mp * sw)}
+            for l, (w, b) in enumerate(zip(bw, bs_)):
+                st[f"w{l}"] = (w[0].numel(), w[0][0].numel())
+                st[f"b{l}"] = (b[0].numel(), b.shape[-1])
+            lw = self.lstk["b_lrp"]
+            lb_ = [self.b_lrp_first[1]] + [b for _, b in self.b_lrp_layers]
+            cst = {"y": sw, "ypre": sw, "add": c0, "out": sw}
+            for l, (w, b) in enumerate(zip(lw, lb_)):
+                cst[f"w{l}"], cst[f"b{l}"] = w[0].numel(), b.shape[-1]
+            ch = dict(w=lw, b=lb_, couts=mid, x1=supy, c1=sw * ms, ld1=M, y=yv + ms * sw * e4, ldy=M,
+                      add=pbase + (off_lrp + ms * c0) * eP, ld_add=Pw, ypre=ypre + ms * sw * e4, ld_ypre=M,
+                      out=yh + ms * sw * esz, ld_out=M, strides=cst)
+            ops.lic_stack(B, g, supy, sw * ms, M, bw, bs_, mid, ms_ser + ms * Mp * sw * e4, sw, True,
+                          addend=pbase + (off_mean + ms * c0) * eP, ld_add=Pw, nb=(2, nb), strides=st, chain=ch)
+        elif nb > 0:
             wait_pre(ms)
             if fused:
                 ms_fused(ms, nb)
@@ -888,7 +907,7 @@ class _Executor:
                 lrp_fused(ms, nb)
             else:
                 lrp_stack(self.b_lrp_first, self.b_lrp_layers, ms, nb, x2=supy + ms * sw * esz)
-        if chain and ms > 0:  # likelihoods of the chained slices (overwrites their dead SUPY / YPRE slots)
-            gc_step(0, ms, ms_ser, ms_ser + ms * Mp * sw * e4, Mp * sw)
+        if chain:  # likelihoods of the chained slices (overwrites their dead SUPY / YPRE slots)
+            gc_step(0, S if (nb > 0 and chain_b) else ms, ms_ser, ms_ser + S * Mp * sw * e4, Mp * sw)
         for k in list(ready):  # join the side stream in every case
             wait_pre(k)

@@ -245,6 +245,11 @@ def lic_stack(n, G, x1, c1, ld1, weights, biases, couts, y, ldy, y_f32, x2=None,
         a.csrc, a.cld_src = _p(chain["ypre"]), chain["ld_ypre"]
         a.cy, a.cldy = _p(chain["out"]), chain["ld_out"]
         a.cy2, a.cldy2 = _p(chain.get("out2")), chain.get("ld_out2", 0)
+        cs = chain.get("strides", {})  # per-slice (b2) element strides of the chain operands
+        a.cs_x1, a.cs_yv, a.cs_src = cs.get("x1", 0), cs.get("y", 0), cs.get("ypre", 0)
+        a.cs_add, a.cs_y, a.cs_y2 = cs.get("add", 0), cs.get("out", 0), cs.get("out2", 0)
+        for l in range(a.cn):
+            a.cs_w[l], a.cs_b[l] = cs.get(f"w{l}", 0), cs.get(f"b{l}", 0)
     for name, (s1, s2) in (strides or {}).items():
         if name[0] in "wb" and name[1:].isdigit():
             getattr(a, f"{name[0]}_s")[int(name[1:])][:] = (s1, s2)

@@ -9,4 +9,6 @@ bash tools/gpu_session.sh \
   "bench_c0:200:TMAE_LIC_CHAIN=0 $B" \
   "bench_c1b:200:TMAE_LIC_CHAIN=1 $B" \
   "bench_c0b:200:TMAE_LIC_CHAIN=0 $B" \
+  "bench_cb:200:TMAE_LIC_CHAIN_B=1 $B" \
+  "bench_cbb:200:TMAE_LIC_CHAIN_B=1 $B" \
   "pytest_more:900:python -u -m pytest tests/test_gpu_bench_config.py tests/test_gpu_coding.py tests/test_gpu_mcm.py tests/test_gpu_eval.py -q --timeout 300 --timeout-method thread -p no:cacheprovider"
