@@ -181,6 +181,13 @@ class LaunchTimer:
             self.stack_bytes += P * (px * ch[0] * 2 + sum(9 * ch[l] * ch[l + 1] * 2 for l in range(c.nlayers))
                                      + (px * ch[1] * 4 if c.addend else 0)
                                      + px * ch[-1] * ((4 if c.y_f32 else 2) + (4 if c.lrp_src else 0)))
+            if c.flags & 1:  # chained: the mean problems (nb2 of them) go on with their lrp stacks
+                c2 = [c.cc1 + c.ccout[c.cn - 1]] + [c.ccout[l] for l in range(c.cn)]
+                fl += 2.0 * c.nb2 * px * 9 * sum(c2[l] * c2[l + 1] for l in range(c.cn))
+                # support slots + y and mu in, y_hat_pre f32 out, lrp weights, addend, y_hat out (bf16)
+                self.stack_bytes += c.nb2 * (px * c.cc1 * 2 + px * c2[-1] * (4 + 4 + 4 + 2)
+                                             + sum(9 * c2[l] * c2[l + 1] * 2 for l in range(c.cn))
+                                             + (px * c2[1] * 4 if c.cadd else 0))
             return "lic_stack", fl
         if name == "tmae_patch_embed_fwd":
             return "patch_embed", 2.0 * a[6] * a[13] * a[11] * a[7] * a[10] * a[10]
@@ -280,8 +287,8 @@ def roofline_report(m, imgs, scores, batch, dump=None):
     d = stat([dom])
     desc = {"lic_conv3x3": " (conv_halo_kernel + conv-source GEMM tiles: h_a / h_s and the slice stacks' "
                            "latent-channel partial sums)",
-            "lic_stack": " (lic_stack_kernel: whole cc_transform_mean/scale and lrp_transform stacks, one "
-                         "workgroup per problem x image)"}
+            "lic_stack": " (lic_stack_kernel: whole cc_transform_mean/scale stacks, each serial slice's mean "
+                         "stack chained into its lrp_transform stack, one workgroup per problem x image)"}
     roof = {"kernel": dom + desc.get(dom, ""),
             "bound": "mfma", "achieved": d["achieved"], "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
             "frac": d["frac"], "traffic": None, "launches_per_step": d["launches"],
