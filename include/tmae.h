@@ -169,7 +169,7 @@ int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream);
 
 /* GaussianConditional likelihood + y_hat quantisation for `nslices` consecutive slices of width sw
  * (MCM.py:767-776): lik[NCHW channel yoff + j*sw + c] = GC(y~, max(sigma, .11), mu), LowerBound 1e-9;
- * yhat (dtype yhat_dtype) and yhat32 (f32, optional) [pixel][channel] = round(y - mu) + mu.
+ * yhat (dtype yhat_dtype, optional) and yhat32 (f32, optional) [pixel][channel] = round(y - mu) + mu.
  * noise (NCHW like lik) selects the training-mode y~ = y + noise. */
 int tmae_gc_slices_fwd(const float* y, int ldy, int yoff, const float* mu, const float* sigma, long long ms_stride,
                        int ld_ms, const float* noise, float* lik, int Mtot, void* yhat, int yhat_dtype, int ld_yhat,

@@ -255,7 +255,7 @@ gc_slices_kernel(const float* __restrict__ y, int ldy, int yoff, const float* __
   const float up = 0.5f * erfcf(k * ((0.5f - val) / s));
   const float lo = 0.5f * erfcf(k * ((-0.5f - val) / s));
   lik[nchw] = fmaxf(up - lo, 1e-9f);
-  yhat[(size_t)m * ld_yhat + ch] = to_out<YT>(q);
+  if (yhat) yhat[(size_t)m * ld_yhat + ch] = to_out<YT>(q);
   if (yhat32) yhat32[(size_t)m * ld32 + ch] = q;
   if constexpr (CODE) {
     // MCM.compress (MCM.py:867-872): symbols = round(y - mu) (quantize "symbols"), indexes =
