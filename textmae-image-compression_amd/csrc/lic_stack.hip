@@ -11,13 +11,15 @@
 //     224 channels each) and is the next layer's input -- no HBM round trip between layers;
 //   * weights never touch LDS: they are pre-packed in MFMA fragment order ([tap][k32][cout16][lane][8])
 //     so every A-fragment is one coalesced 1-KiB wave load from L2 (all images of a problem share them),
-//     prefetched four K-steps ahead into VGPRs; so the K loop has NO workgroup barrier at all, only the
+//     prefetched 4-6 K-steps ahead into VGPRs; so the K loop has NO workgroup barrier at all, only the
 //     one between layers;
 //   * pixel fragments are 16 consecutive pixels; tap (dy, dx) shifts the LDS row by dy*G + dx, pixels
-//     whose tap falls outside the grid read a zero row.  Row pitch = 2 * round32(C) + 32 bytes, so every
-//     fragment read is bank-conflict-free for every tap shift.
-// Work split: 8 waves (two per SIMD); a wave item = one or two 16-channel output fragments x all 9 pixel
-// fragments (x 5 for the narrow last layers), items dealt round-robin to the waves.
+//     whose tap falls outside the grid read the matching row of a 16-row zero block.  Row pitch =
+//     2 * round32(C) + 32 bytes, so every fragment read is bank-conflict-free for every tap shift.
+// Work split: 8 waves (two per SIMD); a wave item = two 16-channel output fragments x all 9 pixel
+// fragments (224-wide layers), x a pixel half (176 / 128), or one fragment x a half (80 / 32); items
+// dealt round-robin to the waves (the layer loop below).
+// Chain mode (TMAE_LIC_STACK_CHAIN): a slice's mean-stack workgroups go on with the slice's lrp stack.
 // MFMA v_mfma_f32_16x16x32_bf16 issued swapped (A = weights 16 couts x 32 k, B = 32 k x 16 pixels):
 // each lane ends with 4 consecutive output channels of one pixel (one 8-B LDS store per fragment).
 // The first layer's epilogue adds the latent-channel partial sums (the P buffer of mcm.py _slices) and
