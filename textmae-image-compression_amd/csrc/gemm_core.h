@@ -339,7 +339,22 @@ __device__ __forceinline__ void epilogue_lds(const EPI& epi, const f32x4 (&acc)[
 // first half's MFMAs, the next step's first half under the second's, DMA two steps ahead): 1-3 %
 // faster on isolated 8-wave GEMMs, 4 % slower on the whole forward (256 VGPRs on the 256 x 256 tile;
 // the 4-wave tiles lost 5-8 % in isolation).
-template <typename T, int BN, int BM, int WGN, int NW, class WS, class XS, class EPI>
+// counted DMA wait + raw barrier of the NS-stage ring: `younger` stages were issued after the one the next
+// step reads (a __syncthreads fence would drain them too)
+template <int PER, int NS>
+__device__ __forceinline__ void gemm_ring_wait(int younger) {
+  if (NS > 3 && younger >= 2)
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(2 * PER) : "memory");
+  else if (younger >= 1)
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(PER) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// NS = LDS stages.  2: the next K-step's DMA in flight under the current MFMAs.  4 (small tiles with long K,
+// e.g. the 6x6 / 3x3-grid LIC convs: a 32x64 tile's K-step is a few MFMAs, so a 2-stage ring pays the
+// whole DMA latency every step): three steps in flight.
+template <typename T, int BN, int BM, int WGN, int NW, class WS, class XS, class EPI, int NS = 2>
 __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2)
 gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
   constexpr int BKE = 8 * Elt<T>::EPC;
@@ -350,7 +365,8 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
   constexpr int WJ = BN / PR, XJ = BM / PR;  // glds instructions per wave per stage
   constexpr int ROWS = BN + BM;
   static_assert(TN >= 1 && TM >= 1 && WJ >= 1 && XJ >= 1 && BN % PR == 0 && BM % PR == 0, "bad tile");
-  __shared__ __attribute__((aligned(16))) uint4 lds[2 * ROWS * 8];
+  static_assert(NS == 2 || NS == 4, "stages");
+  __shared__ __attribute__((aligned(16))) uint4 lds[NS * ROWS * 8];
 
   const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
   ws.batch(b1, b2);
@@ -396,7 +412,7 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
 
   int tn, tm;
   tile_order(xcd_remap(blockIdx.x, gridDim.x), ntn, ntm, tn, tm);
-  if (nk > 0) {
+  if (nk > 0 && NS == 2) {
     set_rows(tn, tm);
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -411,8 +427,22 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
       __syncthreads();
       stage ^= 1;
     }
+  } else if (nk > 0) {
+    // step kt reads stage kt % NS and issues step kt + NS - 1 into the stage step kt - 1 read (retired by
+    // the barrier that closed step kt - 1)
+    constexpr int PER = WJ + XJ;  // LDS-DMA instructions per wave per stage
+    set_rows(tn, tm);
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+      if (s < nk) issue(s, s);
+    gemm_ring_wait<PER, NS>(min(NS - 2, nk - 1));
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + NS - 1 < nk) issue((kt + NS - 1) % NS, kt + NS - 1);
+      mfma_tile<T, BN, WN, WM, TN, TM>(lds + (kt % NS) * ROWS * 8, wn, wm, lane, acc);
+      gemm_ring_wait<PER, NS>(min(kt + NS - 1, nk - 1) - (kt + 1));
+    }
   }
-  static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= 2 * ROWS * 128, "epilogue region exceeds the LDS ring");
+  static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= NS * ROWS * 128, "epilogue region exceeds the LDS ring");
   if (!(diag & 1))
     epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
                              tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
@@ -885,6 +915,16 @@ static int launch_one(const char* name, const WS& ws, const XS& xs, const EPI& e
   const int tiles = ceil_div(N, BN) * ceil_div(M, BM);
   if (tiles == 0 || n1 * n2 == 0) return TMAE_OK;
   if constexpr (GLDS) {
+    // small tiles (<= 160 LDS rows: 4 stages stay within two workgroups per CU) over a long K take the
+    // 4-stage ring (TMAE_GEMM_DEEP=0 disables)
+    constexpr bool deep_ok = sizeof(T) == 2 && NW == 4 && BN + BM <= 160;
+    if constexpr (deep_ok) {
+      if (ceil_div(K, 8 * Elt<T>::EPC) >= 8 && gemm_knob("TMAE_GEMM_DEEP", 1)) {
+        hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, NW, WS, XS, EPI, 4>), dim3(tiles, n1 * n2),
+                           dim3(64 * NW), 0, st, ws, xs, epi, M, N, K, n2, 0);
+        TMAE_LAUNCH_CHECK(name);
+      }
+    }
     hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, NW, WS, XS, EPI>), dim3(tiles, n1 * n2), dim3(64 * NW), 0,
                        st, ws, xs, epi, M, N, K, n2, gemm_knob("TMAE_GEMM_DIAG", 0));
   } else {
