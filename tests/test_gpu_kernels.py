@@ -73,6 +73,19 @@ def test_layernorm(tmae, D, dtype):
     assert rel(y.float(), ref) < tol(dtype)
 
 
+# bench-sized row counts, ragged against the 4-row block (with TMAE_LN_RPW=4 they take the 2- and 4-rows-per-wave
+# paths; the knob is read once per process)
+@pytest.mark.parametrize("groups,glen,D", [(3, 2731, 768), (5, 1700, 1024), (5, 1700, 512), (3, 2731, 2048)])
+def test_layernorm_multirow(tmae, groups, glen, D):
+    torch.manual_seed(glen + D)
+    x = torch.randn(groups, glen, D) * 2 - 1
+    w, b = torch.randn(D), torch.randn(D)
+    y = tmae.ops.layernorm(x.to(DEV), w.to(DEV), b.to(DEV), 1e-6, torch.float32, rows=groups * (glen - 1),
+                           row_group=glen - 1, group_stride=glen, row_offset=1)
+    ref = F.layer_norm(x[:, 1:], (D,), w, b, 1e-6).reshape(-1, D)
+    assert (y.cpu() - ref).abs().max().item() < 1e-4
+
+
 @pytest.mark.parametrize("M,N,K", [(9280, 2304, 768), (300, 64, 32), (129, 704, 640), (77, 32, 96), (1, 4, 8)])
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("act", [0, 1])

@@ -5,55 +5,82 @@
 //   source row = (r / G) * Gs + off + (r % G)
 #include "common.h"
 
-template <typename OT, int VPL>
+// RPW rows per wave: gamma / beta loaded once per wave, all RPW rows' loads in flight together.  Measured
+// slower at the bench shapes (42 launches: 390 us at 4 or 2 rows per wave, 348 us at 1 -- fewer waves hide
+// less latency), so one row per wave is the default; TMAE_LN_RPW=2/4 selects the others.
+template <typename OT, int VPL, int RPW>
 __global__ void __launch_bounds__(256)
 layernorm_kernel(const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
                  OT* __restrict__ y, int rows, int D, int G, int Gs, int off, float eps) {
   const int lane = threadIdx.x & 63;
-  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= rows) return;
-  const int sr = (r / G) * Gs + off + (r % G);
-  const float* xr = x + (size_t)sr * D;
+  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (r0 >= rows) return;
   const int nch = D >> 2;
-  // gamma / beta are loaded with the row, so the wave's only dependent memory latency is the row itself
-  f32x4 v[VPL], gv[VPL], bv[VPL];
+  f32x4 v[RPW][VPL], gv[VPL], bv[VPL];
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const int r = r0 + k;
+    const float* xr = x + (size_t)((r / G) * Gs + off + (r % G)) * D;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + 64 * i;
+      v[k][i] = (c < nch && r < rows) ? load4f(xr + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = lane + 64 * i;
-    v[i] = (c < nch) ? load4f(xr + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
     gv[i] = (c < nch) ? load4f(gamma + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
     bv[i] = (c < nch) ? load4f(beta + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  float s = 0.0f;
+  float s[RPW], q[RPW];
 #pragma unroll
-  for (int i = 0; i < VPL; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  for (int k = 0; k < RPW; ++k) {
+    s[k] = 0.0f;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  const float mean = s / (float)D;
-  float q = 0.0f;
+    for (int i = 0; i < VPL; ++i) s[k] += (v[k][i][0] + v[k][i][1]) + (v[k][i][2] + v[k][i][3]);
+  }
 #pragma unroll
-  for (int i = 0; i < VPL; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nch) {
+  for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float d = v[i][j] - mean;
-        q += d * d;
+    for (int k = 0; k < RPW; ++k) s[k] += __shfl_xor(s[k], o);
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) {
+    const float mean = s[k] / (float)D;
+    s[k] = mean;
+    q[k] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float d = v[k][i][j] - mean;
+          q[k] += d * d;
+        }
       }
     }
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
-  const float rstd = 1.0f / sqrtf(q / (float)D + eps);
-  OT* yr = y + (size_t)r * D;
+  for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
-  for (int i = 0; i < VPL; ++i) {
-    const int c = lane + 64 * i;
-    if (c < nch) {
-      f32x4 o;
+    for (int k = 0; k < RPW; ++k) q[k] += __shfl_xor(q[k], o);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = (v[i][j] - mean) * rstd * gv[i][j] + bv[i][j];
-      store4(yr + 4 * c, o);
+  for (int k = 0; k < RPW; ++k) {
+    const int r = r0 + k;
+    if (r >= rows) break;
+    const float mean = s[k];
+    const float rstd = 1.0f / sqrtf(q[k] / (float)D + eps);
+    OT* yr = y + (size_t)r * D;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nch) {
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (v[k][i][j] - mean) * rstd * gv[i][j] + bv[i][j];
+        store4(yr + 4 * c, o);
+      }
     }
   }
 }
@@ -61,15 +88,32 @@ layernorm_kernel(const float* __restrict__ x, const float* __restrict__ gamma, c
 template <typename OT>
 static int ln_launch(const float* x, const float* g, const float* b, void* y, int rows, int D, int G, int Gs, int off,
                      float eps, hipStream_t st) {
-  const int grid = ceil_div(rows, 4);
   if (rows == 0) return TMAE_OK;
   const int vpl = ceil_div(D / 4, 64);
-#define TMAE_LN(V) hipLaunchKernelGGL((layernorm_kernel<OT, V>), dim3(grid), dim3(256), 0, st, x, g, b, (OT*)y, rows, D, G, Gs, off, eps)
-  if (vpl <= 1) TMAE_LN(1);
-  else if (vpl <= 2) TMAE_LN(2);
-  else if (vpl <= 3) TMAE_LN(3);
-  else if (vpl <= 4) TMAE_LN(4);
-  else TMAE_LN(8);
+  // several rows per wave (opt-in) only when that still leaves >= 2 waves per SIMD
+  static const int rpw_max = [] {
+    const char* e = getenv("TMAE_LN_RPW");
+    return e ? atoi(e) : 1;
+  }();
+  const int rpw = (rpw_max >= 4 && vpl <= 4 && rows >= 4 * 2048) ? 4
+                  : (rpw_max >= 2 && rows >= 2 * 2048)             ? 2
+                                                                   : 1;
+  const int grid = ceil_div(rows, 4 * rpw);
+#define TMAE_LN(V, R) hipLaunchKernelGGL((layernorm_kernel<OT, V, R>), dim3(grid), dim3(256), 0, st, x, g, b, (OT*)y, rows, D, G, Gs, off, eps)
+#define TMAE_LN_V(R)            \
+  if (vpl <= 1) TMAE_LN(1, R);  \
+  else if (vpl <= 2) TMAE_LN(2, R); \
+  else if (vpl <= 3) TMAE_LN(3, R); \
+  else if (vpl <= 4) TMAE_LN(4, R); \
+  else TMAE_LN(8, R);
+  if (rpw == 4) {
+    TMAE_LN_V(4)
+  } else if (rpw == 2) {
+    TMAE_LN_V(2)
+  } else {
+    TMAE_LN_V(1)
+  }
+#undef TMAE_LN_V
 #undef TMAE_LN
   TMAE_LAUNCH_CHECK("tmae_layernorm_fwd");
 }
