@@ -351,9 +351,9 @@ __device__ __forceinline__ void gemm_ring_wait(int younger) {
     asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// NS = LDS stages.  2: the next K-step's DMA in flight under the current MFMAs.  4 (small tiles with long K,
+// NS = LDS stages.  2: the next K-step's DMA in flight under the current MFMAs.  3 / 4 (small tiles, long K,
 // e.g. the 6x6 / 3x3-grid LIC convs: a 32x64 tile's K-step is a few MFMAs, so a 2-stage ring pays the
-// whole DMA latency every step): three steps in flight.
+// whole DMA latency every step): NS - 1 steps in flight.
 template <typename T, int BN, int BM, int WGN, int NW, class WS, class XS, class EPI, int NS = 2>
 __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2)
 gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
@@ -365,7 +365,7 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
   constexpr int WJ = BN / PR, XJ = BM / PR;  // glds instructions per wave per stage
   constexpr int ROWS = BN + BM;
   static_assert(TN >= 1 && TM >= 1 && WJ >= 1 && XJ >= 1 && BN % PR == 0 && BM % PR == 0, "bad tile");
-  static_assert(NS == 2 || NS == 4, "stages");
+  static_assert(NS >= 2 && NS <= 4, "stages");
   __shared__ __attribute__((aligned(16))) uint4 lds[NS * ROWS * 8];
 
   const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
@@ -915,12 +915,13 @@ static int launch_one(const char* name, const WS& ws, const XS& xs, const EPI& e
   const int tiles = ceil_div(N, BN) * ceil_div(M, BM);
   if (tiles == 0 || n1 * n2 == 0) return TMAE_OK;
   if constexpr (GLDS) {
-    // small tiles (<= 160 LDS rows: 4 stages stay within two workgroups per CU) over a long K take the
-    // 4-stage ring (TMAE_GEMM_DEEP=0 disables)
-    constexpr bool deep_ok = sizeof(T) == 2 && NW == 4 && BN + BM <= 160;
+    // small tiles over a long K take a 4-stage (<= 160 LDS rows) or 3-stage (<= 213 rows) ring: either stays
+    // within 80 KB, two workgroups per CU (TMAE_GEMM_DEEP=0 disables)
+    constexpr int DNS = (BN + BM) * 128 * 4 <= 80 * 1024 ? 4 : (BN + BM) * 128 * 3 <= 80 * 1024 ? 3 : 2;
+    constexpr bool deep_ok = sizeof(T) == 2 && NW == 4 && DNS > 2;
     if constexpr (deep_ok) {
       if (ceil_div(K, 8 * Elt<T>::EPC) >= 8 && gemm_knob("TMAE_GEMM_DEEP", 1)) {
-        hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, NW, WS, XS, EPI, 4>), dim3(tiles, n1 * n2),
+        hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, NW, WS, XS, EPI, DNS>), dim3(tiles, n1 * n2),
                            dim3(64 * NW), 0, st, ws, xs, epi, M, N, K, n2, 0);
         TMAE_LAUNCH_CHECK(name);
       }
