@@ -347,7 +347,8 @@ mha_fwd_bf16_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
   const bf16* base = qkv + (size_t)b * Tn * ld + h * DH;
   const int tid = threadIdx.x, nthr = blockDim.x;
   // K and V row-major, 16-B chunks; every load of a thread issued before its first LDS store
-  constexpr int MAXC = 8;  // chunks per thread per operand (Tpad * CPR <= nthr * MAXC)
+  // chunks per thread per operand: Tpad * DH / 8 chunks over 2 * Tpad threads
+  constexpr int MAXC = DH / 16;
   uint4 kv[MAXC], vv[MAXC];
 #pragma unroll
   for (int u = 0; u < MAXC; ++u) {
@@ -390,7 +391,7 @@ static int mha_launch(const void* qkv, void* out, int B, int Tn, int H, float sc
   const size_t lds = lean ? ((size_t)Tpad * (DH + 8) + (size_t)Tpad * AttnTr<DH>::LDV) * 2
                           : ((size_t)Tpad * (DH + AttnCfg<T>::KPAD) + (size_t)DH * (Tpad + AttnCfg<T>::VPAD)) * sizeof(T);
   TMAE_REQUIRE(nthr <= 1024 && lds <= 160 * 1024, "tmae_mha_fwd: sequence length %d too long", Tn);
-  TMAE_REQUIRE(!lean || Tpad * (DH / 8) <= nthr * 8, "tmae_mha_fwd: sequence length %d too long", Tn);
+  TMAE_REQUIRE(!lean || Tpad * (DH / 8) <= nthr * (DH / 16), "tmae_mha_fwd: sequence length %d too long", Tn);
   if (B * H == 0 || Tn == 0) return TMAE_OK;
   if (lean)
     hipLaunchKernelGGL((mha_fwd_bf16_kernel<DH>), dim3(B * H), dim3(nthr), lds, st, (const bf16*)qkv, (bf16*)out, lse,
