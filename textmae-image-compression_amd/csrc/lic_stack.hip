@@ -60,6 +60,9 @@ struct LstkOut {
   int ldy2;
 };
 
+#ifndef LSTK_OPT
+#define LSTK_OPT 0  // A/B builds: 1 = 8-B GELU epilogue stores (no permlane16_swap pairing)
+#endif
 #ifndef LSTK_DIAG
 #define LSTK_DIAG 0  // phase isolation builds (tools/lstk_diag.sh): 4 = no MFMA, 8 = no B reads, 16 = no A loads,
                      // 32 = no epilogue
@@ -204,16 +207,37 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
 #pragma unroll
         for (int j = 0; j < MF; ++j) acc[i][j] += ad[i][j];
     }
-#pragma unroll
-    for (int i = 0; i < NF; ++i)
+    auto gelu4 = [&](int i, int j) {
+      const f32x4 v = acc[i][j] + bias[i];
+      const f32x2 lo = gelu2_bf16out(v.xy), hi = gelu2_bf16out(v.zw);
+      bf16x4 q;
+      q[0] = (bf16)lo.x; q[1] = (bf16)lo.y; q[2] = (bf16)hi.x; q[3] = (bf16)hi.y;
+      return q;
+    };
+    if (NF == 2 && (L.cout & 7) == 0 && !(LSTK_OPT & 1)) {
+      // v_permlane16_swap pairs lane rows (fq, fq ^ 1): even rows gather 8 consecutive channels of
+      // fragment 0, odd rows of fragment 1, so each lane stores 16 B per pixel fragment (one ds_write_b128
+      // instead of two ds_write_b64 with 4-way bank conflicts)
+      const int ch = 16 * (f0 + (fq & 1)) + 4 * (fq & 2);
+      const bool okw = ch < L.cout;
 #pragma unroll
       for (int j = 0; j < MF; ++j) {
-        const f32x4 v = acc[i][j] + bias[i];
-        const f32x2 lo = gelu2_bf16out(v.xy), hi = gelu2_bf16out(v.zw);
-        bf16x4 q;
-        q[0] = (bf16)lo.x; q[1] = (bf16)lo.y; q[2] = (bf16)hi.x; q[3] = (bf16)hi.y;
-        if (okc[i] && pix(j) < npix) *reinterpret_cast<bf16x4*>(lb + out_off + pix(j) * pout + 2 * cc[i]) = q;
+        const bf16x4 qa = gelu4(0, j), qb = gelu4(NF - 1, j);
+        const uint2 ua = *reinterpret_cast<const uint2*>(&qa), ub = *reinterpret_cast<const uint2*>(&qb);
+        const auto r0 = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+        if (okw && pix(j) < npix)
+          *reinterpret_cast<uint4*>(lb + out_off + pix(j) * pout + 2 * ch) = uint4{r0[0], r1[0], r0[1], r1[1]};
       }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NF; ++i)
+#pragma unroll
+        for (int j = 0; j < MF; ++j) {
+          const bf16x4 q = gelu4(i, j);
+          if (okc[i] && pix(j) < npix) *reinterpret_cast<bf16x4*>(lb + out_off + pix(j) * pout + 2 * cc[i]) = q;
+        }
+    }
   } else if (o.src) {  // lrp: y_hat = y_hat_pre + 0.5 tanh(lrp)
     f32x4 sv[NF][MF];
 #pragma unroll
