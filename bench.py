@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--train-warmup", type=int, default=3)
     ap.add_argument("--train-batch", type=int, default=64)
     ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--no-k64", dest="k64_line", action="store_false", help="skip the K=64 (config 2') line")
     ap.add_argument("--kernel-reps", type=int, default=0, help="unused (kept for older command lines)")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for a one-GPU rehearsal)")
     return ap.parse_args()
@@ -143,6 +144,10 @@ class LaunchTimer:
         self.calls = []
         self.conv_bytes = 0
         self.stack_bytes = 0
+        self.hbm_bytes = {}  # memory-bound families: algorithmic HBM bytes per forward
+
+    def _hbm(self, fam, nbytes):
+        self.hbm_bytes[fam] = self.hbm_bytes.get(fam, 0) + nbytes
 
     def classify(self, name, a):
         B, E, Dd, Te, Td = self.B, self.E, self.Dd, self.Te, self.Td
@@ -162,7 +167,10 @@ class LaunchTimer:
             return "lic_1x1_gemm", fl
         if name == "tmae_mha_fwd":
             Bq, T, H, dh = a[2], a[3], a[4], a[5]
-            return ("enc_attn_core" if T == Te else "dec_attn_core"), 4.0 * Bq * H * T * T * dh
+            fam = "enc_attn_core" if T == Te else "dec_attn_core"
+            es = 2 if a[7] == 1 else 4
+            self._hbm(fam, Bq * T * H * dh * es * 4)  # qkv in (3 x), o out
+            return fam, 4.0 * Bq * H * T * T * dh
         if name == "tmae_conv3x3":
             c = a[0]._obj
             Ho = (c.H + 2 - 3) // c.stride + 1
@@ -196,7 +204,19 @@ class LaunchTimer:
         if name in ("tmae_decoder_pred_fwd", "tmae_decoder_pred_cp_fwd"):
             return "dec_pred", 2.0 * a[4] * a[5] * a[6] * a[7] * a[10] * a[10]
         if name == "tmae_layernorm_fwd":
+            rows, D = a[4], a[5]
+            self._hbm("layernorm", rows * D * (4 + (2 if a[10] == 1 else 4)) + 2 * D * 4)  # x f32 in, y out, gamma/beta
             return "layernorm", 0.0
+        if name == "tmae_gc_slices_fwd":
+            # y, mu, sigma in, likelihood out (f32), y_hat_pre out (operand dtype) and its f32 copy, noise in
+            n_el = a[15] * a[16] * a[17] * a[18]
+            per = 16 + ((2 if a[11] == 1 else 4) if a[10] else 0) + (4 if a[13] else 0) + (4 if a[7] else 0)
+            self._hbm("gc_slices", n_el * per)
+            return "gc_slices", 0.0
+        if name == "tmae_eb_likelihood_fwd":
+            n_el = a[7] * a[8] * a[9]  # z in, likelihood out (f32), z_hat out, noise in
+            self._hbm("eb_likelihood", n_el * (8 + ((2 if a[5] == 1 else 4) if a[4] else 0) + (4 if a[2] else 0)))
+            return "eb_likelihood", 0.0
         return "other:" + name, 0.0
 
     def describe(self, name, a):
@@ -244,8 +264,8 @@ class LaunchTimer:
         except Exception:
             pass
         for fam, (launches, fl) in fams.items():
-            if fl <= 0 and fam != "layernorm":
-                continue  # entropy models / ids / copies: not replayed (state-carrying, tiny)
+            if fl <= 0 and fam not in self.hbm_bytes:
+                continue  # ids / copies / state-carrying entropy-model steps: not replayed
             launches = [(name, args[:-1] + (st.cuda_stream,)) for name, args in launches]  # stream is the last arg
             for name, args in launches:  # warm
                 orig(name, *args)
@@ -304,16 +324,60 @@ def roofline_report(m, imgs, scores, batch, dump=None):
     if dom in ("lic_conv3x3", "lic_stack"):
         roof["algorithmic_bytes_per_launch"] = int((lt.conv_bytes if dom == "lic_conv3x3" else lt.stack_bytes)
                                                    / max(d["launches"], 1))
-    pmc = os.path.join(ROOT, "profiles", "r02", "pmc_dominant.json")
-    if os.path.exists(pmc):
-        try:
-            j = json.load(open(pmc))
-            if j.get("family") == dom:
-                roof["traffic"] = j.get("hbm_bytes_per_launch")
-                roof["traffic_source"] = os.path.relpath(pmc, ROOT)
-        except Exception:
-            pass
+    # HBM counters (two rocprofv3 PMC passes, tools/pmc_family.py) and the graph-replayed forward's kernel trace
+    # (tools/family_summary.py --forward), both committed under profiles/ from a run of this code
+    pmc, pmc_src = _committed("pmc_families.json")
+    trace, trace_src = _committed("trace_families.json")
+    fam_pmc = (pmc or {}).get("per_family", {})
+    if dom in fam_pmc:
+        roof["traffic"] = fam_pmc[dom]["hbm_bytes_per_launch"]
+        roof["traffic_source"] = pmc_src
+    fwd = (trace or {}).get("forward", {}).get("families", {})
+    rep = (trace or {}).get("replay", {}).get("families", {})
+    if dom in fwd:
+        us = fwd[dom]["avg_launch_us"]
+        roof["frac_in_forward"] = round(roof["flops_per_launch"] / (us * 1e-6) / PEAK_BF16, 4)
+        roof["avg_launch_us_in_forward"] = us
+        roof["trace_source"] = trace_src
+    if dom in rep:
+        roof["avg_launch_us_replay_trace"] = rep[dom]["avg_launch_us"]
+    # memory-bound families against the HBM roofline: algorithmic bytes / replayed kernel time
+    hbm = {}
+    for f, nbytes in sorted(lt.hbm_bytes.items()):
+        if f not in fam:
+            continue
+        n, t = fam[f][0], fam[f][1]
+        gbs = nbytes / t / 1e9 if t > 0 else 0.0
+        e = {"launches": n, "time_us": round(t * 1e6, 1), "algorithmic_bytes_per_launch": int(nbytes / max(n, 1)),
+             "achieved": round(gbs, 1), "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": round(gbs * 1e9 / PEAK_HBM, 4)}
+        if f in fam_pmc:
+            e["traffic"] = fam_pmc[f]["hbm_bytes_per_launch"]
+            e["traffic_over_algorithmic"] = round(e["traffic"] / max(e["algorithmic_bytes_per_launch"], 1), 3)
+        if f in fwd:
+            e["avg_launch_us_in_forward"] = fwd[f]["avg_launch_us"]
+            e["frac_in_forward"] = round(nbytes / max(n, 1) / (fwd[f]["avg_launch_us"] * 1e-6) / PEAK_HBM, 4)
+        hbm[f] = e
+    roof["hbm_bound"] = hbm
+    if pmc_src or trace_src:
+        roof["sources"] = {"pmc": pmc_src, "trace": trace_src}
     return roof
+
+
+def _committed(name):
+    """the newest profiles/rNN/<name> (committed evidence), parsed, and its repo-relative path"""
+    base = os.path.join(ROOT, "profiles")
+    try:
+        rounds = sorted(d for d in os.listdir(base) if d.startswith("r") and d[1:].isdigit())
+    except OSError:
+        return None, None
+    for d in reversed(rounds):
+        p = os.path.join(base, d, name)
+        if os.path.exists(p):
+            try:
+                return json.load(open(p)), os.path.relpath(p, ROOT)
+            except Exception:
+                return None, None
+    return None, None
 
 
 def train_bench(model, args, rank, world, dev, barrier):
@@ -321,6 +385,7 @@ def train_bench(model, args, rank, world, dev, barrier):
     bpp; VGG needs a weight download), aux loss, backward (HIP reverse pass; for world > 1 the RCCL
     gradient all-reduce runs inside it, bucketed), clip_grad_norm_(1.0), Adam, aux backward, aux Adam"""
     from textmae_amd import engine
+    from textmae_amd.data import SyntheticCropSet
     from textmae_amd.optim import configure_optimizers
     from textmae_amd.parallel import enable_data_parallel
     from textmae_amd.rd_loss import RateDistortionLoss
@@ -331,10 +396,15 @@ def train_bench(model, args, rank, world, dev, barrier):
         enable_data_parallel(model)
     opt, aux_opt = configure_optimizers(model, lr=1e-4, aux_lr=1e-4, fused=True)
     crit = RateDistortionLoss(lmbda=1e-2)
-    L = model.encoder_embed.num_patches
-    imgs, scores = synthetic_inputs(args.train_batch, args.img, L, 2000 + rank, dev)
+    # BASELINE config 3's input: per rank, seeded DIV2K-shaped uint8 images (2040 x 1356) resident in HBM and
+    # a fresh random 256^2 crop per sample per step, ToTensor + Normalize on the device (data.py); seed =
+    # base + rank as training.py:109 seeds its processes
+    data = SyntheticCropSet(dev, seed=2000, rank=rank, crop=args.img,
+                            patch_size=model.encoder_embed.patch_size[0]).plan(args.train_warmup + args.train_steps,
+                                                                               args.train_batch)
 
     def step():
+        imgs, scores = data.next()
         return engine.train_step(model, crit, imgs, scores, opt, aux_opt, clip_max_norm=1.0)
 
     for _ in range(args.train_warmup):
@@ -353,6 +423,8 @@ def train_bench(model, args, rank, world, dev, barrier):
             + ")", "value": round(ips, 2), "unit": "images/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
             "steps": args.train_steps, "warmup": args.train_warmup, "per_gpu_batch": args.train_batch,
             "global_batch": args.train_batch * world, "parallelism": f"dp{world}", "dtype": "bf16",
+            "data": f"DIV2K-shaped: {data.images.shape[0]} seeded uint8 2040x1356 images per rank (seed 2000 + rank), "
+                    f"a random {args.img}^2 crop per sample per step, normalised on the device",
             "loss_last": round(float(out["loss"].detach()), 6), "gflop_per_image": round(fl, 2),
             "step_mfma_frac": round(ips * fl * 1e9 / (world * PEAK_BF16), 4), "hip_graph": False}
 
@@ -369,9 +441,12 @@ def _cpu_model():
 
 def cpu_baseline(args, model_kwargs):
     """the oracle (CPU restatement of MCM.forward, fp32) on the host cores over a bounded
-    sample of the same workload: batch 8 at every thread the process is given, and at 1 thread (the
-    reference eval convention, testing.py:29); plus the reference-semantics get_ids_shuffle alone
-    (the C restatement of MCM.py:364-423, batch 64)."""
+    sample of the same workload (batches of 8), timed per batch and reported at the median:
+      * at torch.set_num_threads(os.cpu_count()) -- §8(d)'s setting;
+      * at the thread count the process is given (OMP_NUM_THREADS; the box's CPU share);
+      * at 1 thread, the reference eval convention (testing.py:29);
+    ``value`` / ``cores`` are the faster of the first two.  Plus the reference-semantics get_ids_shuffle
+    alone (the C restatement of MCM.py:364-423, batch 64, 1 thread)."""
     import numpy as np
 
     from oracle import ids as ids_oracle
@@ -382,22 +457,29 @@ def cpu_baseline(args, model_kwargs):
     L = (cfg.img_size // cfg.patch_size) ** 2
     nb = args.cpu_batch
     x, s = synthetic_inputs(nb, cfg.img_size, L, 0, "cpu")
-    nthreads = torch.get_num_threads()
-    n, t0 = 0, time.perf_counter()
-    while True:
-        mcm_forward(sd, cfg, x, s)
-        n += nb
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds:
-            break
-    all_ips = n / el
-    torch.set_num_threads(1)
+    default_threads = torch.get_num_threads()
+
+    def leg(threads, seconds, max_batches=1000):
+        torch.set_num_threads(threads)
+        ts, t0 = [], time.perf_counter()
+        while len(ts) < max_batches:
+            t1 = time.perf_counter()
+            mcm_forward(sd, cfg, x, s)
+            ts.append(time.perf_counter() - t1)
+            if time.perf_counter() - t0 >= seconds:
+                break
+        ts.sort()
+        med = ts[len(ts) // 2] if len(ts) % 2 else 0.5 * (ts[len(ts) // 2 - 1] + ts[len(ts) // 2])
+        return {"threads": threads, "images_per_s_median": round(nb / med, 3), "batches": len(ts),
+                "images_per_s_mean": round(nb * len(ts) / sum(ts), 3)}
+
     try:
-        t1 = time.perf_counter()
-        mcm_forward(sd, cfg, x, s)
-        one_ips = nb / (time.perf_counter() - t1)
+        legs = {"all_host_cpus": leg(os.cpu_count() or default_threads, args.cpu_seconds),
+                "process_threads": leg(default_threads, args.cpu_seconds),
+                "one_thread": leg(1, 0.0, max_batches=1)}
     finally:
-        torch.set_num_threads(nthreads)
+        torch.set_num_threads(default_threads)
+    best = max(("all_host_cpus", "process_threads"), key=lambda k: legs[k]["images_per_s_median"])
     s64 = torch.rand(64, L, generator=torch.Generator().manual_seed(5)).numpy().astype(np.float32)
     ids_oracle.ids_shuffle(s64, cfg.num_keep_patches)
     reps, t2 = 0, time.perf_counter()
@@ -409,11 +491,78 @@ def cpu_baseline(args, model_kwargs):
         aff = len(os.sched_getaffinity(0))
     except Exception:
         aff = None
-    return {"value": round(all_ips, 3), "unit": "images/s", "cores": nthreads, "kind": "port",
-            "sample": f"{n} images (oracle MCM.forward, fp32, batches of {nb} at {cfg.img_size}^2, "
-                      f"K={cfg.num_keep_patches}) in {el:.1f}s on {nthreads} threads; 1 thread: one batch of {nb}",
-            "value_1thread": round(one_ips, 3), "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
-            "affinity_cpus": aff, "ids_shuffle_ms_per_batch64_1thread": round(ids_ms, 3)}
+    return {"value": legs[best]["images_per_s_median"], "unit": "images/s", "cores": legs[best]["threads"],
+            "kind": "port",
+            "sample": f"oracle MCM.forward (fp32 torch CPU restatement) on batches of {nb} at {cfg.img_size}^2, "
+                      f"K={cfg.num_keep_patches}, timed per batch, median; ~{args.cpu_seconds:.0f} s per multi-thread "
+                      f"leg, one batch at 1 thread; value = the faster of os.cpu_count() and the process's threads",
+            "legs": legs, "value_1thread": legs["one_thread"]["images_per_s_median"], "cpu_model": _cpu_model(),
+            "host_cpus": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "ids_shuffle_ms_per_batch64_1thread": round(ids_ms, 3)}
+
+
+def time_forward(model, imgs, scores, steps, warmup, use_graph, world, dev, backend, barrier):
+    """the timed region: `warmup` untimed forwards, then exactly `steps` forwards (replays of one HIP graph)
+    between barrier + synchronize on both sides; returns (max-over-ranks wall seconds, median step ms from
+    per-step HIP events recorded on the stream -- no host sync inside the region)"""
+    graph = None
+    with torch.no_grad():
+        if use_graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(2):
+                    model(imgs, scores)
+            torch.cuda.current_stream().wait_stream(s)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                model(imgs, scores)
+
+            def step():
+                graph.replay()
+        else:
+            def step():
+                model(imgs, scores)
+
+        for _ in range(warmup):
+            step()
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        evs[0].record()
+        for i in range(steps):
+            step()
+            evs[i + 1].record()
+        torch.cuda.synchronize()
+        barrier()
+        el = max_over_ranks(time.perf_counter() - t0, world, dev, backend)
+    ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(steps))
+    med = ms[len(ms) // 2] if len(ms) % 2 else 0.5 * (ms[len(ms) // 2 - 1] + ms[len(ms) // 2])
+    del graph
+    return el, med
+
+
+def k64_line(args, dev, world, rank, barrier, dtype):
+    """SURVEY §8(d) config 2's secondary point: the same ViT-B model at K=64 kept patches (mask 0.75, g=8),
+    batch 64, timed exactly like the main line"""
+    import textmae_amd
+
+    torch.manual_seed(0)
+    m = textmae_amd.MCM(img_size=args.img, num_keep_patches=64).to(dev).eval()
+    m.compute_dtype = dtype
+    m.distortion = "none"
+    L = m.encoder_embed.num_patches
+    imgs, scores = synthetic_inputs(args.batch, args.img, L, 1000 + rank, dev)
+    el, med = time_forward(m, imgs, scores, args.steps, args.warmup, not args.no_graph, world, dev, args.backend,
+                           barrier)
+    gf = sum(gflop_per_image(m).values())
+    v = world * args.batch * args.steps / el
+    del m
+    torch.cuda.empty_cache()
+    return {"workload": "MCM forward eval, ViT-B/16, K=64 of 256 patches (g=8)", "value": round(v, 2),
+            "unit": "images/s", "ms_per_step": round(el / args.steps * 1e3, 3), "ms_per_step_median": round(med, 3),
+            "gflop_per_image": round(gf, 3), "step_mfma_frac": round(v * gf * 1e9 / (world * PEAK_BF16), 4)}
 
 
 def max_over_ranks(el, world, dev, backend):
@@ -424,10 +573,40 @@ def max_over_ranks(el, world, dev, backend):
     return float(t.item())
 
 
+def _free_port():
+    import socket
+
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    return port
+
+
+def launch_ranks(args):
+    """``--gpus N`` (N > 1) without a torch.distributed launcher: start the N ranks here, one process per
+    GPU, through torch.distributed.run on 127.0.0.1, and return its exit code.  The parent never touches
+    the GPU (torch.cuda.device_count() does not initialise it), so nothing is exec'ed after a GPU call."""
+    import subprocess
+
+    if args.backend == "nccl" and torch.cuda.device_count() < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
     local = int(os.environ.get("LOCAL_RANK", 0))
     local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
@@ -458,39 +637,15 @@ def main():
     gf = gflop_per_image(model)
     gf_img = sum(gf.values())
 
-    graph = None
-    with torch.no_grad():
-        if args.no_graph:
-            def step():
-                model(imgs, scores)
-        else:
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                for _ in range(2):
-                    model(imgs, scores)
-            torch.cuda.current_stream().wait_stream(s)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                model(imgs, scores)
-
-            def step():
-                graph.replay()
-
-        for _ in range(args.warmup):
-            step()
-        barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        barrier()
-        el = max_over_ranks(time.perf_counter() - t0, world, dev, args.backend)
+    el, med_ms = time_forward(model, imgs, scores, args.steps, args.warmup, not args.no_graph, world, dev, args.backend,
+                              barrier)
     roof = None
     if rank == 0 and not args.no_roofline:
         roof = roofline_report(model, imgs, scores, args.batch, dump=args.dump_launches)
-    graph = None
+
+    k64 = None
+    if args.k64_line and args.keep == 144 and args.enc_dim == 768 and args.enc_depth == 12:
+        k64 = k64_line(args, dev, world, rank, barrier, dtype)
 
     train = None
     if not args.no_train and args.train_steps > 0:
@@ -500,7 +655,9 @@ def main():
     value = world * args.batch * args.steps / el
     rec = {
         "metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+        "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 3),
+        "ms_per_step_median": round(med_ms, 3), "value_at_median": round(world * args.batch / (med_ms * 1e-3), 2),
+        "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (seeded uniform RGB, "
         "ImageNet-normalised; uniform patch scores; seeded random-init weights)",
         "config": {"workload": ("MCM forward eval: ids+ViT-B/16 enc" if vitb else
@@ -514,6 +671,8 @@ def main():
         "step_mfma_frac": round(value * gf_img * 1e9 / (world * PEAK_BF16), 4),
         "roofline": roof,
     }
+    if k64 is not None:
+        rec["config2_k64"] = k64
     if train is not None:
         rec["train"] = train
     if rank == 0:

@@ -205,6 +205,13 @@ int tmae_bpp_sum(const float* y_lik, long long ny, const float* z_lik, long long
 /* layout helper: NHWC (channel stride ldx) -> NCHW */
 int tmae_nhwc_to_nchw(const float* x, int ldx, float* y, int n, int C, int HW, void* stream);
 
+/* training-set loader sample (training.py:115-129, utils/dataloader.py:58-61: ToTensor + Normalize) on
+ * device-resident uint8 HWC images [nsrc][H][W][3]: out[b] = (crop / 255 - mean) / std, NCHW f32 [B][3][S][S];
+ * crops [B][3] int32 device = (image, top, left), each crop inside its image (caller's contract).
+ * mean / std: 3 host floats each. */
+int tmae_crop_normalize_u8(const unsigned char* src, int nsrc, int H, int W, const int* crops, int B, int S,
+                           const float* mean, const float* std, float* out, void* stream);
+
 /* ---------------------------------------------------------------- MaskedAutoencoderViT (models/MAE/models_mae.py)
  * random_masking (123-148): ids_shuffle = stable ascending argsort(noise) per row, ids_restore = its
  * inverse, mask[b][l] = 1 where rank >= len_keep (mask may be NULL).  L <= 2048. */

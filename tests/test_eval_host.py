@@ -92,3 +92,28 @@ def test_ms_ssim_oracle_identity():
 
     x = torch.rand(1, 3, 224, 224, generator=torch.Generator().manual_seed(1)) * 255
     assert float(ms_ssim(x, x, data_range=255)) == pytest.approx(1.0, abs=1e-6)
+
+
+def test_load_checkpoint_reference_save_model_layout(tmae, tmp_path):
+    """testing.load_checkpoint reads what the reference's save_model writes (model_utils.py:30-55):
+    {'model', 'optimizer', 'aux_optimizer', 'epoch', 'scaler', 'args': argparse.Namespace}, weights-only"""
+    import argparse
+
+    import torch
+
+    from textmae_amd import testing
+
+    kw = dict(encoder_embed_dim=64, encoder_depth=1, encoder_num_heads=2, decoder_embed_dim=32, decoder_depth=1,
+              decoder_num_heads=2, latent_depth=48, hyperprior_depth=24)
+    torch.manual_seed(0)
+    m = tmae.MCM(img_size=64, num_keep_patches=16, **kw)
+    opt = torch.optim.Adam([p for n, p in m.named_parameters() if not n.endswith(".quantiles")], lr=1e-4)
+    aux = torch.optim.Adam([p for n, p in m.named_parameters() if n.endswith(".quantiles")], lr=1e-4)
+    ck = {"model": m.state_dict(), "optimizer": opt.state_dict(), "aux_optimizer": aux.state_dict(), "epoch": 3,
+          "scaler": {"scale": 65536.0, "growth_factor": 2.0}, "args": argparse.Namespace(lr=1e-4, batch_size=8)}
+    path = tmp_path / "best_model.pth"
+    torch.save(ck, path)
+    net = testing.load_checkpoint(16, str(path), img_size=64, **kw)
+    got = net.state_dict()
+    for k, v in m.state_dict().items():
+        assert torch.equal(got[k], v), k

@@ -27,6 +27,7 @@ import pytest
 import torch
 
 from oracle.mcm_oracle import MCMConfig, make_state_dict, mcm_forward
+from parity_log import check, record
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -90,14 +91,18 @@ def _check_f32(m, cfg, sd, imgs, scores):
     clean = [e for e, f in zip(per_img, flips.tolist()) if f == 0]
     print(f"B={B} K={cfg.num_keep_patches}: flips per image {flips.tolist()}; worst clean x_hat err "
           f"{max(clean):.2e}; worst overall {max(per_img):.2e}")
+    record("images_with_rounding_flips", int((flips > 0).sum()), 2, flips=int(flips.sum()))
     assert int((flips > 0).sum()) <= 2 and int(flips.sum()) <= max(1, int(1e-5 * B * n_lat)), flips.tolist()
-    assert max(clean) < 1e-3
+    check("x_hat_maxrel_clean_images", max(clean), 1e-3, excluded_images=int((flips > 0).sum()))
     ylik, rlik = out["likelihoods"]["y"].double().cpu(), ref.y_likelihood.double()
-    assert float(((ylik - rlik).abs() > 1e-3 * rlik.abs() + 1e-7).double().mean()) <= 1e-3
-    assert _maxrel(out["likelihoods"]["z"], ref.z_likelihood) < 1e-3
+    record("y_lik_maxrel_all", float(((ylik - rlik).abs() / (rlik.abs() + 1e-7)).max()))
+    check("y_lik_frac_outside_1e-3", float(((ylik - rlik).abs() > 1e-3 * rlik.abs() + 1e-7).double().mean()), 1e-3,
+          strict=False)
+    check("z_lik_maxrel", _maxrel(out["likelihoods"]["z"], ref.z_likelihood), 1e-3)
     px = B * imgs.shape[2] * imgs.shape[3]
     b_ref = _bpp(ref.y_likelihood, ref.z_likelihood, px)
-    assert abs(_bpp(out["likelihoods"]["y"], out["likelihoods"]["z"], px) - b_ref) <= 1e-3 * abs(b_ref)
+    check("bpp_rel", abs(_bpp(out["likelihoods"]["y"], out["likelihoods"]["z"], px) - b_ref) / abs(b_ref), 1e-3,
+          strict=False)
     return ref
 
 
@@ -125,6 +130,11 @@ def test_bench_config_k64_f32_batch64(tmae, scores_kind):
     if scores_kind == "tie_heavy":
         scores = tie_heavy_scores(64, 256, 8)
     _check_f32(m, cfg, sd, imgs, scores)
+
+
+# bf16 bounds: about 2x the errors measured on the GPU (profiles/r03/parity_metrics.jsonl)
+BF16_XHAT_RELL2 = 3e-2
+BF16_BPP_REL = 3e-2
 
 
 def _graph_forward(m, imgs, scores):
@@ -164,10 +174,12 @@ def test_bench_config_bf16_graph_batch64(vitb64, scores_kind):
         xh = out["x_hat"].double().cpu()
         per = [float((xh[b] - ref.x_hat[b].double()).norm() / ref.x_hat[b].double().norm()) for b in range(64)]
         print(f"bf16 graph vs oracle: per-image rel L2 max {max(per):.2e} mean {np.mean(per):.2e}")
-        assert max(per) < 3e-2
+        record("x_hat_relL2_mean_bf16", float(np.mean(per)))
+        check("x_hat_relL2_max_bf16", max(per), BF16_XHAT_RELL2)
         px = 64 * 256 * 256
         b_ref = _bpp(ref.y_likelihood, ref.z_likelihood, px)
-        assert abs(_bpp(out["likelihoods"]["y"], out["likelihoods"]["z"], px) - b_ref) <= 3e-2 * abs(b_ref)
+        check("bpp_rel_bf16", abs(_bpp(out["likelihoods"]["y"], out["likelihoods"]["z"], px) - b_ref) / abs(b_ref),
+              BF16_BPP_REL, strict=False)
         del graph
     finally:
         m.compute_dtype = torch.float32
@@ -201,5 +213,5 @@ def test_config4_vitl_bench_batch_bf16(tmae):
     xh = out["x_hat"][pick].double().cpu()
     per = [float((xh[i] - ref.x_hat[i].double()).norm() / ref.x_hat[i].double().norm()) for i in range(3)]
     print(f"config 4 bf16 (batch 128) vs oracle: {per}")
-    assert max(per) < 3e-2
+    check("x_hat_relL2_max_bf16_cfg4", max(per), BF16_XHAT_RELL2)
     assert torch.isfinite(out["likelihoods"]["y"]).all() and torch.isfinite(out["likelihoods"]["z"]).all()

@@ -7,6 +7,7 @@ import os
 import numpy as np
 import pytest
 import torch
+from parity_log import check  # noqa: E402
 import torch.nn.functional as F
 
 from oracle import ids as ids_oracle
@@ -70,7 +71,7 @@ def test_layernorm(tmae, D, dtype):
     y = tmae.ops.layernorm(x.to(DEV), w.to(DEV), b.to(DEV), 1e-6, dtype, rows=3 * 36, row_group=36,
                            group_stride=37, row_offset=1)
     ref = F.layer_norm(x[:, 1:], (D,), w, b, 1e-6).reshape(-1, D)
-    assert rel(y.float(), ref) < tol(dtype)
+    check("rel:y_float", rel(y.float(), ref), tol(dtype))
 
 
 # bench-sized row counts, ragged against the 4-row block (with TMAE_LN_RPW=4 they take the 2- and 4-rows-per-wave
@@ -96,7 +97,7 @@ def test_linear(tmae, M, N, K, dtype, act):
     ref = F.linear(x.to(dtype).float(), w.to(dtype).float(), b)
     if act:
         ref = F.gelu(ref)
-    assert rel(y.float(), ref) < tol(dtype)
+    check("rel:y_float", rel(y.float(), ref), tol(dtype))
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
@@ -105,11 +106,11 @@ def test_linear_f32_source_and_residual(tmae, dtype):
     M, N, K = 500, 384, 512
     x, w, b = torch.randn(M, K), torch.randn(N, K) / K ** 0.5, torch.randn(N)
     y = tmae.ops.linear(x.to(DEV), w.to(DEV).to(dtype), b.to(DEV), dtype, out_dtype=torch.float32)
-    assert rel(y, F.linear(x.to(dtype).float(), w.to(dtype).float(), b)) < tol(dtype)
+    check("rel:y", rel(y, F.linear(x.to(dtype).float(), w.to(dtype).float(), b)), tol(dtype))
     r0 = torch.randn(M, N)
     r = r0.to(DEV).clone()
     tmae.ops.linear_residual(x.to(DEV).to(dtype), w.to(DEV).to(dtype), b.to(DEV), r, dtype)
-    assert rel(r, r0 + F.linear(x.to(dtype).float(), w.to(dtype).float(), b)) < tol(dtype)
+    check("rel:r", rel(r, r0 + F.linear(x.to(dtype).float(), w.to(dtype).float(), b)), tol(dtype))
 
 
 def _ref_attn(qkv, B, T, H, dh):
@@ -125,7 +126,7 @@ def test_mha(tmae, B, T, H, dh, dtype):
     torch.manual_seed(T)
     qkv = torch.randn(B * T, 3 * H * dh) * 1.5
     out = tmae.ops.mha(qkv.to(dtype).to(DEV), B, T, H, dh, dh ** -0.5, dtype)
-    assert rel(out.float(), _ref_attn(qkv.to(dtype).float(), B, T, H, dh)) < (1e-4 if dtype == torch.float32 else 3e-2)
+    check("rel:out_float", rel(out.float(), _ref_attn(qkv.to(dtype).float(), B, T, H, dh)), (1e-4 if dtype == torch.float32 else 3e-2))
 
 
 # ------------------------------------------------------------------------------------ convs
@@ -155,7 +156,7 @@ def test_conv3x3_two_segments(tmae, stride, dtype, H):
     y = torch.empty(n * Ho * Ho, cout, device=DEV)
     tmae.ops.conv3x3(_nhwc(xa, dtype), c1, c1, n, H, H, _wk(w, dtype), b.to(DEV), y, cout, cout, dtype,
                      stride=stride, act=1, x2=wide.data_ptr() + 8 * wide.element_size(), c2=c2, ld2=c2 + 16)
-    assert rel(y.view(n, Ho, Ho, cout).permute(0, 3, 1, 2), ref) < tol(dtype)
+    check("rel:y_view_n_Ho_Ho_cout_permute_0_3_1_2", rel(y.view(n, Ho, Ho, cout).permute(0, 3, 1, 2), ref), tol(dtype))
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
@@ -222,8 +223,8 @@ def test_conv3x3_lrp_epilogue(tmae, dtype):
     tmae.ops.conv3x3(_nhwc(x, dtype), cin, cin, n, H, H, _wk(w, dtype), b.to(DEV), y.data_ptr() + 40 * es, 96, cout,
                      dtype, y_f32=(dtype == torch.float32), lrp_src=s.data_ptr() + 40 * 4, ld_src=96,
                      y2=y2.data_ptr() + 16 * es, ldy2=64)
-    assert rel(y[:, 40:72].float(), ref) < tol(dtype)
-    assert rel(y2[:, 16:48].float(), ref) < tol(dtype)
+    check("rel:y_40_72_float", rel(y[:, 40:72].float(), ref), tol(dtype))
+    check("rel:y2_16_48_float", rel(y2[:, 16:48].float(), ref), tol(dtype))
     assert float(y[:, :40].abs().max()) == 0.0 and float(y[:, 72:].abs().max()) == 0.0
 
 
@@ -237,7 +238,7 @@ def test_subpel_conv(tmae, dtype):
     y = torch.empty(n * 4 * H * H, c, device=DEV)
     tmae.ops.conv3x3(_nhwc(x, dtype), cin, cin, n, H, H, _wk(w, dtype), b.to(DEV), y, c, 4 * c, dtype,
                      act=1, pixel_shuffle=True)
-    assert rel(y.view(n, 2 * H, 2 * H, c).permute(0, 3, 1, 2), ref) < tol(dtype)
+    check("rel:y_view_n_2_H_2_H_c_permute_0_3_1_2", rel(y.view(n, 2 * H, 2 * H, c).permute(0, 3, 1, 2), ref), tol(dtype))
 
 
 @pytest.mark.parametrize("training", [False, True])
@@ -263,7 +264,7 @@ def test_gc_slices(tmae, training, yt):
         sj = sigma[j].reshape(n, HW, sw).permute(0, 2, 1)
         nz = None if noise is None else noise[:, ch]
         ref = orc.gaussian_conditional(ys, sj, mj, nz)
-        assert rel(lik[:, ch].cpu(), ref) < 1e-5
+        check("rel:lik_ch_cpu", rel(lik[:, ch].cpu(), ref), 1e-5)
         q = (torch.round(ys - mj) + mj).permute(0, 2, 1).reshape(-1, sw)
         assert torch.equal(yh32[:, ch].cpu(), q)
         assert rel(yh[:, ch].float(), q) <= (0 if yt == torch.float32 else 1e-2)
@@ -292,7 +293,7 @@ def test_entropy_bottleneck(tmae, training):
     lik_ref, zhat_ref = orc.entropy_bottleneck(sd, "eb.", z, noise)
     eb = eb.to(DEV)
     out, lik = eb(z.to(DEV), training=training, noise=None if noise is None else noise.to(DEV))
-    assert rel(lik, lik_ref) < 1e-5
+    check("rel:lik", rel(lik, lik_ref), 1e-5)
     if not training:
         assert torch.equal(out.cpu(), zhat_ref)
     np.testing.assert_allclose(float(eb.loss().detach()), float(orc.eb_aux_loss(sd, "eb.")), rtol=1e-5)
@@ -308,7 +309,7 @@ def test_gaussian_conditional(tmae, training):
     gc = tmae.GaussianConditional(None).to(DEV)
     _, lik = gc(y.to(DEV), sigma.to(DEV), mu.to(DEV), training=training,
                 noise=None if noise is None else noise.to(DEV))
-    assert rel(lik, ref) < 1e-5
+    check("rel:lik", rel(lik, ref), 1e-5)
 
 
 # ------------------------------------------------------------------------------------ embed / unembed
@@ -326,7 +327,7 @@ def test_patch_embed_kept_only(tmae, dtype):
     tok = torch.zeros(n, K + 1, D, device=DEV)
     tmae.ops.patch_embed(imgs.to(DEV), shuf.to(DEV), w.view(D, -1).to(dtype).to(DEV), b.to(DEV), pos.to(DEV), tok,
                          K, P, dtype)
-    assert rel(tok[:, 1:], ref) < tol(dtype)
+    check("rel:tok_1", rel(tok[:, 1:], ref), tol(dtype))
 
 
 @pytest.mark.parametrize("ntok", [16, 17])
@@ -347,7 +348,7 @@ def test_decoder_embed_unshuffle(tmae, ntok):
     tmae.ops.decoder_embed(x.reshape(-1, Din).to(DEV), w.to(DEV), b.to(DEV), pos.to(DEV), s, out, n, ntok, L,
                            torch.float32)
     tmae.ops.mask_rows(out, mask.to(DEV), pos.to(DEV), s, n, L, ntok, D)
-    assert rel(out, ref) < 1e-5
+    check("rel:out", rel(out, ref), 1e-5)
 
 
 def test_decoder_pred_unpatchify(tmae):
@@ -358,7 +359,7 @@ def test_decoder_pred_unpatchify(tmae):
     ref = orc.unpatchify(F.linear(x, w, b).view(n, L, -1), P)
     imgs = torch.empty(n, 3, 64, 64, device=DEV)
     tmae.ops.decoder_pred(x.to(DEV), w.to(DEV), b.to(DEV), imgs, n, L, P, torch.float32)
-    assert rel(imgs, ref) < 1e-5
+    check("rel:imgs", rel(imgs, ref), 1e-5)
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
@@ -390,4 +391,34 @@ def test_block_module(tmae, dtype):
     ref = orc.block(x, sd, "b.", 4, 1e-6)
     blk = blk.to(DEV)
     blk.compute_dtype = dtype
-    assert rel(blk(x.to(DEV)), ref) < (1e-4 if dtype == torch.float32 else 3e-2)
+    check("rel:blk_x_to_DEV", rel(blk(x.to(DEV)), ref), (1e-4 if dtype == torch.float32 else 3e-2))
+
+
+# ------------------------------------------------------------------------------------ loader crops
+def test_crop_normalize_u8_bitwise_torch(tmae):
+    """the DIV2K-shaped loader sample (data.py): crop of a uint8 HWC image, ToTensor (/255) + Normalize,
+    bitwise equal to the same torch f32 ops (utils/dataloader.py:58-61)"""
+    g = torch.Generator().manual_seed(3)
+    src = torch.randint(0, 256, (3, 61, 90, 3), dtype=torch.uint8, generator=g)
+    S = 24
+    crops = torch.tensor([[0, 0, 0], [2, 61 - S, 90 - S], [1, 17, 33], [2, 5, 0], [0, 37, 66]], dtype=torch.int32)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    out = tmae.ops.crop_normalize_u8(src.to(DEV), crops.to(DEV), S, mean, std)
+    m = torch.tensor(mean).view(3, 1, 1)
+    s = torch.tensor(std).view(3, 1, 1)
+    ref = torch.stack([(src[i, t:t + S, l:l + S].permute(2, 0, 1).float().div(255) - m) / s
+                       for i, t, l in crops.tolist()])
+    assert torch.equal(out.cpu(), ref)
+
+
+def test_synthetic_crop_set_plan_is_seeded(tmae):
+    from textmae_amd.data import SyntheticCropSet
+
+    a = SyntheticCropSet(DEV, seed=5, rank=1, num_images=2, hw=(300, 400)).plan(3, 4)
+    b = SyntheticCropSet(DEV, seed=5, rank=1, num_images=2, hw=(300, 400)).plan(3, 4)
+    c = SyntheticCropSet(DEV, seed=5, rank=0, num_images=2, hw=(300, 400)).plan(3, 4)
+    xa, sa = a.next()
+    xb, sb = b.next()
+    xc, _ = c.next()
+    assert xa.shape == (4, 3, 256, 256) and sa.shape == (4, 256)
+    assert torch.equal(xa, xb) and torch.equal(sa, sb) and not torch.equal(xa, xc)

@@ -15,10 +15,12 @@ import os
 import pytest
 import torch
 import torch.nn.functional as F
+from parity_log import check, record
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 MID = [224, 176, 128, 80, 32]
+STACK_MAXREL = 2e-2  # bf16 operands; about 2x the measured error (profiles/r03/parity_metrics.jsonl)
 
 
 def _bf(t):
@@ -101,7 +103,7 @@ def test_lic_stack_vs_torch(tmae, G, c1, c2, nb, mode):
     torch.cuda.synchronize()
     err = _maxrel(got, ref)
     print(f"G={G} cin={c1}+{c2} nb={nb} {mode}: max rel err {err:.2e}")
-    assert err < 2e-2
+    check(f"lic_stack_maxrel_{mode}", err, STACK_MAXREL)
 
 
 def test_lic_stack_rejects_oversized(tmae):
@@ -159,10 +161,12 @@ def test_mcm_fused_stacks_match_layerwise(tmae):
           f"log y-lik max diff {float(ly.max()):.2e} mean {float(ly.mean()):.2e}")
     e_ms, e_lrp = _maxrel(a["musig"], b["musig"]), _maxrel(a["lrp"], b["lrp"])
     print(f"  mu/sigma (slices 6..11) max rel {e_ms:.2e}; 0.5 tanh(lrp) max rel {e_lrp:.2e}")
-    assert e_ms < 2e-2 and e_lrp < 5e-2
-    assert flips <= 1e-3 * a["yh"].numel()
-    assert xr < 2e-2
-    assert float(ly.mean()) < 2e-2
+    record("log_ylik_maxdiff", float(ly.max()))
+    check("musig_maxrel", e_ms, 2e-2)
+    check("lrp_maxrel", e_lrp, 5e-2)
+    check("y_hat_flip_frac", flips / a["yh"].numel(), 1e-3, strict=False)
+    check("x_hat_relL2", xr, 2e-2)
+    check("log_ylik_meandiff", float(ly.mean()), 2e-2)
 
 
 @pytest.mark.parametrize("training,batched", [(False, "0"), (True, "0"), (False, "1")])

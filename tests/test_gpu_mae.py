@@ -8,6 +8,7 @@ import os
 import numpy as np
 import pytest
 import torch
+from parity_log import check  # noqa: E402
 
 from oracle.mae_oracle import mae_forward
 
@@ -53,7 +54,7 @@ def test_config1_f32_vs_reference(tmae, golden):
     with torch.no_grad():
         loss, pred, mask = m(imgs.to(DEV), 0.75, noise=torch.from_numpy(golden["noise"]).to(DEV))
     np.testing.assert_array_equal(mask.cpu().numpy(), golden["mask"])
-    assert maxrel(pred[:, ::7], golden["pred_rows"]) < 1e-3
+    check("maxrel:pred_7", maxrel(pred[:, ::7], golden["pred_rows"]), 1e-3)
     np.testing.assert_allclose(pred.double().sum((1, 2)).cpu().numpy(), golden["pred_sum"],
                                rtol=1e-3, atol=1e-3 * float(np.abs(golden["pred_rows"]).max()) * pred[0].numel() ** 0.5)
     np.testing.assert_allclose(float(loss), float(golden["loss"]), rtol=1e-3)
@@ -83,7 +84,7 @@ def test_tiny_norm_pix_vs_reference(tmae, golden):
         loss, pred, mask = m(torch.from_numpy(golden["tiny_imgs"]).to(DEV), 0.6,
                              noise=torch.from_numpy(golden["tiny_noise"]).to(DEV))
     np.testing.assert_array_equal(mask.cpu().numpy(), golden["tiny_mask"])
-    assert maxrel(pred, golden["tiny_pred"]) < 1e-3
+    check("maxrel:pred", maxrel(pred, golden["tiny_pred"]), 1e-3)
     np.testing.assert_allclose(float(loss), float(golden["tiny_loss"]), rtol=1e-3)
 
 
@@ -100,12 +101,12 @@ def test_vitl_vs_oracle_and_split_api(tmae):
         rl, rp, rm = mae_forward(sd, imgs, noise, 0.75, 16, 16, 16, 24, 8)
         loss, pred, mask = m(imgs.to(DEV), 0.75, noise=noise.to(DEV))
         assert torch.equal(mask.cpu(), rm)
-        assert maxrel(pred, rp) < 1e-3
+        check("maxrel:pred", maxrel(pred, rp), 1e-3)
         np.testing.assert_allclose(float(loss), float(rl), rtol=1e-3)
         lat, mask2, rest = m.forward_encoder(imgs.to(DEV), 0.75, noise=noise.to(DEV))
         assert lat.shape == (2, 50, 1024) and lat.dtype == torch.float32 and torch.equal(mask2, mask)
         pred2 = m.forward_decoder(lat, rest)
-        assert maxrel(pred2, pred) < 1e-5
+        check("maxrel:pred2", maxrel(pred2, pred), 1e-5)
         np.testing.assert_allclose(float(m.forward_loss(imgs.to(DEV), pred2, mask2)), float(loss), rtol=1e-5)
     with pytest.raises(NotImplementedError, match="autograd"):
         m(imgs.to(DEV))  # parameters require grad and grad mode is on: no backward kernels in this build

@@ -16,6 +16,7 @@ import os
 import numpy as np
 import pytest
 import torch
+from parity_log import check  # noqa: E402
 
 from oracle.mcm_oracle import MCMConfig, make_state_dict, mcm_forward
 
@@ -65,9 +66,9 @@ def test_mcm_vs_reference_golden(golden_dir, tmae, name, cfgd, seed, mode):
     with torch.no_grad():
         out = m(imgs, torch.from_numpy(f["scores"]).to(DEV), noise=noise if mode == "train" else None)
     px = imgs.shape[0] * imgs.shape[2] * imgs.shape[3]
-    assert maxrel(out["x_hat"], f[f"{mode}_x_hat"]) < 1e-3
+    check("maxrel:out_x_hat", maxrel(out["x_hat"], f[f"{mode}_x_hat"]), 1e-3)
     assert frac_bad(out["likelihoods"]["y"], f[f"{mode}_y_lik"], 1e-3) <= 1e-3
-    assert maxrel(out["likelihoods"]["z"], f[f"{mode}_z_lik"]) < 1e-3
+    check("maxrel:out_likelihoods_z", maxrel(out["likelihoods"]["z"], f[f"{mode}_z_lik"]), 1e-3)
     got_bpp = bpp(out["likelihoods"]["y"], out["likelihoods"]["z"], px)
     assert abs(got_bpp - float(f[f"{mode}_bpp_loss"])) <= 1e-3 * abs(float(f[f"{mode}_bpp_loss"]))
     np.testing.assert_allclose(float(out["loss"][0]), f[f"{mode}_ssim_loss"], rtol=1e-3)
@@ -100,9 +101,9 @@ def test_mcm_vitb_f32_vs_oracle(vitb):
     with torch.no_grad():
         out = m(imgs.to(DEV), scores.to(DEV))
     px = 2 * 256 * 256
-    assert maxrel(out["x_hat"], ref.x_hat) < 1e-3
+    check("maxrel:out_x_hat", maxrel(out["x_hat"], ref.x_hat), 1e-3)
     assert frac_bad(out["likelihoods"]["y"], ref.y_likelihood, 1e-3) <= 1e-3
-    assert maxrel(out["likelihoods"]["z"], ref.z_likelihood) < 1e-3
+    check("maxrel:out_likelihoods_z", maxrel(out["likelihoods"]["z"], ref.z_likelihood), 1e-3)
     b_ref = bpp(ref.y_likelihood, ref.z_likelihood, px)
     assert abs(bpp(out["likelihoods"]["y"], out["likelihoods"]["z"], px) - b_ref) <= 1e-3 * abs(b_ref)
 
@@ -130,4 +131,4 @@ def test_mcm_batch_independence(vitb):
     with torch.no_grad():
         a = m(imgs.to(DEV), scores.to(DEV))["x_hat"][:1]
         b = m(imgs[:1].to(DEV), scores[:1].to(DEV))["x_hat"]
-    assert maxrel(a, b) < 1e-5
+    check("maxrel:a", maxrel(a, b), 1e-5)

@@ -6,7 +6,11 @@
 * the DP bucket hand-off: every ``ready(upto)`` the HIP backward reports must come after the last write
   into gradients [0, upto) -- checked with a recording GradSync on one GPU, and with two ranks on
   cuda:0 over gloo, whose averaged gradients must equal a single-process full-batch backward and be
-  bitwise identical to a run that defers every bucket to ``finish()``.
+  bitwise identical to a run that defers every bucket to ``finish()``;
+* the RCCL branch of GradSync (backend "nccl", async ``AVG`` all-reduce per bucket, ``Work.wait()``
+  ordering) run for real in a one-rank group with the world-of-1 short-circuit bypassed: training steps
+  bitwise equal to a run without data parallelism;
+* ``bench.py --gpus 2`` without a launcher spawns its own two ranks.
 """
 import io
 import os
@@ -309,3 +313,105 @@ def test_bench_two_ranks_gloo_prints_one_line():
     assert len(lines) == 1, r.stdout
     rec = json.loads(lines[0])
     assert rec["n_gpus"] == 2 and rec["value"] > 0 and rec["train"]["global_batch"] == 4
+
+
+# ------------------------------------------------------------------------------ RCCL branch, one rank
+def _nccl_w1_worker(port, geom, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        import textmae_amd
+        from textmae_amd.optim import configure_optimizers
+        from textmae_amd.parallel import enable_data_parallel
+        from textmae_amd.rd_loss import RateDistortionLoss
+
+        assert dist.get_backend() == "nccl"
+        crit = RateDistortionLoss(lmbda=1e-2)
+
+        def make():
+            if geom == "small":
+                m, cfg = _model(SMALL, 31, torch.float32)
+            else:
+                from oracle.mcm_oracle import MCMConfig
+
+                torch.manual_seed(0)
+                cfg = MCMConfig(img_size=256, num_keep_patches=144)
+                m = textmae_amd.MCM(img_size=256, num_keep_patches=144).cuda().train()
+                m.compute_dtype = torch.bfloat16
+            m.distortion = "ssim+l1"
+            return m, cfg
+
+        res = {}
+        for mode in ("plain", "rccl"):
+            m, cfg = make()
+            sync = enable_data_parallel(m, bucket_mb=8.0 if geom == "vitb" else 0.05,
+                                        always_collective=True) if mode == "rccl" else None
+            opt, aux = configure_optimizers(m, lr=1e-3, aux_lr=1e-3, fused=True)
+            batches = [_inputs(cfg, 2, 500 + i) for i in range(2)]
+            losses = _train_steps(m, opt, aux, batches, crit)
+            # one more backward, kept: the gradients themselves
+            imgs, scores, zn, yn = _inputs(cfg, 2, 600)
+            out = m(imgs.cuda(), scores.cuda(), noise=(zn.cuda(), yn.cuda()))
+            crit(out, imgs.cuda())["loss"].backward()
+            torch.cuda.synchronize()
+            g = torch.cat([p.grad.reshape(-1).cpu() for p in m.parameters() if p.requires_grad])
+            w = torch.cat([p.detach().reshape(-1).float().cpu() for p in m.parameters()])
+            res[mode] = (losses, g.numpy(), w.numpy(), sync.launched if sync is not None else 0)
+        q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("geom", ["small", "vitb"])
+def test_rccl_grad_sync_one_rank_bitwise(geom):
+    """GradSync's RCCL path executes (nccl process group of one rank, short-circuit bypassed): the
+    bucketed async AVG all-reduces issued from inside the backward and the Work.wait() before the
+    optimizer leave losses, gradients and post-step weights bitwise equal to a run without DP"""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_w1_worker, args=(_port(), geom, q))
+    p.start()
+    res = q.get(timeout=400)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    (l0, g0, w0, _), (l1, g1, w1, launched) = res["plain"], res["rccl"]
+    assert launched > 10, launched  # three backwards' worth of buckets really went through RCCL
+    assert l0 == l1
+    assert np.array_equal(g0, g1)
+    assert np.array_equal(w0, w1)
+
+
+def test_bench_spawns_ranks_without_launcher():
+    """``python bench.py --gpus 2`` with no torch.distributed launcher: bench starts two ranks itself
+    (before any GPU call in the parent) and prints one line for the whole job"""
+    import json
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "2",
+           "--warmup", "1", "--batch", "4", "--train-steps", "1", "--train-warmup", "1", "--train-batch", "2",
+           "--no-roofline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["train"]["global_batch"] == 4
+
+
+def test_fused_adam_rejects_partial_gradients():
+    """one step count per group (optim.FusedAdam): a group in which only some parameters got a gradient
+    would get torch's per-parameter bias correction wrong, so it raises instead"""
+    from textmae_amd.optim import FusedAdam
+
+    a, b = torch.nn.Parameter(torch.ones(4, device="cuda")), torch.nn.Parameter(torch.ones(4, device="cuda"))
+    opt = FusedAdam([a, b], lr=1e-3)
+    a.grad = torch.ones(4, device="cuda")
+    with pytest.raises(ValueError, match="every trainable parameter"):
+        opt.step()

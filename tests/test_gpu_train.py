@@ -5,10 +5,12 @@ Tolerances: f32 operand path max|a-b| / max|b| <= 1e-3 per tensor (bit-level GEL
 and summation order); bf16 operand path relative L2 <= 3e-2 against the fp32 reference.
 """
 import math
+import os
 
 import numpy as np
 import pytest
 import torch
+from parity_log import check  # noqa: E402
 import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
@@ -50,7 +52,7 @@ def test_wgrad_dense(T, K, M, N, dt):
     out = torch.empty(M, N, device="cuda")
     T.wgrad(a.cuda().to(dt), b.cuda().to(dt), M, N, K, out, dt)
     torch.cuda.synchronize()
-    assert _rel(out, ref) < (1e-5 if dt == torch.float32 else 2e-3)
+    check("_rel:out", _rel(out, ref), (1e-5 if dt == torch.float32 else 2e-3))
 
 
 def test_wgrad_remap_transposed_accumulate(T):
@@ -63,7 +65,7 @@ def test_wgrad_remap_transposed_accumulate(T):
     T.wgrad(a_full.cuda(), b.cuda(), 64, 48, K0, out, torch.float32, a_remap=(G, G + 1, 1), layout="dense_t",
             accumulate=True)
     torch.cuda.synchronize()
-    assert _rel(out - 1, ref) < 1e-5
+    check("_rel:out_1", _rel(out - 1, ref), 1e-5)
 
 
 @pytest.mark.parametrize("stride", [1, 2])
@@ -81,7 +83,7 @@ def test_wgrad_conv(T, stride, dt):
     T.wgrad(dy_nhwc, x_nhwc, cout, 9 * cin, n * Ho * Ho, out, dt, conv=dict(c1=cin, H=H, W=H, stride=stride, cin=cin),
             layout="conv")
     torch.cuda.synchronize()
-    assert _rel(out, ref) < (1e-5 if dt == torch.float32 else 2e-3)
+    check("_rel:out", _rel(out, ref), (1e-5 if dt == torch.float32 else 2e-3))
 
 
 def test_wgrad_conv_two_sources(T):
@@ -115,8 +117,8 @@ def test_dgrad_linear_gelu(T, dt):
     T.dgrad_linear(dyq.cuda().to(dt), wt, M, N, K, dt, acc32=acc)
     torch.cuda.synchronize()
     tol = 1e-4 if dt == torch.float32 else 1e-2
-    assert _rel(out, ref) < tol
-    assert _rel(acc - 1, dyq @ wq) < tol
+    check("_rel:out", _rel(out, ref), tol)
+    check("_rel:acc_1", _rel(acc - 1, dyq @ wq), tol)
 
 
 @pytest.mark.parametrize("stride", [1, 2])
@@ -138,8 +140,8 @@ def test_conv_dgrad(T, stride, dt):
     T.conv_dgrad(nh(dyq).cuda().to(dt), wd, n, H, H, stride, cout, cin, dt, routes=[(r0, 16, 16), (r1, 8, 8), (r2, 16, 16)])
     torch.cuda.synchronize()
     tol = 1e-4 if dt == torch.float32 else 1e-2
-    assert _rel(out, nh(x.grad)) < tol
-    assert _rel(torch.cat([r0, r1, r2], 1) - 1, nh(dx)) < tol
+    check("_rel:out", _rel(out, nh(x.grad)), tol)
+    check("_rel:torch_cat_r0_r1_r2_1_1", _rel(torch.cat([r0, r1, r2], 1) - 1, nh(dx)), tol)
 
 
 def test_layernorm_bwd_remap(T):
@@ -157,11 +159,11 @@ def test_layernorm_bwd_remap(T):
     T.layernorm_bwd(x.cuda(), gamma.cuda(), dy.cuda(), dx, len(rows), D, 1e-6, dg, db, dres=dres.cuda(), dxop=dxop,
                     row_group=Tn - 1, group_stride=Tn, row_offset=1, dres_colsum=drs)
     torch.cuda.synchronize()
-    assert _rel(drs, dres[rows].sum(0)) < 1e-5  # bias gradient of the residual's Linear, folded in
+    check("_rel:drs", _rel(drs, dres[rows].sum(0)), 1e-5)  # bias gradient of the residual's Linear, folded in
     ref = xr.grad.clone()
     ref[rows] += dres[rows]
-    assert _rel(dx, ref) < 1e-5
-    assert _rel(dxop.float(), ref) < 1e-2
+    check("_rel:dx", _rel(dx, ref), 1e-5)
+    check("_rel:dxop_float", _rel(dxop.float(), ref), 1e-2)
     assert _rel(dg, g_.grad) < 1e-5 and _rel(db, b_.grad) < 1e-5
 
 
@@ -191,10 +193,10 @@ def test_mha_bwd(T, T_, H, dh, dt):
     torch.cuda.synchronize()
     assert torch.equal(out, o_plain)  # the lse variant computes the same output
     if dt == torch.float32:
-        assert _rel(out, o) < 1e-5
-        assert _rel(dq, q_.grad) < 1e-4
+        check("_rel:out", _rel(out, o), 1e-5)
+        check("_rel:dq", _rel(dq, q_.grad), 1e-4)
     else:
-        assert _rel2(dq.float(), q_.grad) < 2e-2
+        check("_rel2:dq_float", _rel2(dq.float(), q_.grad), 2e-2)
 
 
 # ------------------------------------------------------------------------------ distortion
@@ -213,7 +215,7 @@ def test_distortion_fwd_bwd_vs_oracle():
     (0.7 * s + 1.3 * l).backward()
     torch.cuda.synchronize()
     assert abs(s.item() - s_ref.item()) < 1e-5 and abs(l.item() - l_ref.item()) < 1e-6
-    assert _rel(xg.grad, xr.grad) < 1e-4
+    check("_rel:xg_grad", _rel(xg.grad, xr.grad), 1e-4)
 
 
 # ------------------------------------------------------------------------------ optimizer
@@ -231,7 +233,7 @@ def test_adam_matches_torch(T):
     norm = torch.empty(2, device="cuda")
     T.grad_norm(g.cuda(), 1.0, norm)
     torch.cuda.synchronize()
-    assert _rel(p, ref.detach()) < 1e-6
+    check("_rel:p", _rel(p, ref.detach()), 1e-6)
     assert abs(norm[0].item() - g.norm().item()) < 1e-4 * g.norm().item()
     assert abs(norm[1].item() - min(1.0, 1.0 / (g.norm().item() + 1e-6))) < 1e-6
 
@@ -300,7 +302,7 @@ def test_mcm_train_grads_f32_vs_oracle():
     m, cfg, sd, imgs, scores, zn, yn, R = _model_and_oracle(SMALL, 3, 2, torch.float32)
     hip, out, loss, aux = _hip_grads(m, imgs, scores, zn, yn, R)
     ref, x_ref, loss_ref, aux_ref = _oracle_grads(cfg, sd, imgs, scores, zn, yn, R)
-    assert _rel(out["x_hat"], x_ref) < 1e-4
+    check("_rel:out_x_hat", _rel(out["x_hat"], x_ref), 1e-4)
     assert abs(loss.item() - loss_ref.item()) < 1e-4 * max(1.0, abs(loss_ref.item()))
     assert abs(aux.item() - aux_ref.item()) < 1e-4 * abs(aux_ref.item())
     bad = []
@@ -324,7 +326,59 @@ def test_mcm_train_bf16_close_to_f32():
     flat32 = torch.cat([g32[k].reshape(-1) for k in g32])
     flat16 = torch.cat([g16[k].reshape(-1) for k in g32])
     assert torch.isfinite(flat16).all()
-    assert _rel2(flat16, flat32) < 5e-2
+    check("_rel2:flat16", _rel2(flat16, flat32), 5e-2)
+
+
+def _partial_loss_grads(m, imgs, scores, zn, yn, R, nsel):
+    """HIP backward of a loss over the first `nsel` images only (rate of those images + sum(x_hat * R)), run
+    at the batch of `imgs`: images never mix, so the gradient equals that of the same loss on a batch of
+    `nsel` -- which lets the oracle check the bench batch's tile / split-K geometry on a small sample"""
+    m.zero_grad(set_to_none=True)
+    out = m(imgs.cuda(), scores.cuda(), noise=(zn.cuda(), yn.cuda()))
+    n, _, H, W = imgs.shape
+    ylik, zlik = out["likelihoods"]["y"], out["likelihoods"]["z"]
+    loss = ((torch.log(ylik[:nsel]).sum() + torch.log(zlik[:nsel]).sum()) / (-math.log(2) * nsel * H * W)
+            + (out["x_hat"] * R.cuda()).sum())
+    loss.backward()
+    aux = m.aux_loss()
+    aux.backward()
+    torch.cuda.synchronize()
+    return {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters() if p.requires_grad}, out, loss, aux
+
+
+def test_mcm_train_grads_vitb_batch64_f32_vs_oracle():
+    """north-star geometry (ViT-B/16 256^2, K=144) at the bench's batch of 64, f32 parity path: the whole
+    model's parameter gradients against the autograd oracle (f64) for a loss over images 0-1 (injected
+    noise), i.e. the batch-64 tile / split-K choices and bias-sum folds composed over 12 + 8 blocks"""
+    B, NS = 64, 2
+    m, cfg, sd, imgs, scores, zn, yn, R = _model_and_oracle(dict(img_size=256, num_keep_patches=144), 7, B,
+                                                            torch.float32)
+    R[NS:] = 0
+    hip, out, loss, aux = _partial_loss_grads(m, imgs, scores, zn, yn, R, NS)
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    ref, x_ref, loss_ref, aux_ref = _oracle_grads(cfg, sd, imgs[:NS], scores[:NS], zn[:NS], yn[:NS], R[:NS])
+    check("_rel:x_hat_vitb", _rel(out["x_hat"][:NS], x_ref), 1e-4)
+    check("loss_rel_vitb", abs(loss.item() - loss_ref.item()) / max(1.0, abs(loss_ref.item())), 1e-4)
+    worst, bad = 0.0, []
+    for name, g in hip.items():
+        r = ref[name].float()
+        if r.abs().max() == 0:
+            if g.abs().max() > 1e-6:
+                bad.append((name, "nonzero", g.abs().max().item()))
+            continue
+        e = _rel(g, r)
+        worst = max(worst, e)
+        if e > 2e-3:
+            bad.append((name, e))
+    check("grad_maxrel_worst_tensor_vitb_b64_f32", worst, 2e-3, tensors=len(hip))
+    assert not bad, bad[:20]
+    # the benched operand dtype at the same batch against these f32 gradients
+    m.compute_dtype = torch.bfloat16
+    g16, *_ = _partial_loss_grads(m, imgs, scores, zn, yn, R, NS)
+    flat32 = torch.cat([hip[k].reshape(-1) for k in hip])
+    flat16 = torch.cat([g16[k].reshape(-1) for k in hip])
+    assert torch.isfinite(flat16).all()
+    check("grad_relL2_bf16_vs_f32_vitb_b64", _rel2(flat16, flat32), 5e-2)
 
 
 def test_mcm_train_vitb_step_runs():

@@ -67,3 +67,18 @@ def test_distributed_helpers_single_process(tmae):
 
     assert D.get_rank() == 0 and D.get_world_size() == 1
     assert D.all_reduce_mean(3.5) == 3.5
+
+
+def test_bench_rejects_gpus_world_size_mismatch():
+    """bench.py --gpus N under a launcher that started a different WORLD_SIZE exits non-zero before any GPU
+    call, instead of printing a line for the wrong world"""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8"], capture_output=True, text=True,
+                       env=env, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]

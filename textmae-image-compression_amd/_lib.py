@@ -117,6 +117,7 @@ SIGNATURES = {
     "tmae_eb_aux_loss": [ctypes.POINTER(EBParams), P, P, P, I, P],
     "tmae_gc_likelihood_fwd": [P, P, P, P, P, P, I, F, P],
     "tmae_nhwc_to_nchw": [P, I, P, I, I, I, P],
+    "tmae_crop_normalize_u8": [P, I, I, I, P, I, I, ctypes.POINTER(F), ctypes.POINTER(F), P, P],
     "tmae_bpp_sum": [P, LL, P, LL, P, P, ctypes.c_double, P],
     "tmae_gemm_plan": [I, I, I, I, I, ctypes.c_char_p, I],
     "tmae_mae_masking": [P, P, P, P, I, I, I, P],

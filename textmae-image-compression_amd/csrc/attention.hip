@@ -29,7 +29,7 @@ mha_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, float* __restrict
   T* Ks = reinterpret_cast<T*>(smem);
   T* Vt = Ks + (size_t)Tpad * ldk;
 
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int bh = xcd_remap(blockIdx.x, gridDim.x), b = bh / H, h = bh - b * H;
   const int D = H * DH, ld = 3 * D;
   const T* base = qkv + (size_t)b * Tn * ld + h * DH;
   const int tid = threadIdx.x, nthr = blockDim.x;
@@ -333,9 +333,10 @@ __device__ __forceinline__ void mha_bf16_item(const bf16* Ks, const bf16* Vs, co
 }
 
 
-// QB = 32-query blocks per wave (QB = 2: half the waves per workgroup, each walking two blocks against the
-// staged K / V, so more workgroups fit a CU)
-template <int DH, int QB>
+// one workgroup per (image, head): K / V staged in LDS, one 32-query block per wave.  Workgroup ids go
+// through xcd_remap, so the heads of one image run back to back on one XCD: at dh = 32 two heads share every
+// 128-B line of qkv, which one L2 then fetches once instead of each of two XCDs fetching it.
+template <int DH>
 __global__ void __launch_bounds__(1024)
 mha_fwd_bf16_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float* __restrict__ lse, int Tn, int H,
                     int Tpad, float scale_log2e) {
@@ -344,13 +345,13 @@ mha_fwd_bf16_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
   constexpr int ldk = DH + KPAD;
   bf16* Ks = reinterpret_cast<bf16*>(smem);
   bf16* Vs = Ks + (size_t)Tpad * ldk;
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int bh = xcd_remap(blockIdx.x, gridDim.x), b = bh / H, h = bh - b * H;
   const int D = H * DH, ld = 3 * D;
   const bf16* base = qkv + (size_t)b * Tn * ld + h * DH;
   const int tid = threadIdx.x, nthr = blockDim.x;
   // K and V row-major, 16-B chunks; every load of a thread issued before its first LDS store
-  // chunks per thread per operand: Tpad * DH / 8 chunks over >= 2 * Tpad / QB threads
-  constexpr int MAXC = DH / 16 * QB;
+  // chunks per thread per operand: Tpad * DH / 8 chunks over >= 2 * Tpad threads
+  constexpr int MAXC = DH / 16;
   uint4 kv[MAXC], vv[MAXC];
 #pragma unroll
   for (int u = 0; u < MAXC; ++u) {
@@ -373,29 +374,15 @@ mha_fwd_bf16_kernel(const bf16* __restrict__ qkv, bf16* __restrict__ out, float*
   }
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6;
-  if constexpr (QB == 1) {
-    const int q0 = wave * 32;
-    if (q0 >= Tn) return;  // whole wave: EXEC stays all-ones for the transposed reads below
-    // (Q issued with the K / V loads instead, one HBM round trip for both, measured 5-10 % slower)
-    const bf16* qrow = base + (size_t)min(q0 + (lane & 31), Tn - 1) * ld;
-    bf16x8 qf[DH / 16];
+  const int q0 = wave * 32;
+  if (q0 >= Tn) return;  // whole wave: EXEC stays all-ones for the transposed reads below
+  // (Q issued with the K / V loads instead, one HBM round trip for both, measured 5-10 % slower)
+  const bf16* qrow = base + (size_t)min(q0 + (lane & 31), Tn - 1) * ld;
+  bf16x8 qf[DH / 16];
 #pragma unroll
-    for (int s2 = 0; s2 < DH / 16; ++s2) qf[s2] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s2 + 8 * (lane >> 5));
-    mha_bf16_item<DH>(Ks, Vs, qf, Tn, Tpad, scale_log2e, lane, q0, lse ? lse + (size_t)bh * Tn : nullptr,
-                      out + (size_t)b * Tn * D + h * DH, D);
-  } else {
-    // whole-wave loop bound keeps EXEC all-ones (the QB = 1 kernel keeps its straight-line form: as a loop
-    // it spills)
-    for (int q0 = wave * 32; q0 < Tn; q0 += nthr / 2) {
-      const bf16* qrow = base + (size_t)min(q0 + (lane & 31), Tn - 1) * ld;
-      bf16x8 qf[DH / 16];
-#pragma unroll
-      for (int s2 = 0; s2 < DH / 16; ++s2)
-        qf[s2] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s2 + 8 * (lane >> 5));
-      mha_bf16_item<DH>(Ks, Vs, qf, Tn, Tpad, scale_log2e, lane, q0, lse ? lse + (size_t)bh * Tn : nullptr,
-                        out + (size_t)b * Tn * D + h * DH, D);
-    }
-  }
+  for (int s2 = 0; s2 < DH / 16; ++s2) qf[s2] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s2 + 8 * (lane >> 5));
+  mha_bf16_item<DH>(Ks, Vs, qf, Tn, Tpad, scale_log2e, lane, q0, lse ? lse + (size_t)bh * Tn : nullptr,
+                    out + (size_t)b * Tn * D + h * DH, D);
 }
 
 template <typename T, int DH>
@@ -403,23 +390,14 @@ static int mha_launch(const void* qkv, void* out, int B, int Tn, int H, float sc
                       float* lse = nullptr) {
   const int Tpad = (Tn + 31) / 32 * 32;
   const bool lean = sizeof(T) == 2 && !getenv("TMAE_MHA_PLAIN");
-  static const int qb_knob = getenv("TMAE_MHA_QB") ? atoi(getenv("TMAE_MHA_QB")) : 1;
-  const int qb = (lean && DH == 32 && qb_knob == 2) ? 2 : 1;
-  const int nthr = 64 * ceil_div(Tpad / 32, qb);
+  const int nthr = 64 * (Tpad / 32);
   const size_t lds = lean ? ((size_t)Tpad * (DH + 8) + (size_t)Tpad * AttnTr<DH>::LDV) * 2
                           : ((size_t)Tpad * (DH + AttnCfg<T>::KPAD) + (size_t)DH * (Tpad + AttnCfg<T>::VPAD)) * sizeof(T);
   TMAE_REQUIRE(nthr <= 1024 && lds <= 160 * 1024, "tmae_mha_fwd: sequence length %d too long", Tn);
-  TMAE_REQUIRE(!lean || Tpad * (DH / 8) <= nthr * (DH / 16) * qb, "tmae_mha_fwd: sequence length %d too long", Tn);
+  TMAE_REQUIRE(!lean || Tpad * (DH / 8) <= nthr * (DH / 16), "tmae_mha_fwd: sequence length %d too long", Tn);
   if (B * H == 0 || Tn == 0) return TMAE_OK;
-  if constexpr (DH == 32) {
-    if (lean && qb == 2) {
-      hipLaunchKernelGGL((mha_fwd_bf16_kernel<DH, 2>), dim3(B * H), dim3(nthr), lds, st, (const bf16*)qkv,
-                         (bf16*)out, lse, Tn, H, Tpad, scale * 1.4426950408889634f);
-      TMAE_LAUNCH_CHECK("tmae_mha_fwd");
-    }
-  }
   if (lean)
-    hipLaunchKernelGGL((mha_fwd_bf16_kernel<DH, 1>), dim3(B * H), dim3(nthr), lds, st, (const bf16*)qkv, (bf16*)out,
+    hipLaunchKernelGGL((mha_fwd_bf16_kernel<DH>), dim3(B * H), dim3(nthr), lds, st, (const bf16*)qkv, (bf16*)out,
                        lse, Tn, H, Tpad, scale * 1.4426950408889634f);
   else
     hipLaunchKernelGGL((mha_fwd_kernel<T, DH>), dim3(B * H), dim3(nthr), lds, st, (const T*)qkv, (T*)out, lse, Tn, H,
@@ -476,7 +454,7 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
   float* lse_s = reinterpret_cast<float*>(dOt + (size_t)DH * LDT);
   float* dl_s = lse_s + Tpad;
 
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int bh = xcd_remap(blockIdx.x, gridDim.x), b = bh / H, h = bh - b * H;
   const int D = H * DH, ld = 3 * D;
   const bf16* base = qkv + (size_t)b * Tn * ld + h * DH;
   const bf16* obase = o + (size_t)b * Tn * D + h * DH;
@@ -659,7 +637,7 @@ mha_bwd_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ o, c
                    const float* __restrict__ lse, float* __restrict__ dqkv, int Tn, int H, int Tpad, float scale) {
   constexpr int NDT = DH / 32;
   __shared__ float lse_s[1024], dl_s[1024];
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int bh = xcd_remap(blockIdx.x, gridDim.x), b = bh / H, h = bh - b * H;
   const int D = H * DH, ld = 3 * D;
   const float* Q = qkv + (size_t)b * Tn * ld + h * DH;
   const float* K = Q + D;

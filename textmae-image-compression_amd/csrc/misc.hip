@@ -129,3 +129,38 @@ extern "C" int tmae_bpp_sum(const float* y_lik, long long ny, const float* z_lik
                      1.0 / (-0.69314718055994530942 * num_pixels), out);
   TMAE_LAUNCH_CHECK("tmae_bpp_sum");
 }
+
+// ------------------------------------------------------------------ training-set random crops
+// The training loader's per-sample work on a DIV2K-shaped set (training.py:115-129 builds the loader;
+// utils/dataloader.py:58-61: ToTensor then Normalize): crop S x S from a uint8 HWC image, x = v / 255, then
+// (x - mean) / std per channel, into NCHW f32.  Same f32 operations in the same order as torchvision's
+// ToTensor (div 255) and Normalize (sub mean, div std), so the result is bitwise torch's.
+// crops[b] = (source image, top, left).  One thread per output pixel: 3 byte loads, 3 coalesced plane stores.
+__global__ void crop_normalize_u8_kernel(const unsigned char* __restrict__ src, int H, int W,
+                                         const int* __restrict__ crops, int B, int S, float m0, float m1, float m2,
+                                         float s0, float s1, float s2, float* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long per = (long long)S * S;
+  if (i >= (long long)B * per) return;
+  const int b = (int)(i / per);
+  const int p = (int)(i - (long long)b * per), y = p / S, x = p - y * S;
+  const int img = crops[3 * b], top = crops[3 * b + 1], left = crops[3 * b + 2];
+  const unsigned char* px = src + (((size_t)img * H + top + y) * W + left + x) * 3;
+  float* o = out + (size_t)b * 3 * per + p;
+  o[0] = (px[0] / 255.0f - m0) / s0;
+  o[per] = (px[1] / 255.0f - m1) / s1;
+  o[2 * per] = (px[2] / 255.0f - m2) / s2;
+}
+
+extern "C" int tmae_crop_normalize_u8(const unsigned char* src, int nsrc, int H, int W, const int* crops, int B,
+                                      int S, const float* mean, const float* std, float* out, void* stream) {
+  TMAE_REQUIRE(nsrc > 0 && S > 0 && S <= H && S <= W, "tmae_crop_normalize_u8: crop %d exceeds the %dx%d images", S,
+               H, W);
+  TMAE_REQUIRE(mean != nullptr && std != nullptr, "tmae_crop_normalize_u8: mean / std are NULL");
+  const long long total = (long long)B * S * S;
+  if (total == 0) return TMAE_OK;
+  hipLaunchKernelGGL(crop_normalize_u8_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, src, H, W, crops, B, S, mean[0], mean[1], mean[2], std[0], std[1], std[2],
+                     out);
+  TMAE_LAUNCH_CHECK("tmae_crop_normalize_u8");
+}

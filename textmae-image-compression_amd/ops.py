@@ -418,6 +418,22 @@ def nhwc_to_nchw(x, ldx, n, C, H, W, out=None):
     return out
 
 
+def crop_normalize_u8(src, crops, size, mean, std, out=None):
+    """random-crop loader sample: src uint8 [nsrc, H, W, 3] (device), crops int32 [B, 3] = (image, top, left)
+    (device) -> (crop / 255 - mean) / std as f32 [B, 3, size, size] (utils/dataloader.py:58-61)"""
+    import ctypes
+
+    assert src.dtype == torch.uint8 and src.dim() == 4 and src.shape[3] == 3 and src.is_contiguous()
+    crops = _need(crops.contiguous(), torch.int32, "crops")
+    B = crops.shape[0]
+    out = torch.empty((B, 3, size, size), dtype=torch.float32, device=src.device) if out is None else out
+    m = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    s = (ctypes.c_float * 3)(*[float(v) for v in std])
+    _lib.call("tmae_crop_normalize_u8", src.data_ptr(), src.shape[0], src.shape[1], src.shape[2], crops.data_ptr(), B,
+              size, m, s, out.data_ptr(), _stream())
+    return out
+
+
 _BPP_WORK = {}
 
 

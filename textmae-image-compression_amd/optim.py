@@ -83,6 +83,11 @@ class FusedAdam(torch.optim.Optimizer):
             live = [p for p in group["params"] if p.grad is not None]
             if not live:
                 continue
+            if len(live) != sum(1 for p in group["params"] if p.requires_grad):
+                # torch.optim.Adam keeps a step count per parameter; FusedAdam keeps one per group (one bias
+                # correction for the whole flat buffer), which equals torch's only if every parameter steps
+                raise ValueError("FusedAdam: every trainable parameter of a group needs a gradient at every step "
+                                 "(one step count per group); use torch.optim.Adam for partial updates")
             for p in live:
                 if p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
                     raise ValueError("FusedAdam needs contiguous f32 gradients")

@@ -20,10 +20,17 @@ import torch.distributed as dist
 
 
 class GradSync:
-    def __init__(self, process_group=None, bucket_mb: float = 64.0, average: bool = True):
+    """``always_collective``: issue the collectives even in a one-rank group (by default a world of 1
+    returns before them).  Tests use it to run the RCCL branch -- async ``AVG`` all-reduce per bucket,
+    ``Work.wait()`` ordering against the compute stream -- on a single GPU."""
+
+    def __init__(self, process_group=None, bucket_mb: float = 64.0, average: bool = True,
+                 always_collective: bool = False):
         self.group = process_group
         self.bucket_elems = max(1, int(bucket_mb * (1 << 20) // 4))
         self.average = average
+        self.always_collective = always_collective
+        self.launched = 0  # collectives issued (tests check the buckets really went out)
         self.flat = None
         self._bounds = None
         self._next = 0
@@ -48,8 +55,9 @@ class GradSync:
         a, b = self._bounds[i], self._bounds[i + 1]
         t = self.flat[a:b]
         W = self.world()
-        if W <= 1:
+        if W <= 1 and not (self.always_collective and dist.is_initialized()):
             return
+        self.launched += 1
         if dist.get_backend(self.group) == "nccl":
             op = dist.ReduceOp.AVG if self.average else dist.ReduceOp.SUM
             self._work.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
@@ -102,8 +110,8 @@ def broadcast_parameters(model, src: int = 0, group=None):
     bump_versions(model.parameters())
 
 
-def enable_data_parallel(model, process_group=None, bucket_mb: float = 64.0):
+def enable_data_parallel(model, process_group=None, bucket_mb: float = 64.0, always_collective: bool = False):
     """attach a GradSync to `model` (MCM): its backward then all-reduces (averages) the gradients"""
-    model.grad_sync = GradSync(process_group, bucket_mb)
+    model.grad_sync = GradSync(process_group, bucket_mb, always_collective=always_collective)
     broadcast_parameters(model, group=process_group)
     return model.grad_sync

@@ -24,11 +24,17 @@ IMG_EXTENSIONS = (".jpg", ".jpeg", ".png", ".ppm", ".bmp", ".pgm", ".tif", ".tif
 
 
 def imread_gray(path) -> np.ndarray:
-    """cv2.imread(path, IMREAD_GRAYSCALE) for the RGB images the reference feeds it: libpng's
-    rgb_to_gray(0.299, 0.587) 15-bit fixed point (OpenCV's PNG decoder path).  Host-side data loading."""
+    """cv2.imread(path, IMREAD_GRAYSCALE), host-side data loading:
+      * PNG (and other non-JPEG formats): libpng's rgb_to_gray(0.299, 0.587) 15-bit fixed point, OpenCV's PNG
+        decoder path -- pinned against the reference's glue on the 24 Kodak PNGs (tests/golden/kodak.npz);
+      * JPEG: OpenCV asks libjpeg for JCS_GRAYSCALE output, i.e. the decoded luma plane without colour
+        conversion; PIL's ``draft('L')`` requests the same libjpeg output.  cv2 is absent here, so JPEG
+        parity is UNPINNED (no fixture covers it)."""
     from PIL import Image
 
     im = Image.open(path)
+    if im.format == "JPEG" and im.mode in ("RGB", "YCbCr"):
+        im.draft("L", im.size)  # libjpeg grayscale output at full scale (no DCT downscaling)
     if im.mode == "L":
         return np.array(im)
     rgb = np.array(im.convert("RGB")).astype(np.int64)

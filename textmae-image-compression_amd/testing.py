@@ -145,13 +145,16 @@ def eval_model(model, output_dir, images, scores, names=None, entropy_estimation
     return dict(metrics)
 
 
-def load_checkpoint(num_keep_patches, checkpoint_path, img_size=224):
+def load_checkpoint(num_keep_patches, checkpoint_path, img_size=224, **model_kwargs):
     """testing.py:123-125: the checkpoint's 'model' state_dict into MCM.from_state_dict (CDF buffers resized
-    by the compressai-style load_state_dict).  Loaded with weights_only=True."""
+    by the compressai-style load_state_dict).  Loaded with weights_only=True; the reference's save_model
+    (models/Compression/common/model_utils.py:30-55) stores ``args`` as an argparse.Namespace next to the
+    model, so that one class is allow-listed for the weights-only unpickler."""
     from .mcm import MCM
 
-    sd = torch.load(checkpoint_path, map_location="cpu", weights_only=True)["model"]
-    net = MCM(img_size=img_size, num_keep_patches=num_keep_patches)
+    with torch.serialization.safe_globals([argparse.Namespace]):
+        sd = torch.load(checkpoint_path, map_location="cpu", weights_only=True)["model"]
+    net = MCM(img_size=img_size, num_keep_patches=num_keep_patches, **model_kwargs)
     net.load_state_dict(sd)
     return net.eval()
 
