@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="all-threads oracle sample length")
     ap.add_argument("--cpu-batch", type=int, default=8)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-leg", default=None, help=argparse.SUPPRESS)  # internal: one CPU-baseline leg
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--dump-launches", default=None, help="write every launch of one forward with its family and shape")
     ap.add_argument("--train-steps", type=int, default=10, help="training steps timed after the inference run")
@@ -439,66 +440,99 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
+def _cpu_leg(threads, seconds, max_batches, batch, model_kwargs):
+    """one timed leg of the CPU baseline (runs in a child process: see cpu_baseline)"""
+    from oracle.mcm_oracle import MCMConfig, make_state_dict, mcm_forward
+
+    torch.set_num_threads(threads)
+    cfg = MCMConfig(**model_kwargs)
+    sd = make_state_dict(cfg, 0)
+    L = (cfg.img_size // cfg.patch_size) ** 2
+    x, s = synthetic_inputs(batch, cfg.img_size, L, 0, "cpu")
+    mcm_forward(sd, cfg, x[:1], s[:1])  # untimed warm-up (one image): first-call allocation / primitive setup
+    ts, t0 = [], time.perf_counter()
+    while len(ts) < max_batches:
+        t1 = time.perf_counter()
+        mcm_forward(sd, cfg, x, s)
+        ts.append(time.perf_counter() - t1)
+        if time.perf_counter() - t0 >= seconds:
+            break
+    ts.sort()
+    med = ts[len(ts) // 2] if len(ts) % 2 else 0.5 * (ts[len(ts) // 2 - 1] + ts[len(ts) // 2])
+    return {"threads": torch.get_num_threads(), "images_per_s_median": round(batch / med, 3), "batches": len(ts),
+            "batch": batch, "images_per_s_mean": round(batch * len(ts) / sum(ts), 3)}
+
+
+def _cpu_share():
+    """CPUs the cgroup lets this process use (cpu.max quota / period), or None"""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        return None
+
+
 def cpu_baseline(args, model_kwargs):
     """the oracle (CPU restatement of MCM.forward, fp32) on the host cores over a bounded
     sample of the same workload (batches of 8), timed per batch and reported at the median:
       * at torch.set_num_threads(os.cpu_count()) -- §8(d)'s setting;
       * at the thread count the process is given (OMP_NUM_THREADS; the box's CPU share);
-      * at 1 thread, the reference eval convention (testing.py:29);
-    ``value`` / ``cores`` are the faster of the first two.  Plus the reference-semantics get_ids_shuffle
-    alone (the C restatement of MCM.py:364-423, batch 64, 1 thread)."""
+      * at 1 thread, the reference eval convention (testing.py:29).
+    Each leg runs in its own child process (no GPU use there) under a time limit, so a leg that
+    oversubscribes the box's CPU share cannot stall the run; ``value`` / ``cores`` are the faster of the first
+    two.  Plus the reference-semantics get_ids_shuffle alone (the C restatement of MCM.py:364-423, batch 64)."""
+    import subprocess
+
     import numpy as np
 
     from oracle import ids as ids_oracle
-    from oracle.mcm_oracle import MCMConfig, make_state_dict, mcm_forward
 
-    cfg = MCMConfig(**model_kwargs)
-    sd = make_state_dict(cfg, 0)
-    L = (cfg.img_size // cfg.patch_size) ** 2
     nb = args.cpu_batch
-    x, s = synthetic_inputs(nb, cfg.img_size, L, 0, "cpu")
     default_threads = torch.get_num_threads()
-
-    def leg(threads, seconds, max_batches=1000):
-        torch.set_num_threads(threads)
-        ts, t0 = [], time.perf_counter()
-        while len(ts) < max_batches:
-            t1 = time.perf_counter()
-            mcm_forward(sd, cfg, x, s)
-            ts.append(time.perf_counter() - t1)
-            if time.perf_counter() - t0 >= seconds:
-                break
-        ts.sort()
-        med = ts[len(ts) // 2] if len(ts) % 2 else 0.5 * (ts[len(ts) // 2 - 1] + ts[len(ts) // 2])
-        return {"threads": threads, "images_per_s_median": round(nb / med, 3), "batches": len(ts),
-                "images_per_s_mean": round(nb * len(ts) / sum(ts), 3)}
-
-    try:
-        legs = {"all_host_cpus": leg(os.cpu_count() or default_threads, args.cpu_seconds),
-                "process_threads": leg(default_threads, args.cpu_seconds),
-                "one_thread": leg(1, 0.0, max_batches=1)}
-    finally:
-        torch.set_num_threads(default_threads)
-    best = max(("all_host_cpus", "process_threads"), key=lambda k: legs[k]["images_per_s_median"])
+    legs = {}
+    plan = [("all_host_cpus", os.cpu_count() or default_threads, args.cpu_seconds, 1000),
+            ("process_threads", default_threads, args.cpu_seconds, 1000), ("one_thread", 1, 0.0, 1)]
+    for name, threads, secs, maxb in plan:
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+        cmd = [sys.executable, os.path.abspath(__file__), "--cpu-leg", json.dumps([threads, secs, maxb, nb, model_kwargs])]
+        limit = 4 * secs + 120
+        progress(f"cpu baseline leg {name}: {threads} threads (limit {limit:.0f} s)")
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=limit, env=env)
+            line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+            legs[name] = json.loads(line[-1]) if r.returncode == 0 and line else {"threads": threads,
+                                                                                   "error": r.stderr[-300:]}
+        except subprocess.TimeoutExpired:
+            legs[name] = {"threads": threads, "error": f"no batch of {nb} finished within {limit:.0f} s"}
+    ok = [k for k in ("all_host_cpus", "process_threads") if "images_per_s_median" in legs.get(k, {})]
+    best = max(ok, key=lambda k: legs[k]["images_per_s_median"]) if ok else None
+    L = (model_kwargs["img_size"] // 16) ** 2
     s64 = torch.rand(64, L, generator=torch.Generator().manual_seed(5)).numpy().astype(np.float32)
-    ids_oracle.ids_shuffle(s64, cfg.num_keep_patches)
+    ids_oracle.ids_shuffle(s64, model_kwargs["num_keep_patches"])
     reps, t2 = 0, time.perf_counter()
     while time.perf_counter() - t2 < 1.0:
-        ids_oracle.ids_shuffle(s64, cfg.num_keep_patches)
+        ids_oracle.ids_shuffle(s64, model_kwargs["num_keep_patches"])
         reps += 1
     ids_ms = (time.perf_counter() - t2) / reps * 1e3
     try:
         aff = len(os.sched_getaffinity(0))
     except Exception:
         aff = None
-    return {"value": legs[best]["images_per_s_median"], "unit": "images/s", "cores": legs[best]["threads"],
-            "kind": "port",
-            "sample": f"oracle MCM.forward (fp32 torch CPU restatement) on batches of {nb} at {cfg.img_size}^2, "
-                      f"K={cfg.num_keep_patches}, timed per batch, median; ~{args.cpu_seconds:.0f} s per multi-thread "
-                      f"leg, one batch at 1 thread; value = the faster of os.cpu_count() and the process's threads",
-            "legs": legs, "value_1thread": legs["one_thread"]["images_per_s_median"], "cpu_model": _cpu_model(),
-            "host_cpus": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+    return {"value": legs[best]["images_per_s_median"] if best else None, "unit": "images/s",
+            "cores": legs[best]["threads"] if best else None, "kind": "port",
+            "sample": f"oracle MCM.forward (fp32 torch CPU restatement) on batches of {nb} at "
+                      f"{model_kwargs['img_size']}^2, K={model_kwargs['num_keep_patches']}, timed per batch, median; "
+                      f"~{args.cpu_seconds:.0f} s per multi-thread leg, one batch at 1 thread; value = the faster of "
+                      f"os.cpu_count() threads and the process's threads",
+            "legs": legs, "value_1thread": legs["one_thread"].get("images_per_s_median"), "cpu_model": _cpu_model(),
+            "host_cpus": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_share": _cpu_share(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "ids_shuffle_ms_per_batch64_1thread": round(ids_ms, 3)}
+
+
+def progress(msg):
+    """phase markers on stderr (a long bench keeps its output flowing; stdout carries only the JSON line)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 def time_forward(model, imgs, scores, steps, warmup, use_graph, world, dev, backend, barrier):
@@ -600,6 +634,10 @@ def launch_ranks(args):
 
 def main():
     args = parse()
+    if args.cpu_leg:
+        threads, secs, maxb, nb, kw = json.loads(args.cpu_leg)
+        print(json.dumps(_cpu_leg(threads, secs, maxb, nb, kw)), flush=True)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", 0))
@@ -637,18 +675,22 @@ def main():
     gf = gflop_per_image(model)
     gf_img = sum(gf.values())
 
+    progress(f"forward: batch {args.batch}, {args.steps} timed steps")
     el, med_ms = time_forward(model, imgs, scores, args.steps, args.warmup, not args.no_graph, world, dev, args.backend,
                               barrier)
     roof = None
     if rank == 0 and not args.no_roofline:
+        progress("roofline: per-family replays")
         roof = roofline_report(model, imgs, scores, args.batch, dump=args.dump_launches)
 
     k64 = None
     if args.k64_line and args.keep == 144 and args.enc_dim == 768 and args.enc_depth == 12:
+        progress("config 2' (K=64) line")
         k64 = k64_line(args, dev, world, rank, barrier, dtype)
 
     train = None
     if not args.no_train and args.train_steps > 0:
+        progress("training step")
         train = train_bench(model, args, rank, world, dev, barrier)
 
     vitb = args.enc_dim == 768 and args.enc_depth == 12
@@ -677,6 +719,7 @@ def main():
         rec["train"] = train
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
+            progress("cpu baseline")
             rec["cpu_baseline"] = cpu_baseline(args, kw)
         print(json.dumps(rec), flush=True)
     if world > 1:
