@@ -8,7 +8,8 @@ checked against the oracle (oracle/mcm_oracle.py, pinned to the reference's gold
 * f32 operands (the parity path) at batch 64, K=144 and K=64 (§8(d) config 2'), tie-free and
   tie-heavy scores: ids bit-exact, per-image x_hat max|a-b|/max|b| <= 1e-3, y / z likelihoods, bpp;
 * bf16 operands through the captured HIP graph exactly as bench.py replays it: the graph output equals
-  the eager forward bit for bit, and stays within the bf16 bound of the oracle (relative L2 <= 3e-2);
+  the eager forward bit for bit, and stays within the bf16 bound of the oracle (per-image relative L2
+  <= 1.5e-2, bpp <= 1e-3 relative: about 2x the measured errors);
 * config 4 (MCM with a ViT-L/16 encoder 1024/24/16) at batch 2 in f32 against the oracle, and its
   bench batch (128) in bf16 against the oracle on a sample of images.
 
@@ -133,8 +134,8 @@ def test_bench_config_k64_f32_batch64(tmae, scores_kind):
 
 
 # bf16 bounds: about 2x the errors measured on the GPU (profiles/r03/parity_metrics.jsonl)
-BF16_XHAT_RELL2 = 3e-2
-BF16_BPP_REL = 3e-2
+BF16_XHAT_RELL2 = 1.5e-2  # measured 7.4e-3 (tie-heavy), 5.9e-3 (tie-free), 5.7e-3 (config 4)
+BF16_BPP_REL = 1e-3  # measured 4.7e-4
 
 
 def _graph_forward(m, imgs, scores):

@@ -1,6 +1,6 @@
 """Per-kernel parity: each HIP kernel vs a plain PyTorch fp32 CPU reference of the same op (or the
 oracle, for the masking and entropy models).  Tolerances: f32 MFMA path 1e-4 relative (it is an exact
-f32 fma chain; differences are summation order only), bf16 path 2e-2 relative (operand rounding);
+f32 fma chain; differences are summation order only), bf16 path 7e-3 relative (operand rounding);
 integer outputs bit-exact."""
 import os
 
@@ -23,7 +23,9 @@ def rel(a, b):
 
 
 def tol(dtype):
-    return 1e-4 if dtype == torch.float32 else 2e-2
+    # bf16: about 2x the largest error measured over these cases (3.3e-3, LayerNorm D=512;
+    # profiles/r03/parity_metrics.jsonl)
+    return 1e-4 if dtype == torch.float32 else 7e-3
 
 
 DTYPES = [torch.float32, torch.bfloat16]
@@ -126,7 +128,7 @@ def test_mha(tmae, B, T, H, dh, dtype):
     torch.manual_seed(T)
     qkv = torch.randn(B * T, 3 * H * dh) * 1.5
     out = tmae.ops.mha(qkv.to(dtype).to(DEV), B, T, H, dh, dh ** -0.5, dtype)
-    check("rel:out_float", rel(out.float(), _ref_attn(qkv.to(dtype).float(), B, T, H, dh)), (1e-4 if dtype == torch.float32 else 3e-2))
+    check("rel:out_float", rel(out.float(), _ref_attn(qkv.to(dtype).float(), B, T, H, dh)), (1e-4 if dtype == torch.float32 else 7e-3))
 
 
 # ------------------------------------------------------------------------------------ convs
@@ -179,7 +181,7 @@ def test_conv3x3_batched_addend(tmae, dtype):
         for j in range(nb2):
             ref = F.conv2d(x.to(dtype).float(), w[i, j].to(dtype).float(), b[i, j], padding=1)
             ref = F.gelu(ref.permute(0, 2, 3, 1).reshape(-1, cout) + add[:, (3 * i + j) * cout:(3 * i + j + 1) * cout])
-            assert rel(y[i, j], ref) < tol(dtype), (i, j)
+            check(f"rel:batched_{i}_{j}", rel(y[i, j], ref), tol(dtype))
 
 
 @pytest.mark.parametrize("n", [5, 64])
@@ -391,7 +393,7 @@ def test_block_module(tmae, dtype):
     ref = orc.block(x, sd, "b.", 4, 1e-6)
     blk = blk.to(DEV)
     blk.compute_dtype = dtype
-    check("rel:blk_x_to_DEV", rel(blk(x.to(DEV)), ref), (1e-4 if dtype == torch.float32 else 3e-2))
+    check("rel:blk_x_to_DEV", rel(blk(x.to(DEV)), ref), (1e-4 if dtype == torch.float32 else 7e-3))
 
 
 # ------------------------------------------------------------------------------------ loader crops

@@ -8,7 +8,7 @@ lrp_transform, MCM.py:165-293 applied at MCM.py:761-784) per workgroup.
   layer-0 input (slice 0's mean / scale stacks);
 * the MCM eval forward with the fused stacks against the layer-by-layer launches (TMAE_LIC_STACK=0) on
   the same weights, bf16, at the benched geometry.
-Tolerance: bf16 operands, f32 accumulation -> max|a-b| / max|b| <= 2e-2 per output.
+Tolerance: bf16 operands, f32 accumulation -> max|a-b| / max|b| <= 6e-3 per output (2x the measured 3.0e-3).
 """
 import os
 
@@ -20,7 +20,7 @@ from parity_log import check, record
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
 MID = [224, 176, 128, 80, 32]
-STACK_MAXREL = 2e-2  # bf16 operands; about 2x the measured error (profiles/r03/parity_metrics.jsonl)
+STACK_MAXREL = 6e-3  # bf16 operands; about 2x the largest measured error, 3.0e-3 (profiles/r03/parity_metrics.jsonl)
 
 
 def _bf(t):
@@ -162,11 +162,12 @@ def test_mcm_fused_stacks_match_layerwise(tmae):
     e_ms, e_lrp = _maxrel(a["musig"], b["musig"]), _maxrel(a["lrp"], b["lrp"])
     print(f"  mu/sigma (slices 6..11) max rel {e_ms:.2e}; 0.5 tanh(lrp) max rel {e_lrp:.2e}")
     record("log_ylik_maxdiff", float(ly.max()))
-    check("musig_maxrel", e_ms, 2e-2)
-    check("lrp_maxrel", e_lrp, 5e-2)
-    check("y_hat_flip_frac", flips / a["yh"].numel(), 1e-3, strict=False)
-    check("x_hat_relL2", xr, 2e-2)
-    check("log_ylik_meandiff", float(ly.mean()), 2e-2)
+    # bounds about 2x the measured values (5.4e-4, 1.0e-2, 0 flips, 3.0e-3, 0)
+    check("musig_maxrel", e_ms, 1.5e-3)
+    check("lrp_maxrel", e_lrp, 2e-2)
+    check("y_hat_flip_frac", flips / a["yh"].numel(), 1e-4, strict=False)
+    check("x_hat_relL2", xr, 6e-3)
+    check("log_ylik_meandiff", float(ly.mean()), 1e-3)
 
 
 @pytest.mark.parametrize("training,batched", [(False, "0"), (True, "0"), (False, "1")])

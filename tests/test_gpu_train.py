@@ -163,7 +163,7 @@ def test_layernorm_bwd_remap(T):
     ref = xr.grad.clone()
     ref[rows] += dres[rows]
     check("_rel:dx", _rel(dx, ref), 1e-5)
-    check("_rel:dxop_float", _rel(dxop.float(), ref), 1e-2)
+    check("_rel:dxop_float", _rel(dxop.float(), ref), 6e-3)
     assert _rel(dg, g_.grad) < 1e-5 and _rel(db, b_.grad) < 1e-5
 
 
@@ -196,7 +196,7 @@ def test_mha_bwd(T, T_, H, dh, dt):
         check("_rel:out", _rel(out, o), 1e-5)
         check("_rel:dq", _rel(dq, q_.grad), 1e-4)
     else:
-        check("_rel2:dq_float", _rel2(dq.float(), q_.grad), 2e-2)
+        check("_rel2:dq_float", _rel2(dq.float(), q_.grad), 5e-3)
 
 
 # ------------------------------------------------------------------------------ distortion
@@ -326,7 +326,7 @@ def test_mcm_train_bf16_close_to_f32():
     flat32 = torch.cat([g32[k].reshape(-1) for k in g32])
     flat16 = torch.cat([g16[k].reshape(-1) for k in g32])
     assert torch.isfinite(flat16).all()
-    check("_rel2:flat16", _rel2(flat16, flat32), 5e-2)
+    check("_rel2:flat16", _rel2(flat16, flat32), 3e-3)
 
 
 def _partial_loss_grads(m, imgs, scores, zn, yn, R, nsel):
@@ -368,9 +368,9 @@ def test_mcm_train_grads_vitb_batch64_f32_vs_oracle():
             continue
         e = _rel(g, r)
         worst = max(worst, e)
-        if e > 2e-3:
+        if e > 1e-5:
             bad.append((name, e))
-    check("grad_maxrel_worst_tensor_vitb_b64_f32", worst, 2e-3, tensors=len(hip))
+    check("grad_maxrel_worst_tensor_vitb_b64_f32", worst, 1e-5, tensors=len(hip))  # measured 3.5e-6
     assert not bad, bad[:20]
     # the benched operand dtype at the same batch against these f32 gradients
     m.compute_dtype = torch.bfloat16
@@ -378,7 +378,7 @@ def test_mcm_train_grads_vitb_batch64_f32_vs_oracle():
     flat32 = torch.cat([hip[k].reshape(-1) for k in hip])
     flat16 = torch.cat([g16[k].reshape(-1) for k in hip])
     assert torch.isfinite(flat16).all()
-    check("grad_relL2_bf16_vs_f32_vitb_b64", _rel2(flat16, flat32), 5e-2)
+    check("grad_relL2_bf16_vs_f32_vitb_b64", _rel2(flat16, flat32), 1e-2)  # measured 5.1e-3
 
 
 def test_mcm_train_vitb_step_runs():
