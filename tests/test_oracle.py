@@ -86,3 +86,23 @@ def test_pos_embed_vs_reference(golden_dir, tmae):
             pe = pe.astype(np.float32)
             assert hashlib.sha256(pe.tobytes()).hexdigest()[:16] == str(d[f"d{dim}_g{g}_sha"])
             np.testing.assert_array_equal(pe[[0, 1, g + 3, g * g]], d[f"d{dim}_g{g}_rows"])
+
+
+def test_interpolate_pos_embed_matches_reference(golden_dir):
+    """pos_embed.interpolate_pos_embed against the reference function's outputs (tools/gen_golden.py
+    gen_pos_interp): grid up / down / same size, one and two extra tokens; bitwise"""
+    import types
+
+    from textmae_amd.pos_embed import interpolate_pos_embed
+
+    d = np.load(os.path.join(golden_dir, "pos_interp.npz"))
+    names = sorted({k.rsplit("_", 1)[0] for k in d.files})
+    assert len(names) == 4
+    for n in names:
+        src_g, dst_g, dim, extra = d[f"{n}_meta"].tolist()
+        ck = {"pos_embed": torch.from_numpy(d[f"{n}_in"]), "other": torch.zeros(1)}
+        model = types.SimpleNamespace(encoder_embed=types.SimpleNamespace(num_patches=dst_g * dst_g),
+                                      encoder_pos_embed=torch.zeros(1, extra + dst_g * dst_g, dim))
+        interpolate_pos_embed(model, ck)
+        assert ck["pos_embed"].shape == (1, extra + dst_g * dst_g, dim), n
+        assert np.array_equal(ck["pos_embed"].numpy(), d[f"{n}_out"]), n

@@ -12,7 +12,8 @@ from .mae import (MaskedAutoencoderViT, mae_vit_base_patch16, mae_vit_base_patch
                   mae_vit_huge_patch14, mae_vit_huge_patch14_dec512d8b, mae_vit_large_patch16,
                   mae_vit_large_patch16_dec512d8b)
 from .mcm import MCM  # noqa: F401
+from .pos_embed import get_2d_sincos_pos_embed, interpolate_pos_embed  # noqa: F401
 
 __all__ = ["MCM", "MaskedAutoencoderViT", "mae_vit_base_patch16_dec512d8b", "mae_vit_large_patch16_dec512d8b",
            "mae_vit_huge_patch14_dec512d8b", "Block", "PatchEmbed", "EntropyBottleneck", "GaussianConditional", "CompressionModel", "ops",
-           "load_library", "LIB_PATH", "get_scale_table"]
+           "load_library", "LIB_PATH", "get_scale_table", "get_2d_sincos_pos_embed", "interpolate_pos_embed"]

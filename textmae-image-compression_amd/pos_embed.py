@@ -20,3 +20,28 @@ def get_2d_sincos_pos_embed(embed_dim: int, grid_size: int, cls_token: bool = Fa
     if cls_token:
         emb = np.concatenate([np.zeros([1, embed_dim]), emb], axis=0)
     return emb
+
+
+def interpolate_pos_embed(model, checkpoint_model) -> None:
+    """Resample a checkpoint's ``pos_embed`` to the model's patch grid, in place (reference
+    models/Compression/common/pos_embed.py:103-132, DeiT's recipe; called by training.py:173-174 when
+    ``--checkpoint`` is given).  The leading extra tokens (cls) are kept; the square grid of position
+    tokens is resized bicubically (align_corners=False) from the checkpoint's side to sqrt(num_patches).
+    A one-time host-side checkpoint edit, not part of the device path: it runs on the checkpoint's
+    tensors with torch's own bicubic kernel, so the result is bitwise the reference's
+    (tests/golden/pos_interp.npz, made by the reference function)."""
+    import torch
+
+    if "pos_embed" not in checkpoint_model:
+        return
+    pe = checkpoint_model["pos_embed"]
+    dim = pe.shape[-1]
+    num_patches = model.encoder_embed.num_patches
+    extra = model.encoder_pos_embed.shape[-2] - num_patches
+    src = int((pe.shape[-2] - extra) ** 0.5)
+    dst = int(num_patches ** 0.5)
+    if src == dst:
+        return
+    grid = pe[:, extra:].reshape(-1, src, src, dim).permute(0, 3, 1, 2)
+    grid = torch.nn.functional.interpolate(grid, size=(dst, dst), mode="bicubic", align_corners=False)
+    checkpoint_model["pos_embed"] = torch.cat((pe[:, :extra], grid.permute(0, 2, 3, 1).flatten(1, 2)), dim=1)

@@ -252,20 +252,49 @@ def gen_state_keys(MCM):
     print("mcm_state_keys.json")
 
 
+# ---------------------------------------------------------------------------------------- F3b
+def gen_pos_interp():
+    """interpolate_pos_embed (pos_embed.py:103-132, called by training.py:173-174 on --checkpoint): the
+    reference function on seeded checkpoint tables, for target models given by (num_patches, rows of
+    encoder_pos_embed) -- 14x14 -> 16x16 (224 checkpoint into a 256 model), 16x16 -> 12x12, same size"""
+    import types
+
+    from models.Compression.common.pos_embed import interpolate_pos_embed
+
+    data = {}
+    g = torch.Generator().manual_seed(21)
+    for name, (src_g, dst_g, d, extra) in {"g14_to_g16": (14, 16, 96, 1), "g16_to_g12": (16, 12, 64, 1),
+                                            "g8_to_g8": (8, 8, 32, 1), "g7_to_g9_two_extra": (7, 9, 16, 2)}.items():
+        ck = {"pos_embed": torch.randn(1, extra + src_g * src_g, d, generator=g), "other": torch.zeros(1)}
+        model = types.SimpleNamespace(encoder_embed=types.SimpleNamespace(num_patches=dst_g * dst_g),
+                                      encoder_pos_embed=torch.zeros(1, extra + dst_g * dst_g, d))
+        data[f"{name}_in"] = ck["pos_embed"].numpy()
+        interpolate_pos_embed(model, ck)
+        data[f"{name}_out"] = ck["pos_embed"].numpy()
+        data[f"{name}_meta"] = np.array([src_g, dst_g, d, extra])
+    np.savez_compressed(os.path.join(OUT, "pos_interp.npz"), **data)
+    print("pos_interp.npz")
+
+
 def main():
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", nargs="*", help="generators to run (default: all)")
+    only = ap.parse_args().only
     os.makedirs(OUT, exist_ok=True)
     install_stubs()
     import models.Compression.common.pos_embed  # noqa: F401  (real reference module)
     from models.Compression.MCM import MCM
 
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    gen_ids(MCM)
-    gen_pos()
-    gen_forward(MCM, "tiny", TINY, batch=2, seed=7)
-    gen_forward(MCM, "small12", SMALL12, batch=2, seed=11)
-    gen_mae_masking()
-    gen_mae_forward()
-    gen_state_keys(MCM)
+    gens = {"ids": lambda: gen_ids(MCM), "pos": gen_pos, "pos_interp": gen_pos_interp,
+            "tiny": lambda: gen_forward(MCM, "tiny", TINY, batch=2, seed=7),
+            "small12": lambda: gen_forward(MCM, "small12", SMALL12, batch=2, seed=11),
+            "mae_masking": gen_mae_masking, "mae_forward": gen_mae_forward, "state_keys": lambda: gen_state_keys(MCM)}
+    for k, fn in gens.items():
+        if not only or k in only:
+            fn()
 
 
 if __name__ == "__main__":
