@@ -221,8 +221,8 @@ def test_config4_vitl_bench_batch_bf16(tmae):
 @pytest.mark.parametrize("training", [False, True])
 def test_pipelined_forward_bitwise(tmae, training):
     """MCM.pipeline = 2 (two half-batch executors on two streams, the second half's encoder under the first
-    half's slice loop): x_hat and both likelihoods bit for bit the one-pipeline forward's (eager; bf16, ViT-B
-    256^2, K=144, batch 16; training mode with injected noise)"""
+    half's slice loop): x_hat and both likelihoods bit for bit the one-pipeline forward's, eager and replayed
+    from a captured HIP graph (bf16, ViT-B 256^2, K=144, batch 16; training mode with injected noise)"""
     torch.manual_seed(3)
     m = tmae.MCM(img_size=256, num_keep_patches=144).to(DEV).eval()
     m.compute_dtype = torch.bfloat16
@@ -241,5 +241,12 @@ def test_pipelined_forward_bitwise(tmae, training):
         torch.cuda.synchronize()
         for a, b in zip((got["x_hat"], got["likelihoods"]["y"], got["likelihoods"]["z"]), ref):
             assert torch.equal(a, b)
+        if not training:
+            graph, out = _graph_forward(m, imgs, scores)
+            graph.replay()
+            torch.cuda.synchronize()
+            for a, b in zip((out["x_hat"], out["likelihoods"]["y"], out["likelihoods"]["z"]), ref):
+                assert torch.equal(a, b)
+            del graph
     m.pipeline = 1
     m.eval()
