@@ -446,7 +446,6 @@ class _Executor:
         self.dec = z(B * Td, Dd)
         self.dec_s = BlockScratch(B * Td, Dd, hid_d, dt, dev)
         self.dn = z(B * self.L, Dd, dtype=dt)
-        self.IDS = None  # (ids_shuffle, ids_restore) buffers of the pipelined forward
 
     # ------------------------------------------------------------------ weights
     def refresh_weights(self):
@@ -581,7 +580,7 @@ class _Executor:
         else:
             z_noise = y_noise = None
 
-        shuf, rest = self._front(imgs, scores, ids_out=out is not None)
+        shuf, rest = self._front(imgs, scores)
         if after_front is not None:
             after_front()
 
@@ -650,16 +649,13 @@ class _Executor:
         shuf = ops.invert_permutation(ids_restore.to(self.device))
         return self._back(shuf, m.encoder_embed.proj.in_channels)
 
-    def _front(self, imgs, scores, ids_out=False):
-        """encoder + g_a + h_a (MCM.py:590-634, 729-739): tokens -> Y32/YT -> Z; returns (ids_shuffle, ids_restore)
-        (ids_out: into this executor's own buffers -- no allocation, for the pipelined forward's second stream)"""
+    def _front(self, imgs, scores):
+        """encoder + g_a + h_a (MCM.py:590-634, 729-739): tokens -> Y32/YT -> Z; returns (ids_shuffle, ids_restore)"""
         m, dt, B = self.m, self.dtype, self.batch
         E, M, K, P, g = m.encoder_embed_dim, m.latent_depth, m.num_keep_patches, self.P, self.g
         Te = K + 1
         # ---- encoder (MCM.py:590-634): ids on device, embed only the kept patches
-        if ids_out and self.IDS is None:
-            self.IDS = torch.empty((2, B, self.L), dtype=torch.int64, device=self.device)
-        shuf, rest = ops.ids_shuffle(scores, K, m.sum_lanes, out=(self.IDS[0], self.IDS[1]) if ids_out else None)
+        shuf, rest = ops.ids_shuffle(scores, K, m.sum_lanes)
         pos_e = m.encoder_pos_embed.detach()
         ops.patch_embed(imgs, shuf, self.w_pe, m.encoder_embed.proj.bias.detach(), pos_e, self.tok, K, P, dt)
         ops.cls_rows(self.tok, m.cls_token.detach(), pos_e, B, Te, E)

@@ -60,18 +60,12 @@ def gemm_plan(M: int, N: int, K: int, dtype: torch.dtype, batch: int = 1) -> str
 
 
 # --------------------------------------------------------------------------------------- masking
-def ids_shuffle(scores: torch.Tensor, keep: int, sum_lanes: int = 8, out=None):
-    """MCM.get_ids_shuffle + argsort (MCM.py:364-423, 579-580) -> (ids_shuffle, ids_restore) int64
-    (into `out` = (shuf, rest) when given)."""
+def ids_shuffle(scores: torch.Tensor, keep: int, sum_lanes: int = 8):
+    """MCM.get_ids_shuffle + argsort (MCM.py:364-423, 579-580) -> (ids_shuffle, ids_restore) int64."""
     s = _need(scores.float().contiguous(), name="total_scores")
     n, L = s.shape
-    if out is not None:
-        shuf, rest = out
-        if shuf.shape != (n, L) or rest.shape != (n, L) or shuf.dtype != torch.int64 or rest.dtype != torch.int64:
-            raise ValueError("ids_shuffle: out must be two int64 [n, L] tensors")
-    else:
-        shuf = torch.empty((n, L), dtype=torch.int64, device=s.device)
-        rest = torch.empty_like(shuf)
+    shuf = torch.empty((n, L), dtype=torch.int64, device=s.device)
+    rest = torch.empty_like(shuf)
     _lib.call("tmae_ids_shuffle", s.data_ptr(), shuf.data_ptr(), rest.data_ptr(), n, L, keep, sum_lanes, _stream())
     return shuf, rest
 
