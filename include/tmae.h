@@ -356,7 +356,9 @@ int tmae_patch_gather(const float* imgs, const int64_t* ids_shuffle, void* out, 
  * B dense (same remap) or, b_conv = 1, the implicit im2col of a 3x3 conv (padding 1, stride b_stride) over
  * NHWC maps (channels [0, b_c1) from b, the rest from b2; column = tap * b_Cin + ci).  The split-K partials
  * ([splits][M][N] f32 in work, see tmae_wgrad_workspace) are summed in a fixed order and written to
- * out[o_base + m*o_sm + (n % o_cp)*o_sc + (n / o_cp)*o_st] (= or += with accumulate). */
+ * out[o_base + m*o_sm + (n % o_cp)*o_sc + (n / o_cp)*o_st] (= or += with accumulate).
+ * bias_out (optional): bias_out[m] (= or += with bias_accumulate) sum_k A(k, m), the bias gradient of the layer
+ * whose output gradient A is (the reference's autograd column sum over rows), formed inside the same GEMM. */
 typedef struct tmae_wgrad_args {
   const void* a; int lda; int a_G, a_Gs, a_off;
   const void* b; int ldb; int b_G, b_Gs, b_off;
@@ -364,6 +366,7 @@ typedef struct tmae_wgrad_args {
   int M, N, K;
   float* work; long long work_elems;
   float* out; long long o_base, o_sm, o_sc, o_st; int o_cp; int accumulate;
+  float* bias_out; int bias_accumulate;
 } tmae_wgrad_args;
 int tmae_wgrad(const tmae_wgrad_args* args, int dtype, void* stream);
 long long tmae_wgrad_workspace(int M, int N, int K, int dtype);

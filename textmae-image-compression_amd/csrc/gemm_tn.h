@@ -52,11 +52,13 @@ template <typename T> struct KConvSrc {
   }
 };
 
-// partial tile -> workspace slab of this split
+// partial tile -> workspace slab of this split; bws (optional): the bias slab [split][M] of column sums
 struct EpiSplitWs {
   float* ws;
   int N;
   long long slab;
+  float* bws;
+  int M;
   __device__ void batch(int, int) {}
   __device__ void operator()(int m, int n, f32x4 v) const { store4(ws + (size_t)m * N + n, v); }
   __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const { store8(ws + (size_t)m * N + n, lo, hi); }
@@ -82,7 +84,12 @@ __device__ __forceinline__ bf16x8 tn_frag(const unsigned char* img, int rb, int 
 
 // ------------------------------------------------------------------ bf16 kernel
 // AS = M-side source (MFMA B operand), BS = N-side source (MFMA A operand, rows of the accumulator).
-template <int BN, int BM, int WGN, int NW, class AS, class BS>
+// BIAS: also the column sums sum_k A(k, m) of this split's k range (the bias gradient of the layer whose
+// output gradient A is, reference: the colsum over rows of dY) by MFMAs against an all-ones A fragment:
+// ones^T B = the column sums in every accumulator row.  The same sums are wanted by every (tn, wn) that
+// shares the M columns, so fragment j of a wave is computed by exactly one of them (j = r mod P, P =
+// ntn * WGN sharers): at most ceil(TM / P) extra MFMAs per K-substep on top of TN * TM.
+template <int BN, int BM, int WGN, int NW, bool BIAS, class AS, class BS>
 __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2)
 gemm_tn_bf16_kernel(AS as, BS bs, EpiSplitWs epi, int M, int N, int K, int kchunk) {
   constexpr int BK = 64;
@@ -106,6 +113,8 @@ gemm_tn_bf16_kernel(AS as, BS bs, EpiSplitWs epi, int M, int N, int K, int kchun
   const int k0 = blockIdx.y * kchunk, k1 = min(K, k0 + kchunk);
   const int nk = k1 > k0 ? (k1 - k0 + BK - 1) / BK : 0;
   epi.ws += (size_t)blockIdx.y * epi.slab;
+  // bias fragments owned by this wave (wave-uniform): j with j % P == r % P
+  const int bias_P = ntn * WGN, bias_r = tn * WGN + wn;
 
   // this lane's DMA slots: piece p of the wave covers image bytes [(wave + NW p) KiB, +1 KiB)
   int nrow[WPN], ncol[WPN], mrow[WPM], mcol[WPM];
@@ -146,6 +155,13 @@ gemm_tn_bf16_kernel(AS as, BS bs, EpiSplitWs epi, int M, int N, int K, int kchun
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  f32x4 bacc[TM];
+#pragma unroll
+  for (int j = 0; j < TM; ++j) bacc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
+
   const int g = lane >> 4, ii = lane & 15, q = ii >> 2, pp = ii & 3;
   if (nk > 0) {
     issue(0, 0);
@@ -167,10 +183,24 @@ gemm_tn_bf16_kernel(AS as, BS bs, EpiSplitWs epi, int M, int N, int K, int kchun
         for (int i = 0; i < TN; ++i)
 #pragma unroll
           for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        if constexpr (BIAS) {
+#pragma unroll
+          for (int j = 0; j < TM; ++j)
+            if ((j - bias_r) % bias_P == 0) bacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, b[j], bacc[j], 0, 0, 0);
+        }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       stage ^= 1;
+    }
+  }
+  if constexpr (BIAS) {
+    // every accumulator row holds the column sums: lanes 0-15 (rows 0-3, column fr) store them
+    float* bw = epi.bws + (size_t)blockIdx.y * M;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = tm * BM + wm * WM + 16 * j + ii;
+      if ((j - bias_r) % bias_P == 0 && lane < 16 && m < M) bw[m] = bacc[j][0];
     }
   }
   static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= 2 * STAGE, "tn: epilogue region exceeds the LDS ring");
@@ -258,23 +288,34 @@ static inline TnPlan tn_plan(int M, int N, int K, bool bf) {
   return p;
 }
 
+// bws (bias slab [splits][M]) non-null: the kernel also forms the column sums of A (BIAS instantiation)
 template <class AS, class BS>
-static int launch_tn_bf16(const TnPlan& p, const AS& as, const BS& bs, float* ws, int M, int N, int K, hipStream_t st) {
+static int launch_tn_bf16(const TnPlan& p, const AS& as, const BS& bs, float* ws, float* bws, int M, int N, int K,
+                          hipStream_t st) {
   const int tiles = ceil_div(N, p.bn) * ceil_div(M, p.bm);
-  EpiSplitWs e{ws, N, (long long)M * N};
-  if (p.nw == 8)
-    hipLaunchKernelGGL((gemm_tn_bf16_kernel<256, 256, 2, 8, AS, BS>), dim3(tiles, p.splits), dim3(512), 0, st, as, bs,
-                       e, M, N, K, p.kchunk);
-  else
-    hipLaunchKernelGGL((gemm_tn_bf16_kernel<128, 128, 2, 4, AS, BS>), dim3(tiles, p.splits), dim3(256), 0, st, as, bs,
-                       e, M, N, K, p.kchunk);
+  EpiSplitWs e{ws, N, (long long)M * N, bws, M};
+  if (p.nw == 8) {
+    if (bws)
+      hipLaunchKernelGGL((gemm_tn_bf16_kernel<256, 256, 2, 8, true, AS, BS>), dim3(tiles, p.splits), dim3(512), 0, st,
+                         as, bs, e, M, N, K, p.kchunk);
+    else
+      hipLaunchKernelGGL((gemm_tn_bf16_kernel<256, 256, 2, 8, false, AS, BS>), dim3(tiles, p.splits), dim3(512), 0, st,
+                         as, bs, e, M, N, K, p.kchunk);
+  } else {
+    if (bws)
+      hipLaunchKernelGGL((gemm_tn_bf16_kernel<128, 128, 2, 4, true, AS, BS>), dim3(tiles, p.splits), dim3(256), 0, st,
+                         as, bs, e, M, N, K, p.kchunk);
+    else
+      hipLaunchKernelGGL((gemm_tn_bf16_kernel<128, 128, 2, 4, false, AS, BS>), dim3(tiles, p.splits), dim3(256), 0, st,
+                         as, bs, e, M, N, K, p.kchunk);
+  }
   TMAE_LAUNCH_CHECK("tmae_wgrad");
 }
 
 template <class AS, class BS>
 static int launch_tn_f32(const TnPlan& p, const AS& as, const BS& bs, float* ws, int M, int N, int K, hipStream_t st) {
   const int tiles = ceil_div(N, 64) * ceil_div(M, 64);
-  EpiSplitWs e{ws, N, (long long)M * N};
+  EpiSplitWs e{ws, N, (long long)M * N, nullptr, M};
   hipLaunchKernelGGL((gemm_tn_f32_kernel<AS, BS>), dim3(tiles, p.splits), dim3(256), 0, st, as, bs, e, M, N, K,
                      p.kchunk);
   TMAE_LAUNCH_CHECK("tmae_wgrad");

@@ -5,7 +5,10 @@
 #include "gemm_tn.h"
 
 static int tmae_wgrad_reduce(const float* ws, int splits, int M, int N, float* out, long long base, long long sm,
-                             long long sc, long long st, int cp, int accumulate, hipStream_t s);
+                             long long sc, long long st, int cp, int accumulate, const float* bws, float* bias_out,
+                             int bias_accumulate, hipStream_t s);
+static int colsum_into(const void* x, int x_dtype, int ld, int rows, int C, int row_group, int group_stride,
+                       int row_offset, float* work, long long work_elems, float* out, int accumulate, hipStream_t st);
 static int tmae_ln_fold(const float* part, int waves, int D, float* dg, float* db, int accumulate, hipStream_t st);
 
 // ================================================================== helpers
@@ -53,8 +56,12 @@ static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
   TMAE_REQUIRE(a.a_G > 0 && a.o_cp > 0, "tmae_wgrad: bad row group / column period");
   const bool bf = sizeof(T) == 2;
   const TnPlan p = tn_plan(a.M, a.N, a.K, bf);
-  TMAE_REQUIRE((long long)p.splits * a.M * a.N <= a.work_elems, "tmae_wgrad: workspace too small (%lld < %lld)",
-               a.work_elems, (long long)p.splits * a.M * a.N);
+  const long long slabs = (long long)p.splits * a.M * a.N;
+  TMAE_REQUIRE(slabs + (long long)p.splits * a.M <= a.work_elems, "tmae_wgrad: workspace too small (%lld < %lld)",
+               a.work_elems, slabs + (long long)p.splits * a.M);
+  // bias column sums: in the bf16 kernel (slab [splits][M] after the partial tiles); the f32 parity path
+  // runs the column-sum kernels on A after the GEMM
+  float* bws = (a.bias_out && bf) ? a.work + slabs : nullptr;
   KDenseSrc<T> as{(const T*)a.a, a.lda, a.M, a.a_G, a.a_Gs, a.a_off};
   int rc;
   if (a.b_conv) {
@@ -65,25 +72,41 @@ static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
     bs.x1 = (const T*)a.b; bs.x2 = (const T*)a.b2; bs.c1 = a.b_c1; bs.ld1 = a.ldb; bs.ld2 = a.b_ld2; bs.Cin = a.b_Cin;
     bs.H = a.b_H; bs.W = a.b_W; bs.stride = a.b_stride;
     bs.Ho = (a.b_H + 2 - 3) / a.b_stride + 1; bs.Wo = (a.b_W + 2 - 3) / a.b_stride + 1; bs.cols = a.N;
-    rc = bf ? launch_tn_bf16(p, as, bs, a.work, a.M, a.N, a.K, st) : launch_tn_f32(p, as, bs, a.work, a.M, a.N, a.K, st);
+    rc = bf ? launch_tn_bf16(p, as, bs, a.work, bws, a.M, a.N, a.K, st)
+            : launch_tn_f32(p, as, bs, a.work, a.M, a.N, a.K, st);
   } else {
     TMAE_REQUIRE(a.ldb % e == 0 && a.b_G > 0, "tmae_wgrad: ldb");
     KDenseSrc<T> bs{(const T*)a.b, a.ldb, a.N, a.b_G, a.b_Gs, a.b_off};
-    rc = bf ? launch_tn_bf16(p, as, bs, a.work, a.M, a.N, a.K, st) : launch_tn_f32(p, as, bs, a.work, a.M, a.N, a.K, st);
+    rc = bf ? launch_tn_bf16(p, as, bs, a.work, bws, a.M, a.N, a.K, st)
+            : launch_tn_f32(p, as, bs, a.work, a.M, a.N, a.K, st);
   }
   if (rc != TMAE_OK) return rc;
-  return tmae_wgrad_reduce(a.work, p.splits, a.M, a.N, a.out, a.o_base, a.o_sm, a.o_sc, a.o_st, a.o_cp, a.accumulate, st);
+  rc = tmae_wgrad_reduce(a.work, p.splits, a.M, a.N, a.out, a.o_base, a.o_sm, a.o_sc, a.o_st, a.o_cp, a.accumulate,
+                         bws, bws ? a.bias_out : nullptr, a.bias_accumulate, st);
+  if (rc != TMAE_OK || !a.bias_out || bf) return rc;
+  // f32: the partial-tile slabs are consumed; their space is the column sums' workspace
+  return colsum_into(a.a, TMAE_F32, a.lda, a.K, a.M, a.a_G, a.a_Gs, a.a_off, a.work, a.work_elems, a.bias_out,
+                     a.bias_accumulate, st);
 }
 
 // fixed-order sum over the split slabs, scattered into the parameter's layout:
 // dst = base + m*sm + (n % cp)*sc + (n / cp)*st   (dense [M][N]: sm=N, sc=1, cp=N; conv [co][ci][3][3]
 // from columns tap*Cin + ci: sm=cin_total*9, sc=9, st=1, cp=Cin, base=ci_off*9; transposed: sm=1, sc=M)
+// Threads past M*N fold the bias slab [splits][M] (same fixed order) into bias_out.
 __global__ void __launch_bounds__(256)
 tn_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N, float* __restrict__ out, long long base,
-                 long long sm, long long sc, long long st, int cp, int accumulate) {
+                 long long sm, long long sc, long long st, int cp, int accumulate, const float* __restrict__ bws,
+                 float* __restrict__ bias_out, int bias_accumulate) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   const long long tot = (long long)M * N;
-  if (i >= tot) return;
+  if (i >= tot) {
+    const long long m = i - tot;
+    if (!bias_out || m >= M) return;
+    float s = 0.0f;
+    for (int k = 0; k < splits; ++k) s += bws[(size_t)k * M + m];
+    bias_out[m] = bias_accumulate ? bias_out[m] + s : s;
+    return;
+  }
   const int m = (int)(i / N), n = (int)(i - (long long)m * N);
   float s = 0.0f;
   for (int k = 0; k < splits; ++k) s += ws[(size_t)k * tot + i];
@@ -92,11 +115,12 @@ tn_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N, float* 
 }
 
 static int tmae_wgrad_reduce(const float* ws, int splits, int M, int N, float* out, long long base, long long sm,
-                             long long sc, long long st, int cp, int accumulate, hipStream_t s) {
-  const long long tot = (long long)M * N;
+                             long long sc, long long st, int cp, int accumulate, const float* bws, float* bias_out,
+                             int bias_accumulate, hipStream_t s) {
+  const long long tot = (long long)M * N + (bias_out ? M : 0);
   if (tot == 0) return TMAE_OK;
   hipLaunchKernelGGL(tn_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, ws, splits, M, N, out,
-                     base, sm, sc, st, cp, accumulate);
+                     base, sm, sc, st, cp, accumulate, bws, bias_out, bias_accumulate);
   TMAE_LAUNCH_CHECK("tmae_wgrad");
 }
 
@@ -109,7 +133,7 @@ extern "C" int tmae_wgrad(const tmae_wgrad_args* a, int dtype, void* stream) {
 
 extern "C" long long tmae_wgrad_workspace(int M, int N, int K, int dtype) {
   const TnPlan p = tn_plan(M, N, K, dtype == TMAE_BF16);
-  return (long long)p.splits * M * N;
+  return (long long)p.splits * M * N + (long long)p.splits * M;  // partial tiles + bias column-sum slab
 }
 
 // ================================================================== data gradients (NT core on transposed weights)
@@ -459,9 +483,14 @@ static void fold_rows(const float* part, int rows, int C, float* out0, float* ou
 
 extern "C" int tmae_colsum(const void* x, int x_dtype, int ld, int rows, int C, int row_group, int group_stride,
                            int row_offset, float* work, long long work_elems, float* out, int accumulate, void* stream) {
+  return colsum_into(x, x_dtype, ld, rows, C, row_group, group_stride, row_offset, work, work_elems, out, accumulate,
+                     (hipStream_t)stream);
+}
+
+static int colsum_into(const void* x, int x_dtype, int ld, int rows, int C, int row_group, int group_stride,
+                       int row_offset, float* work, long long work_elems, float* out, int accumulate, hipStream_t st) {
   TMAE_REQUIRE(x && out && work && row_group > 0, "tmae_colsum: bad arguments");
   if (C == 0) return TMAE_OK;
-  hipStream_t st = (hipStream_t)stream;
   int splits = std::max(1, std::min(256, rows / 32));
   while ((long long)splits * C > work_elems && splits > 1) splits /= 2;
   TMAE_REQUIRE((long long)splits * C <= work_elems, "tmae_colsum: workspace too small");

@@ -468,8 +468,7 @@ class TrainExec:
         # ---- decoder_pred + unpatchify (MCM.py:683-686, 797)
         dP = T.patchify(dxhat, self._e(B * L, dxhat.shape[1] * P * P), P, dt)
         npred = dP.shape[1]
-        T.wgrad(dP, self.dn, npred, Dd, B * L, G(m.decoder_pred.weight), dt)
-        T.colsum(dP, B * L, npred, G(m.decoder_pred.bias))
+        T.wgrad(dP, self.dn, npred, Dd, B * L, G(m.decoder_pred.weight), dt, bias=G(m.decoder_pred.bias))
         ddn = torch.empty((B * L, Dd), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dP, W.t(m.decoder_pred.weight), B * L, npred, Dd, dt, out=ddn)
         ddec = self._z(B * Td, Dd)
@@ -485,8 +484,7 @@ class TrainExec:
         # ---- decoder_embed + mask tokens (MCM.py:657-675)
         dtok = self._e(Mp, Dd)
         T.decoder_embed_bwd_gather(ddec, self.shuf, dtok, B, K, L, Dd, dt, dmask=G(m.mask_token).view(-1))
-        T.wgrad(dtok, self.gs_out, Dd, E, Mp, G(m.decoder_embed.weight), dt)
-        T.colsum(dtok, Mp, Dd, G(m.decoder_embed.bias))
+        T.wgrad(dtok, self.gs_out, Dd, E, Mp, G(m.decoder_embed.weight), dt, bias=G(m.decoder_embed.bias))
         d = self._e(Mp, E)
         T.dgrad_linear(dtok, W.t(m.decoder_embed.weight), Mp, Dd, E, dt, out=d)
         self._ready(m.mask_token)
@@ -498,8 +496,7 @@ class TrainExec:
             x, _ = self.gs[j]
             pre_prev = self.gs[j - 1][1] if j > 0 else None
             cin, cout = l.in_channels, l.out_channels
-            T.wgrad(d, x, cout, cin, Mp, G(l.weight), dt, layout="dense_t")
-            T.colsum(d, Mp, cout, G(l.bias))
+            T.wgrad(d, x, cout, cin, Mp, G(l.weight), dt, layout="dense_t", bias=G(l.bias))
             dx = self._e(Mp, cin)
             T.dgrad_linear(d, W.raw(l.weight), Mp, cout, cin, dt, out=dx, pre=pre_prev)
             d = dx
@@ -532,8 +529,7 @@ class TrainExec:
             cout = c.out_channels
             Ho = (H + 2 - 3) // s + 1
             T.wgrad(d, x, cout, 9 * cin, B * Ho * Ho, G(c.weight), dt,
-                    conv=dict(c1=cin, H=H, W=H, stride=s, cin=cin), layout="conv")
-            T.colsum(d, B * Ho * Ho, cout, G(c.bias))
+                    conv=dict(c1=cin, H=H, W=H, stride=s, cin=cin), layout="conv", bias=G(c.bias))
             if j > 0:
                 dx = self._e(B * H * H, cin)
                 T.conv_dgrad(d, W.conv_dg(c.weight), B, H, H, s, cout, cin, dt, out=dx, pre=pre_prev)
@@ -550,8 +546,7 @@ class TrainExec:
             x, _ = self.ga[j]
             pre_prev = self.ga[j - 1][1] if j > 0 else None
             cin, cout = l.in_channels, l.out_channels
-            T.wgrad(d, x, cout, cin, Mp, G(l.weight), dt)
-            T.colsum(d, Mp, cout, G(l.bias))
+            T.wgrad(d, x, cout, cin, Mp, G(l.weight), dt, bias=G(l.bias))
             if j > 0:
                 dx = self._e(Mp, cin)
                 T.dgrad_linear(d, W.t(l.weight), Mp, cout, cin, dt, out=dx, pre=pre_prev)
@@ -613,8 +608,7 @@ class TrainExec:
         dh = self._e(rows, hid)
         T.dgrad_linear(dres_op, W.t(blk.mlp.fc2.weight), rows, D, hid, dt, out=dh, pre=s.hpre)
         # fc1
-        T.wgrad(dh, s.a2, hid, D, rows, G(blk.mlp.fc1.weight), dt)
-        T.colsum(dh, rows, hid, G(blk.mlp.fc1.bias))
+        T.wgrad(dh, s.a2, hid, D, rows, G(blk.mlp.fc1.weight), dt, bias=G(blk.mlp.fc1.bias))
         da2 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dh, W.t(blk.mlp.fc1.weight), rows, hid, D, dt, out=da2)
         # norm2 + residual
@@ -630,9 +624,8 @@ class TrainExec:
         dqkv = self._e(rows, 3 * D)
         T.mha_bwd(s.qkv, s.att, datt, s.lse, dqkv, B, Tn, H, D // H, blk.attn.scale, dt)
         # qkv
-        T.wgrad(dqkv, s.a1, 3 * D, D, rows, G(blk.attn.qkv.weight), dt)
-        if blk.attn.qkv.bias is not None:
-            T.colsum(dqkv, rows, 3 * D, G(blk.attn.qkv.bias))
+        T.wgrad(dqkv, s.a1, 3 * D, D, rows, G(blk.attn.qkv.weight), dt,
+                bias=G(blk.attn.qkv.bias) if blk.attn.qkv.bias is not None else None)
         da1 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dqkv, W.t(blk.attn.qkv.weight), rows, 3 * D, D, dt, out=da1)
         # norm1 + residual
@@ -651,8 +644,7 @@ class TrainExec:
             x, cin, H, _, _ = saved[j]
             cout = c.out_channels
             T.wgrad(d, x, cout, 9 * cin, B * H * H, G(c.weight), dt, conv=dict(c1=cin, H=H, W=H, cin=cin),
-                    layout="conv")
-            T.colsum(d, B * H * H, cout, G(c.bias))
+                    layout="conv", bias=G(c.bias))
             if j == 0:
                 T.conv_dgrad(d, W.conv_dg(c.weight), B, H, H, 1, cout, cin, dt, routes=[(dZH, cin, cin)])
                 break
@@ -711,8 +703,7 @@ class TrainExec:
             cin, cout = c.in_channels, c.out_channels
             act_prev, pre_prev = saved[l - 1]
             T.wgrad(d, act_prev, cout, 9 * cin, Mp, G(c.weight), dt, conv=dict(c1=cin, H=g, W=g, cin=cin),
-                    layout="conv")
-            T.colsum(d, Mp, cout, G(c.bias))
+                    layout="conv", bias=G(c.bias))
             dx = self._e(Mp, cin)
             T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, out=dx, pre=pre_prev)
             d = dx
@@ -720,8 +711,7 @@ class TrainExec:
         x1, c1, ld1, x2, c2, ld2 = first
         cin, cout = c1 + c2, c.out_channels
         T.wgrad(d, x1, cout, 9 * cin, Mp, G(c.weight), dt, ldb=ld1,
-                conv=dict(x2=x2, c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv")
-        T.colsum(d, Mp, cout, G(c.bias))
+                conv=dict(x2=x2, c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
         # zero-width routes (no support slices yet) stay in place: their limits still partition the channels
         T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
 

@@ -73,8 +73,9 @@ def patch_gather(imgs, ids, out, keep, patch, dtype):
 
 # ------------------------------------------------------------------------------------- gradients
 def wgrad(a, b, M, N, K, out, dtype, lda=None, ldb=None, a_remap=(None, 0, 0), b_remap=(None, 0, 0), conv=None,
-          layout="dense", cin_total=None, ci_off=0, accumulate=False):
-    """out <- sum_k A(k, m) B(k, n) in the parameter's layout.
+          layout="dense", cin_total=None, ci_off=0, accumulate=False, bias=None, bias_accumulate=False):
+    """out <- sum_k A(k, m) B(k, n) in the parameter's layout; bias (optional) <- sum_k A(k, m), the bias
+    gradient of the layer whose output gradient A is, formed by the same GEMM.
     layout: "dense" (out [M][N]), "dense_t" (out [N][M]: ConvTranspose2d 1x1 weights), "conv"
     (out [M][cin_total][3][3], columns of B = tap * Cin + ci land at input channel ci_off + ci).
     conv = dict(x2=None, c1=..., ld2=0, H=, W=, stride=, cin=) selects the implicit im2col of B."""
@@ -112,6 +113,8 @@ def wgrad(a, b, M, N, K, out, dtype, lda=None, ldb=None, a_remap=(None, 0, 0), b
     else:
         raise ValueError(layout)
     args.accumulate = int(accumulate)
+    args.bias_out = _p(bias)
+    args.bias_accumulate = int(bias_accumulate)
     _lib.call("tmae_wgrad", ctypes.byref(args), code, _stream())
     return out
 
