@@ -216,37 +216,3 @@ def test_config4_vitl_bench_batch_bf16(tmae):
     print(f"config 4 bf16 (batch 128) vs oracle: {per}")
     check("x_hat_relL2_max_bf16_cfg4", max(per), BF16_XHAT_RELL2)
     assert torch.isfinite(out["likelihoods"]["y"]).all() and torch.isfinite(out["likelihoods"]["z"]).all()
-
-
-@pytest.mark.parametrize("training", [False, True])
-def test_pipelined_forward_bitwise(tmae, training):
-    """MCM.pipeline = 2 (two half-batch executors on two streams, the second half's encoder under the first
-    half's slice loop): x_hat and both likelihoods bit for bit the one-pipeline forward's, eager and replayed
-    from a captured HIP graph (bf16, ViT-B 256^2, K=144, batch 16; training mode with injected noise)"""
-    torch.manual_seed(3)
-    m = tmae.MCM(img_size=256, num_keep_patches=144).to(DEV).eval()
-    m.compute_dtype = torch.bfloat16
-    m.distortion = "none"
-    imgs = torch.randn(16, 3, 256, 256, device=DEV)
-    scores = torch.rand(16, 256, device=DEV)
-    noise = (torch.rand(16, 192, 3, 3, device=DEV) - 0.5, torch.rand(16, 384, 12, 12, device=DEV) - 0.5)
-    m.train(training)
-    kw = {"noise": noise} if training else {}
-    with torch.no_grad():
-        m.pipeline = 1
-        ref = m(imgs, scores, **kw)
-        ref = (ref["x_hat"].clone(), ref["likelihoods"]["y"].clone(), ref["likelihoods"]["z"].clone())
-        m.pipeline = 2
-        got = m(imgs, scores, **kw)
-        torch.cuda.synchronize()
-        for a, b in zip((got["x_hat"], got["likelihoods"]["y"], got["likelihoods"]["z"]), ref):
-            assert torch.equal(a, b)
-        if not training:
-            graph, out = _graph_forward(m, imgs, scores)
-            graph.replay()
-            torch.cuda.synchronize()
-            for a, b in zip((out["x_hat"], out["likelihoods"]["y"], out["likelihoods"]["z"]), ref):
-                assert torch.equal(a, b)
-            del graph
-    m.pipeline = 1
-    m.eval()

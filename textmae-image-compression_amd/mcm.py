@@ -112,12 +112,6 @@ class MCM(CompressionModel):
         self.sum_lanes = 8          # torch CPU float-sum vector width the reference ran with
         self.distortion = "ssim+l1"  # forward_loss terms; "none" skips them (encode/decode/rate only)
         self._exec = None
-        # eval forward as two half-batch pipelines on two streams (the second half's encoder runs under the
-        # first half's latency-bound slice loop, its slice loop under the first half's decoder); images are
-        # independent, so the result is the one-pipeline forward's bit for bit.  TMAE_PIPELINE overrides.
-        self.pipeline = int(os.environ.get("TMAE_PIPELINE", "1"))
-        self._pexec = None
-        self._pstream = None
 
     # ---------------------------------------------------------------------------------- init
     def initialize_weights(self):
@@ -147,7 +141,6 @@ class MCM(CompressionModel):
         # the reference override drops `strict` (MCM.py:445-446); keep the compressai buffer resizing
         r = super().load_state_dict(state_dict, strict=strict)
         self._exec = None
-        self._pexec = None
         self._train_exec = None
         return r
 
@@ -205,57 +198,12 @@ class MCM(CompressionModel):
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             return self._forward_train(imgs, total_scores, noise)
         with torch.no_grad():
-            B = imgs.shape[0]
-            if self.pipeline == 2 and B % 2 == 0 and B >= 8:
-                out = self._run_pipelined(imgs, total_scores, noise)
-            else:
-                ex = self._executor(B, imgs.device)
-                out = ex.run(imgs, total_scores, self.training, noise)
+            ex = self._executor(imgs.shape[0], imgs.device)
+            out = ex.run(imgs, total_scores, self.training, noise)
             x_hat = out["x_hat"]
             loss = self.forward_loss(imgs, x_hat) if self.distortion != "none" else (
                 torch.zeros((), device=imgs.device),) * 3
         return {"loss": loss, "likelihoods": {"y": out["y"], "z": out["z"]}, "x_hat": x_hat}
-
-    def _run_pipelined(self, imgs, total_scores, noise):
-        """two half-batch executors; half A on the current stream, half B on a second stream that starts once
-        A's encoder is done (fork / join by events: graph-capturable).  Outputs land in full-batch tensors."""
-        dt = self.compute_dtype
-        if torch.is_autocast_enabled() and dt == torch.float32:
-            dt = torch.bfloat16
-        B, h, dev = imgs.shape[0], imgs.shape[0] // 2, imgs.device
-        pe = self._pexec
-        if pe is None or pe[0].batch != h or pe[0].dtype != dt or pe[0].device != dev:
-            self._exec = None  # one set of workspaces at a time
-            pe = self._pexec = (_Executor(self, h, dt, dev), _Executor(self, h, dt, dev))
-            self._pstream = torch.cuda.Stream(device=dev)
-        for ex in pe:
-            ex.refresh_weights()
-        M, N = self.latent_depth, self.hyperprior_depth
-        g, hz = pe[0].g, pe[0].hz
-        x_hat = torch.empty((B, imgs.shape[1], pe[0].img, pe[0].img), dtype=torch.float32, device=dev)
-        ylik = torch.empty((B, M, g, g), dtype=torch.float32, device=dev)
-        zlik = torch.empty((B, N, hz, hz), dtype=torch.float32, device=dev)
-        if self.training and noise is None:
-            noise = (torch.empty((B, N, hz, hz), device=dev).uniform_(-0.5, 0.5),
-                     torch.empty((B, M, g, g), device=dev).uniform_(-0.5, 0.5))
-        main, s2 = torch.cuda.current_stream(), self._pstream
-        front_done = torch.cuda.Event()
-        halves = [slice(0, h), slice(h, B)]
-        outs = []
-        for k, (ex, sl) in enumerate(zip(pe, halves)):
-            nz = None if noise is None else (noise[0][sl], noise[1][sl])
-            if k == 0:
-                outs.append(ex.run(imgs[sl], total_scores[sl], self.training, nz, out=(x_hat[sl], ylik[sl], zlik[sl]),
-                                   after_front=lambda: front_done.record(main)))
-            else:
-                s2.wait_event(front_done)
-                with torch.cuda.stream(s2):
-                    outs.append(ex.run(imgs[sl], total_scores[sl], self.training, nz,
-                                       out=(x_hat[sl], ylik[sl], zlik[sl])))
-        main.wait_stream(s2)
-        return {"x_hat": x_hat, "y": ylik, "z": zlik,
-                "ids_restore": torch.cat([o["ids_restore"] for o in outs]),
-                "ids_shuffle": torch.cat([o["ids_shuffle"] for o in outs])}
 
     def _forward_train(self, imgs, total_scores, noise):
         """MCM.forward under autograd (utils/engine.py:75): one autograd node whose forward keeps the
@@ -565,9 +513,7 @@ class _Executor:
             raise ValueError(f"Input image size {tuple(imgs.shape[2:])} doesn't match model ({self.img})")
         return imgs
 
-    def run(self, imgs, scores, training, noise, out=None, after_front=None):
-        """the eval / no-grad forward; out = (x_hat, y_lik, z_lik) views to write into (else allocated /
-        cloned); after_front() is called once the encoder / g_a / h_a are enqueued"""
+    def run(self, imgs, scores, training, noise):
         m, B = self.m, self.batch
         M, N, g, hz = m.latent_depth, m.hyperprior_depth, self.g, self.hz
         imgs = self._check_imgs(imgs)
@@ -581,8 +527,6 @@ class _Executor:
             z_noise = y_noise = None
 
         shuf, rest = self._front(imgs, scores)
-        if after_front is not None:
-            after_front()
 
         # ---- entropy bottleneck + z_hat (MCM.py:741-744)
         ops.eb_likelihood(m.entropy_bottleneck, self.Z, B, N, hz * hz, noise=z_noise, lik=self.ZLIK, zhat=self.ZHAT,
@@ -594,11 +538,6 @@ class _Executor:
         # ---- slice loop (MCM.py:751-787)
         self._slices(self._gc_forward(y_noise), chain_ok=True)
 
-        if out is not None:
-            x_hat = self._back(shuf, imgs.shape[1], out=out[0])
-            out[1].copy_(self.YLIK)
-            out[2].copy_(self.ZLIK)
-            return {"x_hat": out[0], "y": out[1], "z": out[2], "ids_restore": rest, "ids_shuffle": shuf}
         x_hat = self._back(shuf, imgs.shape[1])
         return {"x_hat": x_hat, "y": self.YLIK.clone(), "z": self.ZLIK.clone(), "ids_restore": rest,
                 "ids_shuffle": shuf}
@@ -687,8 +626,8 @@ class _Executor:
             x, cin = out, cout
         return shuf, rest
 
-    def _back(self, shuf, in_chans, out=None):
-        """g_s + decoder + unpatchify (MCM.py:636-688, 790-797) from YH; returns x_hat NCHW f32 (into `out`)"""
+    def _back(self, shuf, in_chans):
+        """g_s + decoder + unpatchify (MCM.py:636-688, 790-797) from YH; returns x_hat NCHW f32"""
         m, dt, B = self.m, self.dtype, self.batch
         Dd, K, L, P = m.decoder_embed_dim, m.num_keep_patches, self.L, self.P
         Td = L + 1
@@ -707,8 +646,7 @@ class _Executor:
             run_block(self.dec, w, B, Td, dt, self.dec_s)
         ops.layernorm(self.dec, m.decoder_norm.weight, m.decoder_norm.bias, m.decoder_norm.eps, dt, rows=B * L,
                       row_group=L, group_stride=Td, row_offset=1, out=self.dn)
-        x_hat = torch.empty((B, in_chans, self.img, self.img), dtype=torch.float32, device=self.device) \
-            if out is None else out
+        x_hat = torch.empty((B, in_chans, self.img, self.img), dtype=torch.float32, device=self.device)
         ops.decoder_pred(self.dn, self.w_dp, self.b_dp, x_hat, B, L, P, dt, channel_planar=self.pred_cp)
         return x_hat
 
