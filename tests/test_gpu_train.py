@@ -438,3 +438,37 @@ def test_relayout_multi_dense_and_strided(T, dt):
     for s, d, dims, st in jobs:
         ref = torch.as_strided(s, dims, st).to(dt)
         assert torch.equal(d.reshape(dims), ref)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_weight_cache_refresh_modes(dt):
+    """mcm_train._Weights: the lazy first build and the one-launch refresh (tmae_relayout_multi modes: plain
+    cast, 64 x 64 LDS transposes for W^T and the conv data-gradient layout, per-row [Cin][9] -> [9][Cin] for conv
+    weights) equal torch's layouts exactly, including ragged transpose edges"""
+    from textmae_amd.mcm_train import _Weights
+    from textmae_amd.optim import bump_versions
+
+    g = torch.Generator().manual_seed(7)
+    lin = torch.nn.Parameter(torch.randn(200, 136, generator=g).cuda())
+    conv = torch.nn.Parameter(torch.randn(72, 40, 3, 3, generator=g).cuda())
+    conv2 = torch.nn.Parameter(torch.randn(32, 608, 3, 3, generator=g).cuda())
+    W = _Weights(dt)
+
+    def check_all():
+        torch.cuda.synchronize()
+        assert torch.equal(W.nt(lin), lin.detach().to(dt))
+        assert torch.equal(W.t(lin), lin.detach().t().contiguous().to(dt))
+        for c in (conv, conv2):
+            co, ci = c.shape[:2]
+            assert torch.equal(W.conv(c), c.detach().permute(0, 2, 3, 1).reshape(co, 9 * ci).to(dt))
+            assert torch.equal(W.conv_dg(c), c.detach().permute(1, 2, 3, 0).reshape(ci, 9 * co).to(dt))
+
+    check_all()  # lazy first builds
+    with torch.no_grad():
+        for p in (lin, conv, conv2):
+            p.mul_(-1.5).add_(0.25)
+    bump_versions([lin, conv, conv2])
+    W.refresh()  # one multi-tensor launch
+    torch.cuda.synchronize()
+    # the cached copies are returned as-is now (signatures current): they must hold the new values
+    check_all()

@@ -360,11 +360,21 @@ extern "C" int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0,
   TMAE_LAUNCH_CHECK("tmae_relayout");
 }
 
-// multi-tensor form: table[t] = {src, dst, dst_dtype, d1, d2, d3, s0, s1, s2, s3, total, first_chunk} (int64);
-// 2048-element chunks, a block finds its tensor by binary search over first_chunk.  One launch re-lays out
-// every weight whose version moved (the optimizer step), instead of one launch per weight and layout.
+// multi-tensor form: table[t] = {src, dst, dst_dtype | mode << 8, d1, d2, d3, s0, s1, s2, s3, total, first_chunk}
+// (int64); a block finds its tensor by binary search over first_chunk.  One launch re-lays out every weight whose
+// version moved (the optimizer step), instead of one launch per weight and layout.  Modes (host-chosen):
+//   0  2048-element chunks: plain casts as 16-B vectors, anything else as a strided gather;
+//   1  2-D transpose dst[c][r] = src[r * s3 + c] (R = d3 source rows, C = total / R): 64 x 64 LDS tiles, coalesced
+//      both ways (nn.Linear data-gradient operands W^T; the conv data-gradient layout [Cin][3][3][Cout], which is
+//      the transpose of the weight seen as [Cout][Cin * 9]);
+//   2  per-row [A][B] -> [B][A] (conv weight [Cout][Cin][3][3] -> [Cout][3][3][Cin]: A = Cin = d3, B = 9): one row
+//      per chunk through LDS (A * B <= 8192).
+template <typename OT>
+__device__ __forceinline__ void relayout_store(void* dst, size_t i, float v) { reinterpret_cast<OT*>(dst)[i] = to_out<OT>(v); }
+
 __global__ void __launch_bounds__(256)
 relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
+  __shared__ float sm[8192];
   const long long b = blockIdx.x;
   int lo = 0, hi = nt - 1;
   while (lo < hi) {
@@ -374,25 +384,62 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
   }
   const long long* e = tab + 12 * lo;
   const float* src = (const float*)e[0];
+  void* dstp = (void*)e[1];
   const unsigned d1 = (unsigned)e[3], d2 = (unsigned)e[4], d3 = (unsigned)e[5];
   const long long s0 = e[6], s1 = e[7], s2 = e[8], s3 = e[9];
   const unsigned total = (unsigned)e[10];  // < 2^31 (host check)
-  const unsigned base = (unsigned)(b - e[11]) * 2048u;
-  const bool to_bf16 = e[2] == TMAE_BF16;
+  const int mode = (int)(e[2] >> 8);
+  const bool to_bf16 = (e[2] & 255) == TMAE_BF16;
+  const unsigned chunk = (unsigned)(b - e[11]);
+  const int tid = threadIdx.x;
+  if (mode == 1) {
+    const unsigned R = d3, C = total / d3;
+    const unsigned ntc = (C + 63) / 64;
+    const unsigned r0 = (chunk / ntc) * 64, c0 = (chunk % ntc) * 64;
+    const int tx = tid & 63, ty = tid >> 6;
+#pragma unroll 4
+    for (int k = ty; k < 64; k += 4) {
+      const unsigned r = r0 + k, c = c0 + tx;
+      sm[k * 65 + tx] = (r < R && c < C) ? src[(size_t)r * s3 + c] : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int k = ty; k < 64; k += 4) {
+      const unsigned c = c0 + k, r = r0 + tx;
+      if (c < C && r < R) {
+        if (to_bf16) relayout_store<bf16>(dstp, (size_t)c * R + r, sm[tx * 65 + k]);
+        else relayout_store<float>(dstp, (size_t)c * R + r, sm[tx * 65 + k]);
+      }
+    }
+    return;
+  }
+  if (mode == 2) {
+    const unsigned A = d3, B = d1 * d2, n = A * B, r = chunk;
+    for (unsigned i = tid; i < n; i += 256) sm[i] = src[(size_t)r * s0 + i];
+    __syncthreads();
+    const size_t ob = (size_t)r * n;
+    for (unsigned t = 0; t < B; ++t)
+      for (unsigned a = tid; a < A; a += 256) {
+        if (to_bf16) relayout_store<bf16>(dstp, ob + (size_t)t * A + a, sm[a * B + t]);
+        else relayout_store<float>(dstp, ob + (size_t)t * A + a, sm[a * B + t]);
+      }
+    return;
+  }
+  const unsigned base = chunk * 2048u;
   // a plain cast (contiguous source, 16-B aligned ends): 8 elements per thread, vector loads and stores
   const bool dense = (d3 == 1 || s3 == 1) && (d2 == 1 || s2 == (long long)d3) && (d1 == 1 || s1 == (long long)d2 * d3) &&
                      s0 == (long long)d1 * d2 * d3 &&
                      ((((unsigned long long)src) | ((unsigned long long)e[1])) & 15) == 0;
   if (dense && base + 2048u <= total) {
-    const unsigned i = base + 8u * threadIdx.x;
-    f32x4 lo, hi;
-    load8f(src + i, lo, hi);
-    if (to_bf16) store8((bf16*)e[1] + i, lo, hi);
-    else store8((float*)e[1] + i, lo, hi);
+    const unsigned i = base + 8u * tid;
+    f32x4 lo4, hi4;
+    load8f(src + i, lo4, hi4);
+    if (to_bf16) store8((bf16*)e[1] + i, lo4, hi4);
+    else store8((float*)e[1] + i, lo4, hi4);
     return;
   }
   // general strided gather: 32-bit index arithmetic (64-bit division is a long VALU sequence)
-  for (unsigned k = threadIdx.x; k < 2048u; k += 256u) {
+  for (unsigned k = tid; k < 2048u; k += 256u) {
     const unsigned i = base + k;
     if (i >= total) break;
     unsigned r = i;

@@ -34,8 +34,9 @@ def _convs(seq):
 class _Weights:
     """Kernel-layout copies of the f32 parameters, rebuilt when a parameter's version changes (once per
     optimizer step).  The first build of each (parameter, layout) is lazy; afterwards ``refresh()`` re-lays
-    out every stale copy in ONE multi-tensor launch (tmae_relayout_multi), plain transposes excepted (their
-    LDS-tiled kernel, one launch each)."""
+    out every stale copy in ONE multi-tensor launch (tmae_relayout_multi): plain casts as vectors, 2-D
+    transposes (W^T, the conv data-gradient layout) as 64 x 64 LDS tiles, conv weights [Cout][Cin][3][3] ->
+    [Cout][3][3][Cin] one row per block through LDS."""
 
     def __init__(self, dtype):
         self.dtype = dtype
@@ -73,17 +74,22 @@ class _Weights:
             if job is None:
                 continue
             dims, strides = job
-            if self._is_transpose(dims, strides):
-                T.relayout(p.detach(), dst, dims, strides)
-                continue
             d = list(dims) + [1] * (4 - len(dims))
             st = list(strides) + [0] * (4 - len(strides))
             total = d[0] * d[1] * d[2] * d[3]
             if total >= 1 << 31:
                 raise ValueError(f"weight relayout of {total} elements exceeds the 32-bit index range")
-            rows.append([p.data_ptr(), dst.data_ptr(), ops.dtype_code(dst.dtype), d[1], d[2], d[3], *st, total, chunk])
+            if self._is_transpose(dims, strides):  # dst [C][R] of src [R][C] (C = d0, R = d3, ld = s3)
+                mode, n = 1, -(-d[3] // 64) * -(-d[0] // 64)
+            elif (d[1] * d[2] * d[3] <= 8192 and st[2] == 1 and st[1] == d[2] and st[3] == d[1] * d[2]
+                  and st[0] == d[1] * d[2] * d[3]):  # per-row [A][B] -> [B][A]
+                mode, n = 2, d[0]
+            else:
+                mode, n = 0, (total + 2047) // 2048
+            rows.append([p.data_ptr(), dst.data_ptr(), ops.dtype_code(dst.dtype) | (mode << 8), d[1], d[2], d[3], *st,
+                         total, chunk])
             ptrs.append((p.data_ptr(), dst.data_ptr()))
-            chunk += (total + 2047) // 2048
+            chunk += n
         if not rows:
             return
         key = tuple(ptrs)
@@ -126,7 +132,8 @@ class _Weights:
         """-> [Cin][3][3][Cout] (transposed-conv data gradient)"""
         def b(w):
             co, ci = w.shape[:2]
-            return torch.empty((ci, 9 * co), dtype=self.dtype, device=w.device), ((ci, 3, 3, co), (9, 3, 1, ci * 9))
+            # dst[ci][tap][co] = w[co][ci][tap]: the transpose of w seen as [Cout][Cin * 9]
+            return torch.empty((ci, 9 * co), dtype=self.dtype, device=w.device), ((ci * 9, 1, 1, co), (1, 0, 0, ci * 9))
         return self._get(p, "conv_dg", b)
 
 
