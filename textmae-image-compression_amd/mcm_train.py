@@ -41,6 +41,7 @@ class _Weights:
     def __init__(self, dtype):
         self.dtype = dtype
         self.cache = {}   # (id(p), kind) -> [sig, tensor, p, job]; job = (dims, strides) or None (a view)
+        self.packs = {}   # (param ids, kind) -> packed buffer whose rows are those params' cache entries
         self._tab = None
 
     def _get(self, p, kind, make):
@@ -50,11 +51,37 @@ class _Weights:
         if hit is not None and hit[0] == sig:
             return hit[1]
         w = p.detach()
-        dst, job = make(w)
+        if hit is not None and hit[3] is not None and hit[0] is not None and hit[0][0] == sig[0]:
+            dst, job = hit[1], hit[3]  # same parameter storage, newer values: re-lay out in place (keeps packing)
+        elif hit is not None and hit[0] is None:
+            dst, job = hit[1], hit[3]  # a packed row registered by packed(), first build
+        else:
+            dst, job = make(w)
         if job is not None:
             T.relayout(w, dst, *job)
         self.cache[key] = [sig, dst, p, job]
         return dst
+
+    def packed(self, params, kind):
+        """one buffer holding the `kind` layouts ("conv" or "bias") of `params` back to back, so a batched
+        launch reaches problem j at a constant stride; each row is also that parameter's cache entry"""
+        key = (tuple(id(p) for p in params), kind)
+        buf = self.packs.get(key)
+        if buf is None:
+            p0 = params[0]
+            if kind == "conv":
+                co, ci = p0.shape[:2]
+                buf = torch.empty((len(params), co, 9 * ci), dtype=self.dtype, device=p0.device)
+                job = ((co, 3, 3, ci), (ci * 9, 3, 1, 9))
+            else:
+                buf = torch.empty((len(params), p0.numel()), dtype=torch.float32, device=p0.device)
+                job = ((p0.numel(),), (1,))
+            for j, p in enumerate(params):
+                self.cache[(id(p), kind)] = [None, buf[j], p, job]
+            self.packs[key] = buf
+        for p in params:
+            self._get(p, kind, None)
+        return buf
 
     @staticmethod
     def _is_transpose(dims, strides):
@@ -304,10 +331,12 @@ class TrainExec:
                           table=torch.empty((N, 59), dtype=torch.float32, device=self.device))
 
         # ---- h_s (MCM.py:747-748): mean straight into the first M columns of LMS = [latent_means | y_hat slots]
+        # h_s_scale into the first M columns of LS, rows 2M apart like LMS: the mean and scale stacks of a slice
+        # then read their inputs with one layout and run as one 2-problem launch per layer (_slices_fwd)
         self.LMS = self._z(self.Mp, 2 * M, dtype=dt)
-        self.LS = self._e(self.Mp, M)
+        self.LS = self._e(self.Mp, 2 * M)
         self.hs_mean = self._h_s_fwd(m.h_s_mean, self.LMS, 2 * M)
-        self.hs_scale = self._h_s_fwd(m.h_s_scale, self.LS, M)
+        self.hs_scale = self._h_s_fwd(m.h_s_scale, self.LS, 2 * M)
 
         # ---- slice loop (MCM.py:751-787)
         self._slices_fwd()
@@ -402,19 +431,132 @@ class TrainExec:
         self.YH = self._e(Mp, M)
         self.YLIK = torch.empty((B, M, g, g), dtype=torch.float32, device=self.device)
         self.sl = []
-        for i in range(S):
+        # slices 0..ms-1 in order (each conditions on the ones before); slices ms..S-1 all condition on y_hat
+        # slots 0..ms-1 only (max_support_slices, MCM.py:73, 756-758), so they run batched (_batched_fwd)
+        nser = ms if S - ms > 1 else S
+        for i in range(nser):
             k = min(i, ms)
             cin_m = M + sw * k
             rec = {}
-            rec["mean"] = self._stack_fwd(_convs(m.cc_transform_mean[i]), (self.LMS, cin_m, 2 * M, None, 0, 0))
-            rec["scale"] = self._stack_fwd(_convs(m.cc_transform_scale[i]),
-                                           (self.LS, M, M, lms + M * esz if k else None, sw * k, 2 * M))
+            rec["mean"], rec["scale"] = self._ms_fwd(i, k)
             mu, sig = rec["mean"][-1], rec["scale"][-1]
             ops.gc_slices(self.Y32, M, i * sw, mu, sig, 0, sw, self.y_noise, self.YLIK, M, self.YPT, dt, M,
                           self.YPRE, M, B, HW, 1, sw)
             ypt = self.YPT.data_ptr() + i * sw * esz
             rec["lrp"] = self._stack_fwd(_convs(m.lrp_transform[i]), (self.LMS, cin_m, 2 * M, ypt, sw, M), lrp=i)
             self.sl.append(rec)
+        if nser < S:
+            self.sl += self._batched_fwd(nser, S - nser)
+
+    def _batched_fwd(self, i0, nbs):
+        """slices i0..i0+nbs-1 together: their mean / scale stacks as one 2 x nbs-problem launch per layer, the
+        Gaussian likelihoods of all nbs slices in one launch, their lrp stacks as one nbs-problem launch per layer
+        (weights / biases of each group packed so problem j sits at a constant stride).  Same arithmetic per
+        slice as the serial form; returns one saved-activation record per slice"""
+        m, dt, W, B, g, Mp = self.m, self.dtype, self.w, self.batch, self.g, self.Mp
+        M, sw, HW = m.latent_depth, self.sw, g * g
+        k = self.ms  # support slots of every batched slice
+        esz = self.LMS.element_size()
+        sl = range(i0, i0 + nbs)
+        cm = [_convs(m.cc_transform_mean[i]) for i in sl]
+        cs = [_convs(m.cc_transform_scale[i]) for i in sl]
+        cl = [_convs(m.lrp_transform[i]) for i in sl]
+        recs = [{"mean": [], "scale": [], "lrp": []} for _ in sl]
+        x1, c1, ld1 = self.LMS, M, 2 * M
+        x1s = ((self.LS.data_ptr() - self.LMS.data_ptr()) // esz, 0)
+        x2, c2 = self.LMS.data_ptr() + M * esz, sw * k
+        nl = len(cm[0])
+        for l in range(nl):
+            cout = cm[0][l].out_channels
+            wm_, ws_ = W.packed([c[l].weight for c in cm], "conv"), W.packed([c[l].weight for c in cs], "conv")
+            bm_, bs_ = W.packed([c[l].bias for c in cm], "bias"), W.packed([c[l].bias for c in cs], "bias")
+            st = {"x1": x1s, "w": ((ws_.data_ptr() - wm_.data_ptr()) // wm_.element_size(), wm_[0].numel()),
+                  "b": ((bs_.data_ptr() - bm_.data_ptr()) // 4, cout), "y": (nbs * Mp * cout, Mp * cout)}
+            if l < nl - 1:
+                act, pre = self._e(2, nbs, Mp, cout), self._e(2, nbs, Mp, cout)
+                st["pre"] = st["y"]
+                ops.conv3x3(x1, c1, ld1, B, g, g, wm_, bm_, act, cout, cout, dt, act=ACT_GELU, x2=x2, c2=c2, ld2=2 * M,
+                            pre=pre, ldp=cout, nb=(2, nbs), strides=st)
+                for j in range(nbs):
+                    recs[j]["mean"].append((act[0, j], pre[0, j]))
+                    recs[j]["scale"].append((act[1, j], pre[1, j]))
+                x1, c1, ld1, x1s, x2, c2 = act, cout, cout, (nbs * Mp * cout, Mp * cout), None, 0
+            else:
+                out = torch.empty((2, nbs, Mp, cout), dtype=torch.float32, device=self.device)
+                ops.conv3x3(x1, c1, ld1, B, g, g, wm_, bm_, out, cout, cout, dt, y_f32=True, x2=x2, c2=c2, ld2=2 * M,
+                            nb=(2, nbs), strides=st)
+                for j in range(nbs):
+                    recs[j]["mean"].append(out[0, j])
+                    recs[j]["scale"].append(out[1, j])
+                mus = out
+        # GaussianConditional + quantize_ste of all nbs slices (mu / sigma blocks Mp * sw apart)
+        ops.gc_slices(self.Y32, M, i0 * sw, mus[0], mus[1], Mp * sw, sw, self.y_noise, self.YLIK, M, self.YPT, dt, M,
+                      self.YPRE, M, B, HW, nbs, sw)
+        # lrp stacks: input [latent_means | slots 0..k-1] (shared) + this slice's y_hat_pre (x2, sw apart)
+        x1, c1, ld1, x1s = self.LMS, M + sw * k, 2 * M, (0, 0)
+        x2, c2, ld2, x2s = self.YPT.data_ptr() + i0 * sw * esz, sw, M, (0, sw)
+        for l in range(nl):
+            cout = cl[0][l].out_channels
+            wl_, bl_ = W.packed([c[l].weight for c in cl], "conv"), W.packed([c[l].bias for c in cl], "bias")
+            st = {"x1": x1s, "x2": x2s, "w": (0, wl_[0].numel()), "b": (0, cout)}
+            if l < nl - 1:
+                act, pre = self._e(nbs, Mp, cout), self._e(nbs, Mp, cout)
+                st["y"] = st["pre"] = (0, Mp * cout)
+                ops.conv3x3(x1, c1, ld1, B, g, g, wl_, bl_, act, cout, cout, dt, act=ACT_GELU, x2=x2, c2=c2, ld2=ld2,
+                            pre=pre, ldp=cout, nb=(1, nbs), strides=st)
+                for j in range(nbs):
+                    recs[j]["lrp"].append((act[j], pre[j]))
+                x1, c1, ld1, x1s, x2, c2, ld2, x2s = act, cout, cout, (0, Mp * cout), None, 0, 0, (0, 0)
+            else:
+                # y_hat = y_hat_pre + 0.5 tanh(t) into YH (slice j at channels (i0 + j) sw), t kept in f32
+                t = torch.empty((nbs, Mp, cout), dtype=torch.float32, device=self.device)
+                st.update({"y": (0, sw), "src": (0, sw), "pre": (0, Mp * cout)})
+                ops.conv3x3(x1, c1, ld1, B, g, g, wl_, bl_, self.YH.data_ptr() + i0 * sw * esz, M, cout, dt,
+                            y_f32=(dt == torch.float32), lrp_src=self.YPRE.data_ptr() + i0 * sw * 4, ld_src=M,
+                            pre=t, ldp=cout, nb=(1, nbs), strides=st)
+                for j in range(nbs):
+                    recs[j]["lrp"].append(t[j])
+        return recs
+
+    def _ms_fwd(self, i, k):
+        """cc_transform_mean[i] and cc_transform_scale[i] (MCM.py:761-768) as one 2-problem conv launch per layer:
+        problem 0 reads [latent_means | y_hat slots 0..k-1] from LMS, problem 1 [latent_scales | the same slots]
+        (LS and LMS share the 2M row pitch; per-problem weight / bias / input offsets are pointer differences).
+        Returns the saved activations of each stack as _stack_fwd does."""
+        m, dt, W, B, g, Mp = self.m, self.dtype, self.w, self.batch, self.g, self.Mp
+        M, sw = m.latent_depth, self.sw
+        cm, cs = _convs(m.cc_transform_mean[i]), _convs(m.cc_transform_scale[i])
+        esz = self.LMS.element_size()
+
+        def diff(a, b, e):
+            d = b.data_ptr() - a.data_ptr()
+            assert d % e == 0
+            return d // e
+
+        sv_m, sv_s = [], []
+        x1, ld1, xs = self.LMS, 2 * M, diff(self.LMS, self.LS, esz)
+        c1, c2 = M, sw * k
+        x2 = self.LMS.data_ptr() + M * esz if k else None
+        for l, (a, b) in enumerate(zip(cm, cs)):
+            cout = a.out_channels
+            wa, wb = W.conv(a.weight), W.conv(b.weight)
+            st = {"x1": (xs, 0), "w": (diff(wa, wb, wa.element_size()), 0),
+                  "b": (diff(a.bias, b.bias, 4), 0), "y": (Mp * cout, 0)}
+            if l < 4:
+                act, pre = self._e(2, Mp, cout), self._e(2, Mp, cout)
+                st["pre"] = (Mp * cout, 0)
+                ops.conv3x3(x1, c1, ld1, B, g, g, wa, a.bias.detach(), act, cout, cout, dt, act=ACT_GELU, x2=x2, c2=c2,
+                            ld2=2 * M, pre=pre, ldp=cout, nb=(2, 1), strides=st)
+                sv_m.append((act[0], pre[0]))
+                sv_s.append((act[1], pre[1]))
+                x1, c1, ld1, xs, x2, c2 = act, cout, cout, Mp * cout, None, 0
+            else:
+                out = torch.empty((2, Mp, cout), dtype=torch.float32, device=self.device)
+                ops.conv3x3(x1, c1, ld1, B, g, g, wa, a.bias.detach(), out, cout, cout, dt, y_f32=True, x2=x2, c2=c2,
+                            ld2=2 * M, nb=(2, 1), strides=st)
+                sv_m.append(out[0])
+                sv_s.append(out[1])
+        return sv_m, sv_s
 
     def _stack_fwd(self, convs, first, lrp=None):
         """5-conv stack (cc_transform / lrp_transform): returns [(act_l, pre_l) for l < 4] + [out]"""
@@ -697,7 +839,7 @@ class TrainExec:
             self._stack_bwd(_convs(m.cc_transform_mean[i]), rec["mean"], dMU, (self.LMS, cin_m, 2 * M, None, 0, 0),
                             [(dLM, M, M), (dSUP, M, sw * k)])
             self._stack_bwd(_convs(m.cc_transform_scale[i]), rec["scale"], dSG,
-                            (self.LS, M, M, lms + M * esz if k else None, sw * k, 2 * M),
+                            (self.LS, M, 2 * M, lms + M * esz if k else None, sw * k, 2 * M),
                             [(dLS, M, M), (dSUP, M, sw * k)])
             self._ready(_convs(m.cc_transform_scale[i])[0].bias)
         return DY, dLM, dLS
