@@ -435,23 +435,62 @@ extern "C" int tmae_mha_fwd_lse(const void* qkv, void* out, float* lse, int B, i
 //            (cdna_hip_programming.md §3, "accumulator tile as the next operand");
 //   phase 2 (wave = 32 queries, loop over key tiles): S^T, dP^T with the query on the lane -> dQ += scale dS K.
 // Both phases own their outputs: no atomics, bitwise reproducible.  delta = rowsum(dO * O).
+template <int DH> struct AttnBwd;
+// LDS row stride (elements) of the staged operands: both row-wise ds_read_b128 fragment reads and
+// ds_read_b64_tr_b16 transposed reads come from the same rows; 48 / 16 dwords keep the transposed reads
+// conflict-free (as the forward's V^T)
+template <> struct AttnBwd<64> { static constexpr int LDR = 96; };
+template <> struct AttnBwd<32> { static constexpr int LDR = 32; };
+
+// B (or A) operand of a 32x32x16 MFMA whose k runs over 16 ROWS of a row-major LDS array (rows k0.., the
+// 32 columns c0..c0+31 on the lanes): two transposed 4-row reads, the element order of the accumulator
+// layout (k = (j & 3) + 8 (j >> 2) + 4 hh), as the forward's V^T operand
+template <int LD>
+__device__ __forceinline__ bf16x8 attn_tr_frag(const bf16* arr, int k0, int c0, int lane) {
+  const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+  const int trow = 4 * (g >> 1) + qq, tcol = 16 * (g & 1) + 4 * pp;
+  const bf16* p = arr + (size_t)(k0 + trow) * LD + c0 + tcol;
+  const attn_s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((attn_lds_s4*)p);
+  const attn_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((attn_lds_s4*)(p + 8 * LD));
+  typedef __attribute__((ext_vector_type(8))) short s8;
+  s8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return *reinterpret_cast<bf16x8*>(&v);
+}
+
+// rows [0, Tpad) of two head slices (row-major, 16-B chunks, zero past Tn) -> A0 / A1 (stride LDR)
+template <int DH, int LDR>
+__device__ __forceinline__ void attn_stage2(bf16* A0, const bf16* g0, int ld0, bf16* A1, const bf16* g1, int ld1,
+                                            int Tn, int Tpad, int tid, int nthr) {
+  constexpr int CPR = DH / 8;
+  for (int i = tid; i < Tpad * CPR; i += nthr) {
+    const int r = i / CPR, c = i - r * CPR;
+    uint4 x = uint4{0, 0, 0, 0}, y = x;
+    if (r < Tn) {
+      x = *reinterpret_cast<const uint4*>(g0 + (size_t)r * ld0 + c * 8);
+      y = *reinterpret_cast<const uint4*>(g1 + (size_t)r * ld1 + c * 8);
+    }
+    *reinterpret_cast<uint4*>(A0 + (size_t)r * LDR + c * 8) = x;
+    *reinterpret_cast<uint4*>(A1 + (size_t)r * LDR + c * 8) = y;
+  }
+}
+
+// Two phases over ONE pair of staged arrays (48 / 37 KB instead of the seven arrays of both phases at once,
+// so 2-3 workgroups share a CU): phase 1 stages Q and dO (all queries) and reads this wave's 32 keys of K / V
+// from global; phase 2 re-stages K and V (all keys) and reads this wave's 32 queries of Q / dO from global.
+// The transposed operands (dO^T, Q^T, K^T) are ds_read_b64_tr_b16 reads of the same row-major arrays.
 template <int DH>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(DH == 64 ? 512 : 1024)  // dh 64: <= 256 keys, 256 VGPRs (no spills)
 mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
                     const float* __restrict__ lse, bf16* __restrict__ dqkv, int Tn, int H, int Tpad, float scale) {
-  constexpr int LDR = DH + 8;
+  constexpr int LDR = AttnBwd<DH>::LDR;
   constexpr int NDT = DH / 32;
   constexpr int CPR = DH / 8;
-  const int LDT = Tpad + 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  bf16* Qs = reinterpret_cast<bf16*>(smem);
-  bf16* Ks = Qs + (size_t)Tpad * LDR;
-  bf16* Vs = Ks + (size_t)Tpad * LDR;
-  bf16* dOs = Vs + (size_t)Tpad * LDR;
-  bf16* Qt = dOs + (size_t)Tpad * LDR;
-  bf16* Kt = Qt + (size_t)DH * LDT;
-  bf16* dOt = Kt + (size_t)DH * LDT;
-  float* lse_s = reinterpret_cast<float*>(dOt + (size_t)DH * LDT);
+  bf16* A0 = reinterpret_cast<bf16*>(smem);
+  bf16* A1 = A0 + (size_t)Tpad * LDR;
+  float* lse_s = reinterpret_cast<float*>(A1 + (size_t)Tpad * LDR);
   float* dl_s = lse_s + Tpad;
 
   const int bh = xcd_remap(blockIdx.x, gridDim.x), b = bh / H, h = bh - b * H;
@@ -461,36 +500,20 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
   const bf16* gbase = dout + (size_t)b * Tn * D + h * DH;
   const int tid = threadIdx.x, nthr = blockDim.x;
 
-  for (int i = tid; i < Tpad * CPR; i += nthr) {
-    const int r = i / CPR, c = i - r * CPR;
-    uint4 qv = uint4{0, 0, 0, 0}, kv = qv, vv = qv, gv = qv;
-    if (r < Tn) {
-      qv = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + c * 8);
-      kv = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + D + c * 8);
-      vv = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + 2 * D + c * 8);
-      gv = *reinterpret_cast<const uint4*>(gbase + (size_t)r * D + c * 8);
-    }
-    *reinterpret_cast<uint4*>(Qs + (size_t)r * LDR + c * 8) = qv;
-    *reinterpret_cast<uint4*>(Ks + (size_t)r * LDR + c * 8) = kv;
-    *reinterpret_cast<uint4*>(Vs + (size_t)r * LDR + c * 8) = vv;
-    *reinterpret_cast<uint4*>(dOs + (size_t)r * LDR + c * 8) = gv;
-    const bf16* qe = reinterpret_cast<const bf16*>(&qv);
-    const bf16* ke = reinterpret_cast<const bf16*>(&kv);
-    const bf16* ge = reinterpret_cast<const bf16*>(&gv);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      Qt[(size_t)(c * 8 + e) * LDT + r] = qe[e];
-      Kt[(size_t)(c * 8 + e) * LDT + r] = ke[e];
-      dOt[(size_t)(c * 8 + e) * LDT + r] = ge[e];
-    }
-  }
+  attn_stage2<DH, LDR>(A0, base, ld, A1, gbase, D, Tn, Tpad, tid, nthr);  // Q, dO
+  // delta = rowsum(dO * O) (16-B loads, CPR chunks per row), lse
   for (int r = tid; r < Tpad; r += nthr) {
     float d = 0.0f, l = 0.0f;
     if (r < Tn) {
       const bf16* orow = obase + (size_t)r * D;
       const bf16* grow = gbase + (size_t)r * D;
-#pragma unroll 8
-      for (int k = 0; k < DH; ++k) d += (float)orow[k] * (float)grow[k];
+#pragma unroll
+      for (int c = 0; c < CPR; ++c) {
+        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(orow + 8 * c);
+        const bf16x8 gv = *reinterpret_cast<const bf16x8*>(grow + 8 * c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += (float)ov[e] * (float)gv[e];
+      }
       l = lse[(size_t)bh * Tn + r];
     }
     dl_s[r] = d;
@@ -501,16 +524,17 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
   const int lane = tid & 63, wave = tid >> 6, nw = Tpad / 32;
   const int col = lane & 31, hh = lane >> 5;
   const float c2 = scale * 1.4426950408889634f;
-  if (wave >= nw) return;
+  const bool active = wave < nw;
 
-  // ---------------- phase 1: this wave's 32 keys
-  {
+  // ---------------- phase 1: this wave's 32 keys (K / V rows from global), all queries from LDS
+  if (active) {
     const int kb = 32 * wave;
+    const int kr = min(kb + col, Tn - 1);
     bf16x8 kf[DH / 16], vf[DH / 16];
 #pragma unroll
     for (int s = 0; s < DH / 16; ++s) {
-      kf[s] = *reinterpret_cast<const bf16x8*>(Ks + (size_t)(kb + col) * LDR + 16 * s + 8 * hh);
-      vf[s] = *reinterpret_cast<const bf16x8*>(Vs + (size_t)(kb + col) * LDR + 16 * s + 8 * hh);
+      kf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)kr * ld + D + 16 * s + 8 * hh);
+      vf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)kr * ld + 2 * D + 16 * s + 8 * hh);
     }
     f32x16 dV[NDT], dK[NDT];
 #pragma unroll
@@ -524,9 +548,9 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
       for (int r = 0; r < 16; ++r) S[r] = G[r] = 0.0f;
 #pragma unroll
       for (int s = 0; s < DH / 16; ++s) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Qs + (size_t)(qt * 32 + col) * LDR + 16 * s + 8 * hh);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(A0 + (size_t)(qt * 32 + col) * LDR + 16 * s + 8 * hh);
         S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, kf[s], S, 0, 0, 0);
-        const bf16x8 g = *reinterpret_cast<const bf16x8*>(dOs + (size_t)(qt * 32 + col) * LDR + 16 * s + 8 * hh);
+        const bf16x8 g = *reinterpret_cast<const bf16x8*>(A1 + (size_t)(qt * 32 + col) * LDR + 16 * s + 8 * hh);
         G = __builtin_amdgcn_mfma_f32_32x32x16_bf16(g, vf[s], G, 0, 0, 0);
       }
 #pragma unroll
@@ -541,18 +565,11 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
         bf16x8 pa, da;
 #pragma unroll
         for (int j = 0; j < 8; ++j) { pa[j] = (bf16)S[8 * s + j]; da[j] = (bf16)G[8 * s + j]; }
-        const int k0 = qt * 32 + 16 * s + 4 * hh;
+        const int k0 = qt * 32 + 16 * s;
 #pragma unroll
         for (int t = 0; t < NDT; ++t) {
-          const bf16* grow = dOt + (size_t)(32 * t + col) * LDT + k0;
-          const bf16* qrow = Qt + (size_t)(32 * t + col) * LDT + k0;
-          const bf16x4 g0 = *reinterpret_cast<const bf16x4*>(grow), g1 = *reinterpret_cast<const bf16x4*>(grow + 8);
-          const bf16x4 q0 = *reinterpret_cast<const bf16x4*>(qrow), q1 = *reinterpret_cast<const bf16x4*>(qrow + 8);
-          bf16x8 gb, qb8;
-          gb[0] = g0[0]; gb[1] = g0[1]; gb[2] = g0[2]; gb[3] = g0[3]; gb[4] = g1[0]; gb[5] = g1[1]; gb[6] = g1[2]; gb[7] = g1[3];
-          qb8[0] = q0[0]; qb8[1] = q0[1]; qb8[2] = q0[2]; qb8[3] = q0[3]; qb8[4] = q1[0]; qb8[5] = q1[1]; qb8[6] = q1[2]; qb8[7] = q1[3];
-          dV[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, gb, dV[t], 0, 0, 0);
-          dK[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, qb8, dK[t], 0, 0, 0);
+          dV[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, attn_tr_frag<LDR>(A1, k0, 32 * t, lane), dV[t], 0, 0, 0);
+          dK[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, attn_tr_frag<LDR>(A0, k0, 32 * t, lane), dK[t], 0, 0, 0);
         }
       }
     }
@@ -568,15 +585,19 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
         }
       }
   }
+  __syncthreads();  // every wave is done with Q / dO in LDS
+  attn_stage2<DH, LDR>(A0, base + D, ld, A1, base + 2 * D, ld, Tn, Tpad, tid, nthr);  // K, V
+  __syncthreads();
 
-  // ---------------- phase 2: this wave's 32 queries
-  {
+  // ---------------- phase 2: this wave's 32 queries (Q / dO rows from global), all keys from LDS
+  if (active) {
     const int qb = 32 * wave;
+    const int qr = min(qb + col, Tn - 1);
     bf16x8 qf[DH / 16], gf[DH / 16];
 #pragma unroll
     for (int s = 0; s < DH / 16; ++s) {
-      qf[s] = *reinterpret_cast<const bf16x8*>(Qs + (size_t)(qb + col) * LDR + 16 * s + 8 * hh);
-      gf[s] = *reinterpret_cast<const bf16x8*>(dOs + (size_t)(qb + col) * LDR + 16 * s + 8 * hh);
+      qf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)qr * ld + 16 * s + 8 * hh);
+      gf[s] = *reinterpret_cast<const bf16x8*>(gbase + (size_t)qr * D + 16 * s + 8 * hh);
     }
     const bool qok = qb + col < Tn;
     const float lq = lse_s[qb + col], dq = dl_s[qb + col];
@@ -591,9 +612,9 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
       for (int r = 0; r < 16; ++r) S[r] = G[r] = 0.0f;
 #pragma unroll
       for (int s = 0; s < DH / 16; ++s) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Ks + (size_t)(kt * 32 + col) * LDR + 16 * s + 8 * hh);
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(A0 + (size_t)(kt * 32 + col) * LDR + 16 * s + 8 * hh);
         S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], S, 0, 0, 0);
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(Vs + (size_t)(kt * 32 + col) * LDR + 16 * s + 8 * hh);
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(A1 + (size_t)(kt * 32 + col) * LDR + 16 * s + 8 * hh);
         G = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v, gf[s], G, 0, 0, 0);
       }
 #pragma unroll
@@ -607,16 +628,10 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
         bf16x8 da;
 #pragma unroll
         for (int j = 0; j < 8; ++j) da[j] = (bf16)G[8 * s + j];
-        const int k0 = kt * 32 + 16 * s + 4 * hh;
+        const int k0 = kt * 32 + 16 * s;
 #pragma unroll
-        for (int t = 0; t < NDT; ++t) {
-          const bf16* krow = Kt + (size_t)(32 * t + col) * LDT + k0;
-          const bf16x4 k0v = *reinterpret_cast<const bf16x4*>(krow), k1v = *reinterpret_cast<const bf16x4*>(krow + 8);
-          bf16x8 kb8;
-          kb8[0] = k0v[0]; kb8[1] = k0v[1]; kb8[2] = k0v[2]; kb8[3] = k0v[3];
-          kb8[4] = k1v[0]; kb8[5] = k1v[1]; kb8[6] = k1v[2]; kb8[7] = k1v[3];
-          dQ[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, kb8, dQ[t], 0, 0, 0);
-        }
+        for (int t = 0; t < NDT; ++t)
+          dQ[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, attn_tr_frag<LDR>(A0, k0, 32 * t, lane), dQ[t], 0, 0, 0);
       }
     }
 #pragma unroll
@@ -759,7 +774,8 @@ static int mha_bwd_launch(const void* qkv, const void* o, const void* dout, cons
   TMAE_REQUIRE(nthr <= 1024, "tmae_mha_bwd: sequence length %d too long", Tn);
   if (B * H == 0 || Tn == 0) return TMAE_OK;
   if (dtype == TMAE_BF16) {
-    const size_t lds = ((size_t)4 * Tpad * (DH + 8) + (size_t)3 * DH * (Tpad + 4)) * 2 + (size_t)2 * Tpad * 4;
+    TMAE_REQUIRE(DH != 64 || nthr <= 512, "tmae_mha_bwd: sequence length %d too long for head dim 64", Tn);
+    const size_t lds = (size_t)2 * Tpad * AttnBwd<DH>::LDR * 2 + (size_t)2 * Tpad * 4;
     TMAE_REQUIRE(lds <= 160 * 1024, "tmae_mha_bwd: sequence length %d needs %zu B of LDS", Tn, lds);
     hipLaunchKernelGGL((mha_bwd_bf16_kernel<DH>), dim3(B * H), dim3(nthr), lds, st, (const bf16*)qkv, (const bf16*)o,
                        (const bf16*)dout, lse, (bf16*)dqkv, Tn, H, Tpad, scale);

@@ -567,16 +567,20 @@ static int colsum_into(const void* x, int x_dtype, int ld, int rows, int C, int 
 // ================================================================== LayerNorm backward
 // x rows remapped like the forward (source row sr = (r / G) * Gs + off + r % G); dy dense [rows][D] f32.
 // dx lands at row sr of dx32 (f32; + dres[sr] when given) and of dxop (operand dtype copy, optional).
-// Each wave walks a contiguous run of rows and keeps its dgamma / dbeta partial in registers -> part.
-// RS: also the column sums of dres (the bias gradient of the Linear whose output the residual adds:
-// fc2 before norm2's input gradient, proj before norm1's) -> a third partial block; part is [wave][3D].
+// Waves walk rows r = wave, wave + nwaves, ... with the NEXT row's x / dy / dres loads issued before this row's
+// reductions (one row's latency hidden under the previous row's math; 8 waves per CU); dgamma / dbeta (and RS)
+// partials stay in registers per wave, are summed over the workgroup's 4 waves in LDS and written once per
+// workgroup -> part [workgroup][np * D] (np = 2, or 3 with RS: also the column sums of dres, the bias gradient
+// of the Linear whose output the residual adds: fc2 before norm2's input gradient, proj before norm1's).
 template <typename OT, int VPL, bool RS>
 __global__ void __launch_bounds__(256)
 layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ dy,
                      const float* __restrict__ dres, float* __restrict__ dx32, OT* __restrict__ dxop, int rows, int D,
-                     int G, int Gs, int off, float eps, int rows_per_wave, float* __restrict__ part) {
-  const int lane = threadIdx.x & 63;
-  const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+                     int G, int Gs, int off, float eps, float* __restrict__ part) {
+  constexpr int NP = RS ? 3 : 2;
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][NP * D]
+  const int lane = threadIdx.x & 63, wl = threadIdx.x >> 6;
+  const int nwaves = gridDim.x * 4;
   const int nch = D >> 2;
   f32x4 dg[VPL], db[VPL], gm[VPL], dr[VPL];
 #pragma unroll
@@ -585,20 +589,27 @@ layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamm
     const int c = lane + 64 * i;
     gm[i] = c < nch ? load4f(gamma + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  const int r0 = wave * rows_per_wave, r1 = min(rows, r0 + rows_per_wave);
-  for (int r = r0; r < r1; ++r) {
+  f32x4 v[VPL], g[VPL], rv[VPL];
+  auto load_row = [&](int r, f32x4 (&vv)[VPL], f32x4 (&gg)[VPL], f32x4 (&rr)[VPL]) {
     const int sr = (r / G) * Gs + off + (r % G);
-    const float* xr = x + (size_t)sr * D;
-    const float* gr = dy + (size_t)r * D;
-    f32x4 v[VPL], g[VPL];
-    float s = 0.0f;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) {
       const int c = lane + 64 * i;
-      v[i] = c < nch ? load4f(xr + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
-      g[i] = c < nch ? load4f(gr + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
-      s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+      const bool ok = c < nch && r < rows;
+      vv[i] = ok ? load4f(x + (size_t)sr * D + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      gg[i] = ok ? load4f(dy + (size_t)r * D + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      rr[i] = (ok && dres) ? load4f(dres + (size_t)sr * D + 4 * c) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+  };
+  int r = blockIdx.x * 4 + wl;
+  if (r < rows) load_row(r, v, g, rv);
+  for (; r < rows; r += nwaves) {
+    const int sr = (r / G) * Gs + off + (r % G);
+    f32x4 vn[VPL], gn[VPL], rn[VPL];
+    if (r + nwaves < rows) load_row(r + nwaves, vn, gn, rn);  // next row in flight under this one
+    float s = 0.0f;
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
     const float mean = s / (float)D;
@@ -649,25 +660,35 @@ layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamm
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = rstd * (g[i][j] * gm[i][j] - sa - v[i][j] * sb);
         if (dres) {
-          const f32x4 rv = load4f(dres + (size_t)sr * D + 4 * c);
-          o += rv;
-          if (RS) dr[i] += rv;
+          o += rv[i];
+          if (RS) dr[i] += rv[i];
         }
         store4(dx32 + (size_t)sr * D + 4 * c, o);
         if (dxop) store4(dxop + (size_t)sr * D + 4 * c, o);
       }
     }
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      v[i] = vn[i];
+      g[i] = gn[i];
+      rv[i] = rn[i];
+    }
   }
-  float* pw = part + (size_t)wave * (RS ? 3 : 2) * D;
+  // the workgroup's four wave partials -> one row of part (fixed order: deterministic)
+  float* rw = red + (size_t)wl * NP * D;
 #pragma unroll
   for (int i = 0; i < VPL; ++i) {
     const int c = lane + 64 * i;
     if (c < nch) {
-      store4(pw + 4 * c, dg[i]);
-      store4(pw + D + 4 * c, db[i]);
-      if (RS) store4(pw + 2 * D + 4 * c, dr[i]);
+      *reinterpret_cast<f32x4*>(rw + 4 * c) = dg[i];
+      *reinterpret_cast<f32x4*>(rw + D + 4 * c) = db[i];
+      if (RS) *reinterpret_cast<f32x4*>(rw + 2 * D + 4 * c) = dr[i];
     }
   }
+  __syncthreads();
+  float* pw = part + (size_t)blockIdx.x * NP * D;
+  for (int e = threadIdx.x; e < NP * D; e += 256)
+    pw[e] = ((red[e] + red[NP * D + e]) + red[2 * NP * D + e]) + red[3 * NP * D + e];
 }
 
 static int tmae_ln_fold(const float* part, int waves, int D, float* dg, float* db, float* drs, int accumulate,
@@ -685,21 +706,22 @@ extern "C" int tmae_layernorm_bwd(const float* x, const float* gamma, const floa
   TMAE_REQUIRE(x && gamma && dy && dx32 && work && dgamma && dbeta, "tmae_layernorm_bwd: null argument");
   TMAE_REQUIRE(!dres_colsum || dres, "tmae_layernorm_bwd: dres_colsum needs dres");
   hipStream_t st = (hipStream_t)stream;
-  const int np = dres_colsum ? 3 : 2;  // partial blocks per wave
-  int waves = std::min(1024, std::max(4, rows / 8));
-  while ((long long)(waves + 4) * np * D > work_elems && waves > 4) waves /= 2;
-  const int rpw = ceil_div(std::max(rows, 1), waves);
-  waves = ceil_div(ceil_div(std::max(rows, 1), rpw), 4) * 4;
-  TMAE_REQUIRE((long long)waves * np * D <= work_elems, "tmae_layernorm_bwd: workspace too small");
+  const int np = dres_colsum ? 3 : 2;  // partial blocks per workgroup
+  // 2 workgroups (8 waves) per CU, each wave ~rows / 2048 rows; fewer when the rows are few
+  int wgs = std::max(1, std::min(512, ceil_div(std::max(rows, 1), 4 * 2)));
+  while ((long long)wgs * np * D > work_elems && wgs > 1) wgs /= 2;
+  TMAE_REQUIRE((long long)wgs * np * D <= work_elems, "tmae_layernorm_bwd: workspace too small");
+  const int waves = wgs;  // partial rows for the fold
   const int vpl = ceil_div(D / 4, 64);
-  const dim3 grid(waves / 4);
+  const dim3 grid(wgs);
+  const size_t lds = (size_t)4 * np * D * sizeof(float);
 #define TMAE_LNB(OT, V)                                                                                               \
   if (dres_colsum)                                                                                                    \
-    hipLaunchKernelGGL((layernorm_bwd_kernel<OT, V, true>), grid, dim3(256), 0, st, x, gamma, dy, dres, dx32,           \
-                       (OT*)dxop, rows, D, row_group, group_stride, row_offset, eps, rpw, work);                      \
+    hipLaunchKernelGGL((layernorm_bwd_kernel<OT, V, true>), grid, dim3(256), lds, st, x, gamma, dy, dres, dx32,         \
+                       (OT*)dxop, rows, D, row_group, group_stride, row_offset, eps, work);                           \
   else                                                                                                                \
-    hipLaunchKernelGGL((layernorm_bwd_kernel<OT, V, false>), grid, dim3(256), 0, st, x, gamma, dy, dres, dx32,          \
-                       (OT*)dxop, rows, D, row_group, group_stride, row_offset, eps, rpw, work)
+    hipLaunchKernelGGL((layernorm_bwd_kernel<OT, V, false>), grid, dim3(256), lds, st, x, gamma, dy, dres, dx32,        \
+                       (OT*)dxop, rows, D, row_group, group_stride, row_offset, eps, work)
 #define TMAE_LNB_V(OT)          \
   if (vpl <= 1) TMAE_LNB(OT, 1);  \
   else if (vpl <= 2) TMAE_LNB(OT, 2); \
