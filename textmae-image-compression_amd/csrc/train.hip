@@ -93,31 +93,49 @@ static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
 // dst = base + m*sm + (n % cp)*sc + (n / cp)*st   (dense [M][N]: sm=N, sc=1, cp=N; conv [co][ci][3][3]
 // from columns tap*Cin + ci: sm=cin_total*9, sc=9, st=1, cp=Cin, base=ci_off*9; transposed: sm=1, sc=M)
 // Threads past M*N fold the bias slab [splits][M] (same fixed order) into bias_out.
+// Each thread sums 4 consecutive elements (16-B loads of every split slab; N is a multiple of 8, so the 4 share
+// a row); threads past M*N/4 fold the bias slab [splits][M] (same fixed order) into bias_out.
 __global__ void __launch_bounds__(256)
 tn_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N, float* __restrict__ out, long long base,
                  long long sm, long long sc, long long st, int cp, int accumulate, const float* __restrict__ bws,
                  float* __restrict__ bias_out, int bias_accumulate) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  const long long tot = (long long)M * N;
-  if (i >= tot) {
-    const long long m = i - tot;
+  const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
+  const long long tot = (long long)M * N, tot4 = tot >> 2;
+  if (t >= tot4) {
+    const long long m = t - tot4;
     if (!bias_out || m >= M) return;
     float s = 0.0f;
     for (int k = 0; k < splits; ++k) s += bws[(size_t)k * M + m];
     bias_out[m] = bias_accumulate ? bias_out[m] + s : s;
     return;
   }
+  const long long i = 4 * t;
   const int m = (int)(i / N), n = (int)(i - (long long)m * N);
-  float s = 0.0f;
-  for (int k = 0; k < splits; ++k) s += ws[(size_t)k * tot + i];
-  const long long d = base + m * sm + (long long)(n % cp) * sc + (long long)(n / cp) * st;
-  out[d] = accumulate ? out[d] + s : s;
+  f32x4 s = load4f(ws + i);
+  for (int k = 1; k < splits; ++k) s += load4f(ws + (size_t)k * tot + i);
+  if (sc == 1 && (n % cp) + 4 <= cp) {  // 4 consecutive destinations (dense layouts, and a conv's channel run)
+    float* d = out + base + m * sm + (long long)(n % cp) + (long long)(n / cp) * st;
+    if (accumulate) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] += s[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) d[e] = s[e];
+    }
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int ne = n + e;
+    const long long d = base + m * sm + (long long)(ne % cp) * sc + (long long)(ne / cp) * st;
+    out[d] = accumulate ? out[d] + s[e] : s[e];
+  }
 }
 
 static int tmae_wgrad_reduce(const float* ws, int splits, int M, int N, float* out, long long base, long long sm,
                              long long sc, long long st, int cp, int accumulate, const float* bws, float* bias_out,
                              int bias_accumulate, hipStream_t s) {
-  const long long tot = (long long)M * N + (bias_out ? M : 0);
+  const long long tot = (long long)M * N / 4 + (bias_out ? M : 0);  // threads (N % 8 == 0: wgrad_t)
   if (tot == 0) return TMAE_OK;
   hipLaunchKernelGGL(tn_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, ws, splits, M, N, out,
                      base, sm, sc, st, cp, accumulate, bws, bias_out, bias_accumulate);

@@ -141,16 +141,26 @@ class FusedAdam(torch.optim.Optimizer):
 
 
 def _flat_owner(params):
-    """the flat gradient buffer when every gradient is a view of one executor buffer covering it exactly"""
+    """the flat gradient buffer when the gradients tile one executor buffer exactly: the same f32 storage,
+    contiguous, disjoint, covering it (autograd detaches the views the HIP backward returns, so they are
+    matched by storage and offsets, not by ``_base``)"""
     gs = [p.grad for p in params if p.grad is not None]
     if not gs:
         return None
-    base = gs[0]._base
-    if base is None or any(g._base is not base for g in gs):
+    st = gs[0].untyped_storage()
+    sp = st.data_ptr()
+    if any(g.dtype != torch.float32 or not g.is_contiguous() or g.untyped_storage().data_ptr() != sp for g in gs):
         return None
-    if sum(g.numel() for g in gs) != base.numel():
+    n = st.nbytes() // 4
+    spans = sorted((g.storage_offset(), g.numel()) for g in gs)
+    pos = 0
+    for off, k in spans:
+        if off != pos:
+            return None
+        pos += k
+    if pos != n:
         return None
-    return base
+    return torch.empty(0, dtype=torch.float32, device=gs[0].device).set_(st, 0, (n,))
 
 
 def clip_grad_norm_(parameters, max_norm, out=None):
