@@ -110,7 +110,7 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
     // A ring: step s's fragments in slot s % D, the load of step s + D issued right after slot s is read;
     // all 9 x NKC steps are unrolled so the slots are static registers (a rolled tap loop needed copies
     // of the in-flight loads at its back edge, i.e. a vmcnt(0) at the end of every tap)
-    constexpr int NS = 9 * NKC, D = NF >= 3 ? 3 : NF == 2 ? 4 : 6;
+    constexpr int NS = 9 * NKC, D = NF == 2 ? 4 : 6;
     bf16x8 ar[D][NF];
     const bf16* wl[NF];
 #pragma unroll
@@ -214,23 +214,20 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
       q[0] = (bf16)lo.x; q[1] = (bf16)lo.y; q[2] = (bf16)hi.x; q[3] = (bf16)hi.y;
       return q;
     };
-    if (NF % 2 == 0 && (L.cout & 7) == 0 && !(LSTK_OPT & 1)) {
-      // v_permlane16_swap pairs lane rows (fq, fq ^ 1) of fragments (2p, 2p + 1): even rows gather 8
-      // consecutive channels of fragment 2p, odd rows of fragment 2p + 1, so each lane stores 16 B per pixel
-      // fragment (one ds_write_b128 instead of two ds_write_b64 with 4-way bank conflicts)
+    if (NF == 2 && (L.cout & 7) == 0 && !(LSTK_OPT & 1)) {
+      // v_permlane16_swap pairs lane rows (fq, fq ^ 1): even rows gather 8 consecutive channels of
+      // fragment 0, odd rows of fragment 1, so each lane stores 16 B per pixel fragment (one ds_write_b128
+      // instead of two ds_write_b64 with 4-way bank conflicts)
+      const int ch = 16 * (f0 + (fq & 1)) + 4 * (fq & 2);
+      const bool okw = ch < L.cout;
 #pragma unroll
-      for (int pr = 0; pr < NF / 2; ++pr) {
-        const int ch = 16 * (f0 + 2 * pr + (fq & 1)) + 4 * (fq & 2);
-        const bool okw = ch < L.cout;
-#pragma unroll
-        for (int j = 0; j < MF; ++j) {
-          const bf16x4 qa = gelu4(2 * pr, j), qb = gelu4(2 * pr + 1, j);
-          const uint2 ua = *reinterpret_cast<const uint2*>(&qa), ub = *reinterpret_cast<const uint2*>(&qb);
-          const auto r0 = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
-          const auto r1 = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
-          if (okw && pix(j) < npix)
-            *reinterpret_cast<uint4*>(lb + out_off + pix(j) * pout + 2 * ch) = uint4{r0[0], r1[0], r0[1], r1[1]};
-        }
+      for (int j = 0; j < MF; ++j) {
+        const bf16x4 qa = gelu4(0, j), qb = gelu4(NF - 1, j);
+        const uint2 ua = *reinterpret_cast<const uint2*>(&qa), ub = *reinterpret_cast<const uint2*>(&qb);
+        const auto r0 = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+        const auto r1 = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+        if (okw && pix(j) < npix)
+          *reinterpret_cast<uint4*>(lb + out_off + pix(j) * pout + 2 * ch) = uint4{r0[0], r1[0], r0[1], r1[1]};
       }
     } else {
 #pragma unroll
@@ -417,22 +414,13 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
       const int nfr = (L.cout + 15) >> 4;
       const int nkc = pad32(L.cin) >> 5;
       // wave items.  LDS bandwidth binds first: one 1-KiB B read per 16-cycle MFMA on every SIMD is the
-      // whole 256 B/clk array, so every wide layer shares each B read between several output fragments
-      // (NF = 2 or 3) and the items are cut so that the 8 waves get 8 of them where that works out:
+      // whole 256 B/clk array, so every wide layer shares each B read between two output fragments
+      // (NF = 2); the pixel fragments are split in halves (5 + 4) where that balances the four SIMDs better:
       //   >= 14 output fragments (224): fragment pairs x all pixel fragments (7 items);
-      //   11..13 (176): groups of 3 fragments x pixel halves (4 x 2 items, each B read feeding 3 MFMAs; as
-      //         pairs it was 12 items, i.e. two rounds for half of the waves);
-      //   8..10 (128): fragment pairs x pixel halves, all first halves dealt before the second ones;
+      //   8..13 (176, 128): fragment pairs x pixel halves, all first halves dealt before the second ones;
       //   < 8 (80, 32): single fragments x pixel halves.
       const bool halves = nmf > 5;
-      if (nfr >= 11 && nfr < 14 && halves && !(LSTK_OPT & 2)) {
-        const int ng = (nfr + 2) / 3;
-        for (int it = wave; it < 2 * ng; it += NW) {
-          const int g = it < ng ? it : it - ng;
-          if (it < ng) lstk_dispatch<3, 5>(nkc, L, first, last, o, img, 3 * g, 0, lb, in_off, out_off, npix, G, lane);
-          else lstk_dispatch<3, 4>(nkc, L, first, last, o, img, 3 * g, 5, lb, in_off, out_off, npix, G, lane);
-        }
-      } else if (nfr >= 8) {
+      if (nfr >= 8) {
         const int ng = (nfr + 1) >> 1;
         if (nfr >= 14 || !halves) {
           for (int it = wave; it < ng; it += NW)
