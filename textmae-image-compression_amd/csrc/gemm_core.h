@@ -75,8 +75,11 @@ template <typename T> struct DenseSrc {
   BStride bs;
   struct Row { const T* ptr; };
   __device__ void batch(int b1, int b2) { p += bs.at(b1, b2); }
+  // rows past the end are clamped to the last row: their products only reach output rows / columns that
+  // every epilogue drops (m < M, n < N), so no lane needs a zero-page select in the K loop
   __device__ Row row(int m) const {
-    if (m >= rows) return {nullptr};
+    if (rows <= 0) return {nullptr};
+    m = min(m, rows - 1);
     const int sm = (m / G) * Gs + off + (m % G);
     return {p + (size_t)sm * ld};
   }
@@ -85,6 +88,10 @@ template <typename T> struct DenseSrc {
   }
   __device__ const void* addr(const Row& r, int kt, int c) const {
     return addr_k(r, kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC);
+  }
+  // a K-step that lies wholly inside K (the caller checks that, wave-uniformly): plain pointer arithmetic
+  __device__ const void* addr_full(const Row& r, int kt, int c) const {
+    return r.ptr + kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC;
   }
   __device__ uint4 load(const Row& r, int kt, int c) const { return *reinterpret_cast<const uint4*>(addr(r, kt, c)); }
 };
@@ -148,6 +155,17 @@ template <typename T> struct PatchSrc {
     return load_chunk_from_f32<T>(r.base + (ch * H + py) * W + px);
   }
 };
+
+// address of a whole (in-K) K-step chunk: the source's addr_full when it has one, else its checked addr
+template <class S, class = void> struct HasAddrFull : std::false_type {};
+template <class S>
+struct HasAddrFull<S, std::void_t<decltype(std::declval<const S&>().addr_full(std::declval<const typename S::Row&>(), 0, 0))>>
+    : std::true_type {};
+template <class S>
+__device__ __forceinline__ const void* src_addr_full(const S& s, const typename S::Row& r, int kt, int c) {
+  if constexpr (HasAddrFull<S>::value) return s.addr_full(r, kt, c);
+  else return s.addr(r, kt, c);
+}
 
 // ------------------------------------------------------------------ tile order
 // logical tile id -> (n tile, m tile): groups of 8 M-tiles x all N-tiles, M fastest, so workgroups
@@ -398,10 +416,20 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
   auto issue = [&](int stage, int kt) {
     if (diag & 4) return;  // timing diagnostic: no staging
     const unsigned sb = lds_base + (unsigned)stage * ROWS * 128u;
+    if (kt * BKE + BKE <= K) {  // whole K-step: sources with addr_full skip the per-lane bounds select
 #pragma unroll
-    for (int j = 0; j < WJ; ++j) glds16(ws.addr(wrow[j], kt, wc[j]), sb + (unsigned)(PR * j + 8 * wave_u) * 128u);
+      for (int j = 0; j < WJ; ++j)
+        glds16(src_addr_full(ws, wrow[j], kt, wc[j]), sb + (unsigned)(PR * j + 8 * wave_u) * 128u);
 #pragma unroll
-    for (int j = 0; j < XJ; ++j) glds16(xs.addr(xrow[j], kt, xc[j]), sb + (unsigned)(BN + PR * j + 8 * wave_u) * 128u);
+      for (int j = 0; j < XJ; ++j)
+        glds16(src_addr_full(xs, xrow[j], kt, xc[j]), sb + (unsigned)(BN + PR * j + 8 * wave_u) * 128u);
+    } else {
+#pragma unroll
+      for (int j = 0; j < WJ; ++j) glds16(ws.addr(wrow[j], kt, wc[j]), sb + (unsigned)(PR * j + 8 * wave_u) * 128u);
+#pragma unroll
+      for (int j = 0; j < XJ; ++j)
+        glds16(xs.addr(xrow[j], kt, xc[j]), sb + (unsigned)(BN + PR * j + 8 * wave_u) * 128u);
+    }
   };
 
   f32x4 acc[TN][TM];
