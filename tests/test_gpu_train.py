@@ -68,6 +68,23 @@ def test_wgrad_remap_transposed_accumulate(T):
     check("_rel:out_1", _rel(out - 1, ref), 1e-5)
 
 
+@pytest.mark.parametrize("M,N", [(768, 200), (72, 1000)])
+def test_wgrad_remap_bf16(T, M, N):
+    # the bf16 kernel's in-range address path on grouped rows (the encoder's 144 patch rows of every 145, cls
+    # row first) on both operands; tile / split / column tails (M, N not multiples of the tiles)
+    G, imgs = 144, 20
+    K = G * imgs
+    a_full, b_full = _rnd(imgs * (G + 1), M, seed=5), _rnd(imgs * (G + 1), N, seed=6)
+    rows = torch.tensor([(k // G) * (G + 1) + 1 + k % G for k in range(K)])
+    dt = torch.bfloat16
+    ref = (a_full[rows].to(dt).double().t() @ b_full[rows].to(dt).double()).float()
+    out = torch.empty(M, N, device="cuda")
+    T.wgrad(a_full.cuda().to(dt), b_full.cuda().to(dt), M, N, K, out, dt, a_remap=(G, G + 1, 1),
+            b_remap=(G, G + 1, 1))
+    torch.cuda.synchronize()
+    check("_rel:out", _rel(out, ref), 2e-3)
+
+
 @pytest.mark.parametrize("stride", [1, 2])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_wgrad_conv(T, stride, dt):

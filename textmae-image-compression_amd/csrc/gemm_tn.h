@@ -30,6 +30,22 @@ template <typename T> struct KDenseSrc {
     const int sk = (k / G) * Gs + off + (k % G);
     return p + (size_t)sk * ld + c;
   }
+  // row k inside the operand (the caller's K-step lies wholly inside the k range): columns past `cols`
+  // read the last 8 columns (their products reach only output rows / columns the epilogue drops);
+  // `grouped` (wave-uniform, G < K): the row group k / G is a float-reciprocal quotient with one correction
+  // instead of an integer division; ungrouped rows are plain 32-bit offset arithmetic
+  __device__ const void* addr_in(int k, int c, float inv_g, bool grouped) const {
+    c = min(c, cols - 8);
+    int sk = off + k;
+    if (grouped) {
+      int q = (int)((float)k * inv_g);
+      int r = k - q * G;
+      if (r >= G) { ++q; r -= G; }
+      if (r < 0) { --q; r += G; }
+      sk = q * Gs + off + r;
+    }
+    return p + ((unsigned)sk * (unsigned)ld + (unsigned)c);
+  }
 };
 
 // implicit im2col of a 3x3 conv (padding 1, stride s) over NHWC maps: row k = output pixel
@@ -63,6 +79,19 @@ struct EpiSplitWs {
   __device__ void operator()(int m, int n, f32x4 v) const { store4(ws + (size_t)m * N + n, v); }
   __device__ void wide(int m, int n, f32x4 lo, f32x4 hi) const { store8(ws + (size_t)m * N + n, lo, hi); }
 };
+
+// in-range address of a k-major source: KDenseSrc's addr_in, the checked addr for the others
+template <class S> __device__ __forceinline__ float tn_inv_g(const S&) { return 0.0f; }
+template <typename T> __device__ __forceinline__ float tn_inv_g(const KDenseSrc<T>& s) { return 1.0f / (float)s.G; }
+template <class S> __device__ __forceinline__ bool tn_grouped(const S&, int) { return true; }
+template <typename T> __device__ __forceinline__ bool tn_grouped(const KDenseSrc<T>& s, int K) { return s.G < K; }
+template <class S> __device__ __forceinline__ const void* tn_addr_in(const S& s, int k, int c, float, bool) {
+  return s.addr(k, c);
+}
+template <typename T>
+__device__ __forceinline__ const void* tn_addr_in(const KDenseSrc<T>& s, int k, int c, float inv_g, bool grouped) {
+  return s.addr_in(k, c, inv_g, grouped);
+}
 
 __device__ __forceinline__ int tn_swz(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
 
@@ -134,9 +163,19 @@ gemm_tn_bf16_kernel(AS as, BS bs, EpiSplitWs epi, int M, int N, int K, int kchun
   }
   const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
+  const float inv_ga = tn_inv_g(as), inv_gb = tn_inv_g(bs);
+  const bool grp_a = tn_grouped(as, K), grp_b = tn_grouped(bs, K);  // wave-uniform
   auto issue = [&](int stage, int kt) {
     const unsigned sb = lds_base + (unsigned)stage * STAGE;
     const int kb = k0 + kt * BK;
+    if (kb + BK <= k1) {  // whole K-step inside this split's range (wave-uniform): no per-row bounds select
+#pragma unroll
+      for (int p = 0; p < WPN; ++p) glds16(tn_addr_in(bs, kb + nrow[p], ncol[p], inv_gb, grp_b), sb + (wave_u + NW * p) * 1024u);
+#pragma unroll
+      for (int p = 0; p < WPM; ++p)
+        glds16(tn_addr_in(as, kb + mrow[p], mcol[p], inv_ga, grp_a), sb + IMG_N + (wave_u + NW * p) * 1024u);
+      return;
+    }
 #pragma unroll
     for (int p = 0; p < WPN; ++p) {
       const int k = kb + nrow[p];
