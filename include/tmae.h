@@ -396,7 +396,8 @@ int tmae_conv_dgrad(const tmae_conv_dgrad_args* args, int dtype, void* stream);
 int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0, int d1, int d2, int d3, long long s0, long long s1,
                   long long s2, long long s3, void* stream);
 /* every relayout of a table in one launch: table[t] = {src, dst, dst_dtype, d1, d2, d3, s0, s1, s2, s3, total,
- * first_chunk} (int64, device memory), first_chunk = sum of ceil(total / 2048) over the tensors before t */
+ * first_chunk} (int64, device memory), first_chunk = the chunks of the tensors before t (a plain or strided
+ * copy: ceil(total / 8192); a 2-D transpose: 64 x 64 tiles; a per-row transpose: rows) */
 int tmae_relayout_multi(const long long* table, int ntensors, long long nchunks, void* stream);
 
 /* bias gradient: out[c] (=/+=) sum over rows r of x[(r/G)*Gs + off + r%G][c]; work >= 256*C floats */
@@ -453,7 +454,7 @@ int tmae_adam(float* p, const float* g, float* m, float* v, long long n, float l
  * chunks of 1024 elements, nchunks in total */
 int tmae_adam_multi(const long long* table, int ntensors, long long nchunks, float lr, float beta1, float beta2,
                     float eps, float weight_decay, int step, const float* clip, void* stream);
-/* clip_grad_norm_: out[0] = ||g||_2, out[1] = min(1, max_norm / (norm + 1e-6)); work >= 512 doubles */
+/* clip_grad_norm_: out[0] = ||g||_2, out[1] = min(1, max_norm / (norm + 1e-6)); work >= 2048 doubles */
 int tmae_grad_norm(const float* g, long long n, double* work, float max_norm, float* out, void* stream);
 /* g *= scale[0] */
 int tmae_scale(float* g, long long n, const float* scale, void* stream);

@@ -255,6 +255,22 @@ def test_adam_matches_torch(T):
     assert abs(norm[1].item() - min(1.0, 1.0 / (g.norm().item() + 1e-6))) < 1e-6
 
 
+@pytest.mark.parametrize("n,off", [(3_000_013, 0), (1_048_576 + 5, 1)])
+def test_grad_norm_and_scale_vector_paths(T, n, off):
+    # the 16-B paths of the norm and the in-place scale, a ragged tail, and an unaligned buffer (off = 1 float)
+    g0 = _rnd(n + off, seed=25)
+    buf = g0.cuda()
+    g = buf[off:]
+    norm = torch.empty(2, device="cuda")
+    T.grad_norm(g, 0.5, norm)
+    T.scale_(g, norm[1:])
+    torch.cuda.synchronize()
+    ref = g0[off:].double().norm().item()
+    assert abs(norm[0].item() - ref) < 1e-5 * ref
+    assert torch.equal(buf[off:].cpu(), g0[off:] * norm[1].item())
+    assert torch.equal(buf[:off].cpu(), g0[:off])
+
+
 # ------------------------------------------------------------------------------ whole model
 SMALL = dict(img_size=64, patch_size=16, encoder_embed_dim=64, encoder_depth=2, encoder_num_heads=2,
              decoder_embed_dim=64, decoder_depth=2, decoder_num_heads=2, latent_depth=192, hyperprior_depth=96,
@@ -431,16 +447,16 @@ def test_relayout_multi_dense_and_strided(T, dt):
     from textmae_amd import _lib, ops
 
     dev = "cuda"
-    srcs = [_rnd(5000, seed=1), _rnd(64, 3, 3, 40, seed=2), _rnd(4096, seed=3), _rnd(96, 130, seed=4),
-            _rnd(2048 * 3 + 7, seed=5)]
+    srcs = [_rnd(5000, seed=1), _rnd(64, 3, 3, 40, seed=2), _rnd(8192 * 2 + 16, seed=3), _rnd(96, 130, seed=4),
+            _rnd(8192 * 2 + 7, seed=5)]
     srcs = [s.to(dev) for s in srcs]
-    big = torch.empty(2048 * 3 + 8, dtype=dt, device=dev)
+    big = torch.empty(8192 * 2 + 8, dtype=dt, device=dev)
     jobs = [  # (source, destination, dims, element strides)
         (srcs[0], torch.empty(5000, dtype=dt, device=dev), (5000,), (1,)),
         (srcs[1], torch.empty(64, 40, 3, 3, dtype=dt, device=dev), (64, 40, 3, 3), (360, 1, 120, 40)),
-        (srcs[2], torch.empty(4096, dtype=dt, device=dev), (4096,), (1,)),
+        (srcs[2], torch.empty(8192 * 2 + 16, dtype=dt, device=dev), (8192 * 2 + 16,), (1,)),  # 3 chunks, ragged last
         (srcs[3], torch.empty(130, 96, dtype=dt, device=dev), (130, 96), (1, 130)),
-        (srcs[4], big[1:], (2048 * 3 + 7,), (1,)),   # destination 2 or 4 B past a 16-B boundary
+        (srcs[4], big[1:], (8192 * 2 + 7,), (1,)),   # destination 2 or 4 B past a 16-B boundary
     ]
     rows, chunk = [], 0
     for s, d, dims, st in jobs:
@@ -448,7 +464,7 @@ def test_relayout_multi_dense_and_strided(T, dt):
         ss = list(st) + [0] * (4 - len(st))
         total = dd[0] * dd[1] * dd[2] * dd[3]
         rows.append([s.data_ptr(), d.data_ptr(), ops.dtype_code(dt), dd[1], dd[2], dd[3], *ss, total, chunk])
-        chunk += (total + 2047) // 2048
+        chunk += (total + 8191) // 8192
     tab = torch.tensor(rows, dtype=torch.int64).to(dev)
     _lib.call("tmae_relayout_multi", tab.data_ptr(), len(rows), chunk, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()

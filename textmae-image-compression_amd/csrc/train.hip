@@ -379,9 +379,12 @@ extern "C" int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0,
 }
 
 // multi-tensor form: table[t] = {src, dst, dst_dtype | mode << 8, d1, d2, d3, s0, s1, s2, s3, total, first_chunk}
-// (int64); a block finds its tensor by binary search over first_chunk.  One launch re-lays out every weight whose
+// (int64); a block finds its tensor by binary search over first_chunk (staged in LDS by one coalesced read when
+// nt <= 1024: a search over the global table was ~9 dependent global-load round trips per block, the bulk of the
+// launch for the plain casts).  One launch re-lays out every weight whose
 // version moved (the optimizer step), instead of one launch per weight and layout.  Modes (host-chosen):
-//   0  2048-element chunks: plain casts as 16-B vectors, anything else as a strided gather;
+//   0  8192-element chunks: plain casts as 16-B vectors (4 x 8 elements per thread), anything else as a
+//      strided gather;
 //   1  2-D transpose dst[c][r] = src[r * s3 + c] (R = d3 source rows, C = total / R): 64 x 64 LDS tiles, coalesced
 //      both ways (nn.Linear data-gradient operands W^T; the conv data-gradient layout [Cin][3][3][Cout], which is
 //      the transpose of the weight seen as [Cout][Cin * 9]);
@@ -393,12 +396,23 @@ __device__ __forceinline__ void relayout_store(void* dst, size_t i, float v) { r
 __global__ void __launch_bounds__(256)
 relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
   __shared__ float sm[8192];
+  __shared__ long long first[1024];
   const long long b = blockIdx.x;
   int lo = 0, hi = nt - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (tab[12 * mid + 11] <= b) lo = mid;
-    else hi = mid - 1;
+  if (nt <= 1024) {
+    for (int t = threadIdx.x; t < nt; t += 256) first[t] = tab[12 * t + 11];
+    __syncthreads();
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (first[mid] <= b) lo = mid;
+      else hi = mid - 1;
+    }
+  } else {
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tab[12 * mid + 11] <= b) lo = mid;
+      else hi = mid - 1;
+    }
   }
   const long long* e = tab + 12 * lo;
   const float* src = (const float*)e[0];
@@ -443,21 +457,29 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
       }
     return;
   }
-  const unsigned base = chunk * 2048u;
-  // a plain cast (contiguous source, 16-B aligned ends): 8 elements per thread, vector loads and stores
+  const unsigned base = chunk * 8192u;
+  // a plain cast (contiguous source, 16-B aligned ends): 4 x 8 elements per thread, vector loads and stores
   const bool dense = (d3 == 1 || s3 == 1) && (d2 == 1 || s2 == (long long)d3) && (d1 == 1 || s1 == (long long)d2 * d3) &&
                      s0 == (long long)d1 * d2 * d3 &&
                      ((((unsigned long long)src) | ((unsigned long long)e[1])) & 15) == 0;
-  if (dense && base + 2048u <= total) {
-    const unsigned i = base + 8u * tid;
-    f32x4 lo4, hi4;
-    load8f(src + i, lo4, hi4);
-    if (to_bf16) store8((bf16*)e[1] + i, lo4, hi4);
-    else store8((float*)e[1] + i, lo4, hi4);
+  if (dense && (total & 7u) == 0) {
+    f32x4 lo4[4], hi4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned i = base + 2048u * u + 8u * tid;
+      if (i < total) load8f(src + i, lo4[u], hi4[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned i = base + 2048u * u + 8u * tid;
+      if (i >= total) break;
+      if (to_bf16) store8((bf16*)e[1] + i, lo4[u], hi4[u]);
+      else store8((float*)e[1] + i, lo4[u], hi4[u]);
+    }
     return;
   }
   // general strided gather: 32-bit index arithmetic (64-bit division is a long VALU sequence)
-  for (unsigned k = tid; k < 2048u; k += 256u) {
+  for (unsigned k = tid; k < 8192u; k += 256u) {
     const unsigned i = base + k;
     if (i >= total) break;
     unsigned r = i;
@@ -522,15 +544,17 @@ colsum_partial8_kernel(const T* __restrict__ x, int ld, int rows, int C, int G, 
 __global__ void __launch_bounds__(1024)
 fold_rows_kernel(const float* __restrict__ part, int rows, int C, float* __restrict__ out0, float* __restrict__ out1,
                  int split, int accumulate, float* __restrict__ out2, int split2) {
-  __shared__ float red[16][65];
-  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cx;
+  // 16 columns x 64 row-lanes per block (64-B row segments): four times the blocks and a quarter of the
+  // serial rows per thread of a 64 x 16 block -- these folds are latency-bound (C = 2304 gave 36 blocks)
+  __shared__ float red[64][17];
+  const int cx = threadIdx.x & 15, ry = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cx;
   float s = 0.0f;
   if (c < C)
-    for (int r = ry; r < rows; r += 16) s += part[(size_t)r * C + c];
+    for (int r = ry; r < rows; r += 64) s += part[(size_t)r * C + c];
   red[ry][cx] = s;
   __syncthreads();
-  for (int o = 8; o > 0; o >>= 1) {
+  for (int o = 32; o > 0; o >>= 1) {
     if (ry < o) red[ry][cx] += red[ry + o][cx];
     __syncthreads();
   }
@@ -542,7 +566,7 @@ fold_rows_kernel(const float* __restrict__ part, int rows, int C, float* __restr
 
 static void fold_rows(const float* part, int rows, int C, float* out0, float* out1, int split, int accumulate,
                       hipStream_t st, float* out2 = nullptr, int split2 = -1) {
-  hipLaunchKernelGGL(fold_rows_kernel, dim3(ceil_div(C, 64)), dim3(1024), 0, st, part, rows, C, out0, out1, split,
+  hipLaunchKernelGGL(fold_rows_kernel, dim3(ceil_div(C, 16)), dim3(1024), 0, st, part, rows, C, out0, out1, split,
                      accumulate, out2, split2 < 0 ? C : split2);
 }
 
@@ -1389,9 +1413,23 @@ extern "C" int tmae_adam_multi(const long long* table, int ntensors, long long n
 // order), out[1] = min(1, max_norm / (norm + 1e-6)) -- the factor applied to the gradients (no host sync)
 __global__ void __launch_bounds__(256)
 sumsq_partial_kernel(const float* __restrict__ g, long long n, double* __restrict__ part) {
+  // 16-B loads, four of them in flight per thread (a 4-B load per iteration ran at ~1.3 TB/s); element
+  // assignment and summation order fixed by the grid, so the norm is reproducible
   __shared__ double red[256];
   double s = 0.0;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+  const long long n16 = (((unsigned long long)g & 15) == 0) ? n / 16 * 16 : 0;
+  const long long stride = (long long)gridDim.x * 256 * 16;
+  // block b's window per trip: 4096 elements at b * 4096 (+ stride per trip); thread t: float4s t, t + 256, ...
+  for (long long i = (long long)blockIdx.x * 4096 + threadIdx.x * 4; i < n16; i += stride) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (i + 1024 * u < n16) ? load4f(g + i + 1024 * u) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) s += (double)v[u][e] * (double)v[u][e];
+  }
+  for (long long i = n16 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     const double x = g[i];
     s += x * x;
   }
@@ -1425,19 +1463,27 @@ clip_final_kernel(const double* __restrict__ part, int np, float max_norm, float
 extern "C" int tmae_grad_norm(const float* g, long long n, double* work, float max_norm, float* out, void* stream) {
   TMAE_REQUIRE(g && work && out, "tmae_grad_norm: null argument");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(512), dim3(256), 0, st, g, n, work);
-  hipLaunchKernelGGL(clip_final_kernel, dim3(1), dim3(256), 0, st, work, 512, max_norm, out);
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(2048), dim3(256), 0, st, g, n, work);
+  hipLaunchKernelGGL(clip_final_kernel, dim3(1), dim3(256), 0, st, work, 2048, max_norm, out);
   TMAE_LAUNCH_CHECK("tmae_grad_norm");
 }
 
 // grads *= scale[0] (clip_grad_norm_ applies its factor to the stored gradients)
+// 8 elements per thread by 16-B accesses when g is 16-B aligned (one element per thread ran at ~3.8 TB/s)
 __global__ void __launch_bounds__(256) scale_kernel(float* __restrict__ g, long long n, const float* __restrict__ s) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) g[i] *= s[0];
+  const float f = s[0];
+  const long long i = ((long long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (((unsigned long long)g & 15) == 0 && i + 8 <= n) {
+    f32x4 a, b;
+    load8f(g + i, a, b);
+    store8(g + i, a * f, b * f);
+    return;
+  }
+  for (long long k = i; k < i + 8 && k < n; ++k) g[k] *= f;
 }
 
 extern "C" int tmae_scale(float* g, long long n, const float* scale, void* stream) {
   if (n <= 0) return TMAE_OK;
-  hipLaunchKernelGGL(scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, g, n, scale);
+  hipLaunchKernelGGL(scale_kernel, dim3((unsigned)((n + 2047) / 2048)), dim3(256), 0, (hipStream_t)stream, g, n, scale);
   TMAE_LAUNCH_CHECK("tmae_scale");
 }

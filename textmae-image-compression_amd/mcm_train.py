@@ -112,7 +112,7 @@ class _Weights:
                   and st[0] == d[1] * d[2] * d[3]):  # per-row [A][B] -> [B][A]
                 mode, n = 2, d[0]
             else:
-                mode, n = 0, (total + 2047) // 2048
+                mode, n = 0, (total + 8191) // 8192
             rows.append([p.data_ptr(), dst.data_ptr(), ops.dtype_code(dst.dtype) | (mode << 8), d[1], d[2], d[3], *st,
                          total, chunk])
             ptrs.append((p.data_ptr(), dst.data_ptr()))

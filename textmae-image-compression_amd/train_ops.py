@@ -241,7 +241,7 @@ def adam(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, clip=None):
 
 def grad_norm(g, max_norm, out):
     """out[0] = ||g||, out[1] = clip factor (device f32 [2])"""
-    work = scratch(g.device, 1024, slot=3)
+    work = scratch(g.device, 4096, slot=3)  # 2048 f64 partials
     _lib.call("tmae_grad_norm", g.data_ptr(), g.numel(), work.data_ptr(), float(max_norm), out.data_ptr(), _stream())
     return out
 
