@@ -64,7 +64,8 @@ int tmae_linear_residual_fwd(const void* x, int ldx, const void* w, const float*
 
 /* PatchEmbed conv16/s16 + pos_embed + masking gather, over the KEPT patches only
  * (MCM.py:615-621 then the gather at 585-586): tokens [n][keep+1][D], rows 1..keep written;
- * w = proj.weight viewed [D][C*P*P]. */
+ * w = proj.weight viewed [D][C*P*P], each row zero-padded to a multiple of 8 values when C*P*P is not
+ * (patch 14: 588 -> 592).  Any patch size dividing the image; rows of P % 8 != 0 gather per value. */
 int tmae_patch_embed_fwd(const float* imgs, const int64_t* ids_shuffle, const void* w, const float* bias,
                          const float* pos, float* tokens, int n, int C, int H, int W, int patch, int D, int L,
                          int keep, int dtype, void* stream);
@@ -73,7 +74,7 @@ int tmae_patch_embed_fwd(const float* imgs, const int64_t* ids_shuffle, const vo
 int tmae_cls_rows(float* tokens, const float* cls, const float* pos, int n, int rows_per_img, int D, void* stream);
 
 /* Fused multi-head attention over qkv [B*T][3*H*dh] (timm layout (3, H, dh)) -> out [B*T][H*dh];
- * softmax((q k^T) * scale) v, dh in {32, 64}, T <= 512. */
+ * softmax((q k^T) * scale) v, dh in {32, 64, 80} (80: ViT-H, models_mae.py:239-244), T <= 512. */
 int tmae_mha_fwd(const void* qkv, void* out, int B, int T, int H, int dh, float scale, int dtype, void* stream);
 
 /* decoder_embed + mask-token unshuffle + decoder_pos_embed (MCM.py:657-675):

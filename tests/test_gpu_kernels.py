@@ -122,7 +122,7 @@ def _ref_attn(qkv, B, T, H, dh):
 
 
 @pytest.mark.parametrize("B,T,H,dh", [(4, 145, 12, 64), (3, 257, 16, 32), (2, 17, 2, 32), (1, 32, 1, 64),
-                                      (2, 33, 4, 64)])
+                                      (2, 33, 4, 64), (2, 65, 16, 80), (1, 161, 3, 80)])
 @pytest.mark.parametrize("dtype", DTYPES)
 def test_mha(tmae, B, T, H, dh, dtype):
     torch.manual_seed(T)

@@ -112,7 +112,28 @@ def test_vitl_vs_oracle_and_split_api(tmae):
         m(imgs.to(DEV))  # parameters require grad and grad mode is on: no backward kernels in this build
 
 
-def test_huge_head_dim_reports(tmae):
+def test_huge_patch14_vs_oracle(tmae):
+    """ViT-H factory (models_mae.py:239-244): patch 14 (588-value patch rows, per-value gather), 32 x 1280,
+    16 heads of dim 80 (attention tiles padded to 96), dec512d8b; f32 against the oracle at batch 1"""
+    torch.manual_seed(6)
     m = tmae.mae_vit_huge_patch14_dec512d8b().to(DEV)
-    with torch.no_grad(), pytest.raises(ValueError, match="head dim"):
-        m(torch.zeros(1, 3, 224, 224, device=DEV))
+    imgs = torch.randn(1, 3, 224, 224, generator=torch.Generator().manual_seed(7))
+    noise = torch.rand(1, 256, generator=torch.Generator().manual_seed(8))
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    with torch.no_grad():
+        rl, rp, rm = mae_forward(sd, imgs, noise, 0.75, 14, 16, 16, 32, 8)
+        loss, pred, mask = m(imgs.to(DEV), 0.75, noise=noise.to(DEV))
+    assert pred.shape == (1, 256, 588) and torch.equal(mask.cpu(), rm)
+    check("maxrel:pred", maxrel(pred, rp), 1e-3)
+    np.testing.assert_allclose(float(loss), float(rl), rtol=1e-3)
+
+
+def test_head_dim_reports(tmae):
+    from functools import partial
+
+    m = tmae.MaskedAutoencoderViT(img_size=32, patch_size=16, embed_dim=96, depth=1, num_heads=2,
+                                  decoder_embed_dim=32, decoder_depth=1, decoder_num_heads=1,
+                                  norm_layer=partial(torch.nn.LayerNorm, eps=1e-6)).to(DEV)
+    with torch.no_grad(), pytest.raises(ValueError, match="head dim 48"):
+        m(torch.zeros(1, 3, 32, 32, device=DEV))

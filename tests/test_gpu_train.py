@@ -185,7 +185,7 @@ def test_layernorm_bwd_remap(T):
 
 
 # ------------------------------------------------------------------------------ attention
-@pytest.mark.parametrize("T_,H,dh", [(145, 12, 64), (257, 16, 32), (20, 2, 64)])
+@pytest.mark.parametrize("T_,H,dh", [(145, 12, 64), (257, 16, 32), (20, 2, 64), (65, 4, 80), (161, 2, 80)])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_mha_bwd(T, T_, H, dh, dt):
     from textmae_amd import ops

@@ -23,7 +23,10 @@ __global__ void __launch_bounds__(1024)
 mha_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, float* __restrict__ lse, int Tn, int H, int Tpad,
                float scale_log2e) {
   constexpr int KPAD = AttnCfg<T>::KPAD, VPAD = AttnCfg<T>::VPAD, EPC = AttnCfg<T>::EPC;
-  constexpr int NDT = DH / 32;  // 32-wide output tiles along the head dim
+  // 32-wide output tiles along the head dim; a head dim that is not a multiple of 32 (ViT-H: 80) gets
+  // zero rows DH..DHP-1 in V^T, so the last tile's extra output columns are zero and never stored
+  constexpr int DHP = (DH + 31) / 32 * 32, NDT = DHP / 32;
+  static_assert(DH % 16 == 0, "head dim must be a multiple of 16");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int ldk = DH + KPAD, ldv = Tpad + VPAD;
   T* Ks = reinterpret_cast<T*>(smem);
@@ -34,8 +37,10 @@ mha_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, float* __restrict
   const T* base = qkv + (size_t)b * Tn * ld + h * DH;
   const int tid = threadIdx.x, nthr = blockDim.x;
 
-  // stage K [Tpad][DH] and V^T [DH][Tpad] of this head
+  // stage K [Tpad][DH] and V^T [DHP][Tpad] of this head
   constexpr int CPR = DH / EPC;  // 16-B chunks per row
+  if constexpr (DHP != DH)
+    for (int i = tid; i < (DHP - DH) * ldv; i += nthr) Vt[(size_t)DH * ldv + i] = (T)0.0f;
   for (int i = tid; i < Tpad * CPR; i += nthr) {
     const int r = i / CPR, c = i - r * CPR;
     uint4 kv = uint4{0, 0, 0, 0}, vv = uint4{0, 0, 0, 0};
@@ -172,6 +177,7 @@ mha_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, float* __restrict
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int d = 32 * dt + 8 * g + 4 * hh;
+      if (DHP != DH && d >= DH) continue;
       f32x4 v{O[dt][4 * g] * inv_l, O[dt][4 * g + 1] * inv_l, O[dt][4 * g + 2] * inv_l, O[dt][4 * g + 3] * inv_l};
       store4(orow + d, v);
     }
@@ -186,7 +192,7 @@ mha_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, float* __restrict
 //     P <= 2^8, exact after the final 1/l (same m for O and l);
 //   * per-lane partial row sums, combined across the two lane halves once at the end;
 //   * V^T staged with keys on consecutive lanes (2-byte LDS stores to consecutive addresses).
-template <int DH> struct AttnTr;
+template <int DH> struct AttnTr { static constexpr int LDV = 0; };  // no lean form
 // V row stride (elements) for conflict-free ds_read_b64_tr_b16: 4 key rows x 2 lane groups of 8 dwords
 // must cover all 64 banks -> row stride = 16 or 48 dwords mod 64
 template <> struct AttnTr<64> { static constexpr int LDV = 96; };
@@ -389,41 +395,50 @@ template <typename T, int DH>
 static int mha_launch(const void* qkv, void* out, int B, int Tn, int H, float scale, hipStream_t st,
                       float* lse = nullptr) {
   const int Tpad = (Tn + 31) / 32 * 32;
-  const bool lean = sizeof(T) == 2 && !getenv("TMAE_MHA_PLAIN");
+  constexpr bool lean_ok = sizeof(T) == 2 && DH % 32 == 0;  // the VALU-lean kernel takes whole 32-wide tiles
+  constexpr int DHP = (DH + 31) / 32 * 32;
+  const bool lean = lean_ok && !getenv("TMAE_MHA_PLAIN");
   const int nthr = 64 * (Tpad / 32);
   const size_t lds = lean ? ((size_t)Tpad * (DH + 8) + (size_t)Tpad * AttnTr<DH>::LDV) * 2
-                          : ((size_t)Tpad * (DH + AttnCfg<T>::KPAD) + (size_t)DH * (Tpad + AttnCfg<T>::VPAD)) * sizeof(T);
+                          : ((size_t)Tpad * (DH + AttnCfg<T>::KPAD) + (size_t)DHP * (Tpad + AttnCfg<T>::VPAD)) * sizeof(T);
   TMAE_REQUIRE(nthr <= 1024 && lds <= 160 * 1024, "tmae_mha_fwd: sequence length %d too long", Tn);
   TMAE_REQUIRE(!lean || Tpad * (DH / 8) <= nthr * (DH / 16), "tmae_mha_fwd: sequence length %d too long", Tn);
   if (B * H == 0 || Tn == 0) return TMAE_OK;
-  if (lean)
-    hipLaunchKernelGGL((mha_fwd_bf16_kernel<DH>), dim3(B * H), dim3(nthr), lds, st, (const bf16*)qkv, (bf16*)out,
-                       lse, Tn, H, Tpad, scale * 1.4426950408889634f);
-  else
+  if constexpr (lean_ok) {
+    if (lean) {
+      hipLaunchKernelGGL((mha_fwd_bf16_kernel<DH>), dim3(B * H), dim3(nthr), lds, st, (const bf16*)qkv, (bf16*)out,
+                         lse, Tn, H, Tpad, scale * 1.4426950408889634f);
+      TMAE_LAUNCH_CHECK("tmae_mha_fwd");
+    }
+  }
     hipLaunchKernelGGL((mha_fwd_kernel<T, DH>), dim3(B * H), dim3(nthr), lds, st, (const T*)qkv, (T*)out, lse, Tn, H,
                        Tpad, scale * 1.4426950408889634f);
   TMAE_LAUNCH_CHECK("tmae_mha_fwd");
 }
 
+template <typename E>
+static int mha_dispatch(const void* qkv, void* out, int B, int T, int H, int dh, float scale, hipStream_t st,
+                        float* lse) {
+  if (dh == 64) return mha_launch<E, 64>(qkv, out, B, T, H, scale, st, lse);
+  if (dh == 80) return mha_launch<E, 80>(qkv, out, B, T, H, scale, st, lse);  // ViT-H (models_mae.py:239-244)
+  return mha_launch<E, 32>(qkv, out, B, T, H, scale, st, lse);
+}
+
 extern "C" int tmae_mha_fwd(const void* qkv, void* out, int B, int T, int H, int dh, float scale, int dtype,
                             void* stream) {
-  TMAE_REQUIRE(dh == 32 || dh == 64, "tmae_mha_fwd: head dim %d unsupported (32 or 64)", dh);
+  TMAE_REQUIRE(dh == 32 || dh == 64 || dh == 80, "tmae_mha_fwd: head dim %d unsupported (32, 64 or 80)", dh);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == TMAE_BF16) return dh == 64 ? mha_launch<bf16, 64>(qkv, out, B, T, H, scale, st)
-                                          : mha_launch<bf16, 32>(qkv, out, B, T, H, scale, st);
-  return dh == 64 ? mha_launch<float, 64>(qkv, out, B, T, H, scale, st)
-                  : mha_launch<float, 32>(qkv, out, B, T, H, scale, st);
+  if (dtype == TMAE_BF16) return mha_dispatch<bf16>(qkv, out, B, T, H, dh, scale, st, nullptr);
+  return mha_dispatch<float>(qkv, out, B, T, H, dh, scale, st, nullptr);
 }
 
 extern "C" int tmae_mha_fwd_lse(const void* qkv, void* out, float* lse, int B, int T, int H, int dh, float scale,
                                 int dtype, void* stream) {
-  TMAE_REQUIRE(dh == 32 || dh == 64, "tmae_mha_fwd_lse: head dim %d unsupported (32 or 64)", dh);
+  TMAE_REQUIRE(dh == 32 || dh == 64 || dh == 80, "tmae_mha_fwd_lse: head dim %d unsupported (32, 64 or 80)", dh);
   TMAE_REQUIRE(lse != nullptr, "tmae_mha_fwd_lse: lse is NULL");
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == TMAE_BF16) return dh == 64 ? mha_launch<bf16, 64>(qkv, out, B, T, H, scale, st, lse)
-                                          : mha_launch<bf16, 32>(qkv, out, B, T, H, scale, st, lse);
-  return dh == 64 ? mha_launch<float, 64>(qkv, out, B, T, H, scale, st, lse)
-                  : mha_launch<float, 32>(qkv, out, B, T, H, scale, st, lse);
+  if (dtype == TMAE_BF16) return mha_dispatch<bf16>(qkv, out, B, T, H, dh, scale, st, lse);
+  return mha_dispatch<float>(qkv, out, B, T, H, dh, scale, st, lse);
 }
 
 // ====================================================================================== backward
@@ -441,6 +456,7 @@ template <int DH> struct AttnBwd;
 // conflict-free (as the forward's V^T)
 template <> struct AttnBwd<64> { static constexpr int LDR = 96; };
 template <> struct AttnBwd<32> { static constexpr int LDR = 32; };
+template <> struct AttnBwd<80> { static constexpr int LDR = 96; };  // columns 80..95 staged as zeros
 
 // B (or A) operand of a 32x32x16 MFMA whose k runs over 16 ROWS of a row-major LDS array (rows k0.., the
 // 32 columns c0..c0+31 on the lanes): two transposed 4-row reads, the element order of the accumulator
@@ -459,15 +475,16 @@ __device__ __forceinline__ bf16x8 attn_tr_frag(const bf16* arr, int k0, int c0, 
   return *reinterpret_cast<bf16x8*>(&v);
 }
 
-// rows [0, Tpad) of two head slices (row-major, 16-B chunks, zero past Tn) -> A0 / A1 (stride LDR)
+// rows [0, Tpad) of two head slices (row-major, 16-B chunks, zero past Tn and in the columns DH..DHP-1 that
+// pad the head dim to whole 32-wide tiles) -> A0 / A1 (stride LDR)
 template <int DH, int LDR>
 __device__ __forceinline__ void attn_stage2(bf16* A0, const bf16* g0, int ld0, bf16* A1, const bf16* g1, int ld1,
                                             int Tn, int Tpad, int tid, int nthr) {
-  constexpr int CPR = DH / 8;
+  constexpr int CPR = (DH + 31) / 32 * 32 / 8;
   for (int i = tid; i < Tpad * CPR; i += nthr) {
     const int r = i / CPR, c = i - r * CPR;
     uint4 x = uint4{0, 0, 0, 0}, y = x;
-    if (r < Tn) {
+    if (r < Tn && 8 * c < DH) {
       x = *reinterpret_cast<const uint4*>(g0 + (size_t)r * ld0 + c * 8);
       y = *reinterpret_cast<const uint4*>(g1 + (size_t)r * ld1 + c * 8);
     }
@@ -481,12 +498,13 @@ __device__ __forceinline__ void attn_stage2(bf16* A0, const bf16* g0, int ld0, b
 // from global; phase 2 re-stages K and V (all keys) and reads this wave's 32 queries of Q / dO from global.
 // The transposed operands (dO^T, Q^T, K^T) are ds_read_b64_tr_b16 reads of the same row-major arrays.
 template <int DH>
-__global__ void __launch_bounds__(DH == 64 ? 512 : 1024)  // dh 64: <= 256 keys, 256 VGPRs (no spills)
+__global__ void __launch_bounds__(DH == 32 ? 1024 : 512)  // dh 64 / 80: <= 256 keys, 256 VGPRs
 mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
                     const float* __restrict__ lse, bf16* __restrict__ dqkv, int Tn, int H, int Tpad, float scale) {
   constexpr int LDR = AttnBwd<DH>::LDR;
-  constexpr int NDT = DH / 32;
+  constexpr int NDT = (DH + 31) / 32;  // output tiles; columns >= DH of the last one are zero, never stored
   constexpr int CPR = DH / 8;
+  static_assert(DH % 16 == 0, "head dim must be a multiple of 16");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   bf16* A0 = reinterpret_cast<bf16*>(smem);
   bf16* A1 = A0 + (size_t)Tpad * LDR;
@@ -578,7 +596,7 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (key < Tn) {
+        if (key < Tn && 32 * t + col < DH) {
           bf16* row = dqkv + ((size_t)b * Tn + key) * ld + h * DH + 32 * t + col;
           row[D] = (bf16)dK[t][r];
           row[2 * D] = (bf16)dV[t][r];
@@ -639,7 +657,7 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int q = qb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (q < Tn) dqkv[((size_t)b * Tn + q) * ld + h * DH + 32 * t + col] = (bf16)dQ[t][r];
+        if (q < Tn && 32 * t + col < DH) dqkv[((size_t)b * Tn + q) * ld + h * DH + 32 * t + col] = (bf16)dQ[t][r];
       }
   }
 }
@@ -647,10 +665,10 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
 // f32 (parity) form: same two phases on v_mfma_f32_32x32x2_f32, operands read straight from global memory
 // (L2-resident per head); exact f32 products.
 template <int DH>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(DH == 80 ? 512 : 1024)
 mha_bwd_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ o, const float* __restrict__ dout,
                    const float* __restrict__ lse, float* __restrict__ dqkv, int Tn, int H, int Tpad, float scale) {
-  constexpr int NDT = DH / 32;
+  constexpr int NDT = (DH + 31) / 32;  // columns >= DH of the last tile read as zero, never stored
   __shared__ float lse_s[1024], dl_s[1024];
   const int bh = xcd_remap(blockIdx.x, gridDim.x), b = bh / H, h = bh - b * H;
   const int D = H * DH, ld = 3 * D;
@@ -675,7 +693,7 @@ mha_bwd_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ o, c
   const float c2 = scale * 1.4426950408889634f;
   if (wave >= nw) return;
   auto ld_row = [&](const float* m, int row, int stride, int k) -> float {
-    return row < Tn ? m[(size_t)row * stride + k] : 0.0f;
+    return row < Tn && k < DH ? m[(size_t)row * stride + k] : 0.0f;
   };
   {  // phase 1
     const int kb = 32 * wave;
@@ -717,7 +735,7 @@ mha_bwd_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ o, c
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (key < Tn) {
+        if (key < Tn && 32 * t + col < DH) {
           float* row = dqkv + ((size_t)b * Tn + key) * ld + h * DH + 32 * t + col;
           row[D] = dK[t][r];
           row[2 * D] = dV[t][r];
@@ -761,7 +779,7 @@ mha_bwd_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ o, c
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int q = qb + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (q < Tn) dqkv[((size_t)b * Tn + q) * ld + h * DH + 32 * t + col] = dQ[t][r];
+        if (q < Tn && 32 * t + col < DH) dqkv[((size_t)b * Tn + q) * ld + h * DH + 32 * t + col] = dQ[t][r];
       }
   }
 }
@@ -774,12 +792,13 @@ static int mha_bwd_launch(const void* qkv, const void* o, const void* dout, cons
   TMAE_REQUIRE(nthr <= 1024, "tmae_mha_bwd: sequence length %d too long", Tn);
   if (B * H == 0 || Tn == 0) return TMAE_OK;
   if (dtype == TMAE_BF16) {
-    TMAE_REQUIRE(DH != 64 || nthr <= 512, "tmae_mha_bwd: sequence length %d too long for head dim 64", Tn);
+    TMAE_REQUIRE(DH == 32 || nthr <= 512, "tmae_mha_bwd: sequence length %d too long for head dim %d", Tn, DH);
     const size_t lds = (size_t)2 * Tpad * AttnBwd<DH>::LDR * 2 + (size_t)2 * Tpad * 4;
     TMAE_REQUIRE(lds <= 160 * 1024, "tmae_mha_bwd: sequence length %d needs %zu B of LDS", Tn, lds);
     hipLaunchKernelGGL((mha_bwd_bf16_kernel<DH>), dim3(B * H), dim3(nthr), lds, st, (const bf16*)qkv, (const bf16*)o,
                        (const bf16*)dout, lse, (bf16*)dqkv, Tn, H, Tpad, scale);
   } else {
+    TMAE_REQUIRE(DH != 80 || nthr <= 512, "tmae_mha_bwd: sequence length %d too long for head dim 80", Tn);
     hipLaunchKernelGGL((mha_bwd_f32_kernel<DH>), dim3(B * H), dim3(nthr), 0, st, (const float*)qkv, (const float*)o,
                        (const float*)dout, lse, (float*)dqkv, Tn, H, Tpad, scale);
   }
@@ -788,9 +807,10 @@ static int mha_bwd_launch(const void* qkv, const void* o, const void* dout, cons
 
 extern "C" int tmae_mha_bwd(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv, int B,
                             int T, int H, int dh, float scale, int dtype, void* stream) {
-  TMAE_REQUIRE(dh == 32 || dh == 64, "tmae_mha_bwd: head dim %d unsupported (32 or 64)", dh);
+  TMAE_REQUIRE(dh == 32 || dh == 64 || dh == 80, "tmae_mha_bwd: head dim %d unsupported (32, 64 or 80)", dh);
   TMAE_REQUIRE(qkv && o && dout && lse && dqkv, "tmae_mha_bwd: null argument");
   hipStream_t st = (hipStream_t)stream;
+  if (dh == 80) return mha_bwd_launch<80>(qkv, o, dout, lse, dqkv, B, T, H, scale, dtype, st);
   return dh == 64 ? mha_bwd_launch<64>(qkv, o, dout, lse, dqkv, B, T, H, scale, dtype, st)
                   : mha_bwd_launch<32>(qkv, o, dout, lse, dqkv, B, T, H, scale, dtype, st);
 }

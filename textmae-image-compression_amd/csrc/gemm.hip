@@ -289,10 +289,11 @@ static int patch_t(const float* imgs, const int64_t* ids, const void* w, const f
   const int G = W / P;
   TMAE_REQUIRE(H == W && H % P == 0 && G * G == L, "tmae_patch_embed_fwd: image %dx%d, patch %d, L=%d mismatch", H,
                W, P, L);
-  TMAE_REQUIRE(P % Elt<T>::EPC == 0 && D % 4 == 0, "tmae_patch_embed_fwd: patch %d / dim %d unsupported", P, D);
-  const int K = C * P * P;
+  TMAE_REQUIRE(P > 0 && D % 4 == 0, "tmae_patch_embed_fwd: patch %d / dim %d unsupported", P, D);
+  // weight rows hold Kw = C*P*P rounded up to a multiple of 8 (zero tail: ViT-H's 588 -> 592)
+  const int K = C * P * P, Kw = (K + 7) / 8 * 8;
   PatchSrc<T> xs{imgs, ids, L, keep, C, H, W, P, G, n * keep, K};
-  return launch_gemm<false, T>("tmae_patch_embed_fwd", (const T*)w, 0, 0, D, K, xs,
+  return launch_gemm<false, T>("tmae_patch_embed_fwd", (const T*)w, 0, 0, D, Kw, xs,
                                EpiPatchEmbed{tok, bias, pos, ids, L, keep, D}, n * keep, 1, 1, st);
 }
 

@@ -149,12 +149,27 @@ template <typename T> struct PatchSrc {
     return {img + (size_t)b * C * H * W + (size_t)(hy * P) * W + hx * P};
   }
   __device__ uint4 load(const Row& r, int kt, int c) const {
-    const int k = kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC;
+    constexpr int EPC = Elt<T>::EPC;
+    const int k = kt * 8 * EPC + c * EPC;
     if (!r.base || k >= K) return uint4{0, 0, 0, 0};
     const int pp = P * P;
-    const int ch = k / pp, rem = k - ch * pp;
-    const int py = rem / P, px = rem - py * P;
-    return load_chunk_from_f32<T>(r.base + (ch * H + py) * W + px);
+    if (P % EPC == 0) {  // a chunk is EPC pixels of one patch row
+      const int ch = k / pp, rem = k - ch * pp;
+      const int py = rem / P, px = rem - py * P;
+      return load_chunk_from_f32<T>(r.base + (ch * H + py) * W + px);
+    }
+    // patch rows that are not whole chunks (ViT-H: 14 pixels): element by element, zero past K
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int kk = k + e;
+      const int ch = kk / pp, rem = kk - ch * pp;
+      const int py = rem / P, px = rem - py * P;
+      v[e] = (e < EPC && kk < K) ? r.base[(ch * H + py) * W + px] : 0.0f;
+    }
+    const f32x4 a{v[0], v[1], v[2], v[3]}, b{v[4], v[5], v[6], v[7]};
+    if constexpr (sizeof(T) == 2) return pack8_bf16(a, b);
+    else return *reinterpret_cast<const uint4*>(&a);
   }
 };
 

@@ -109,16 +109,13 @@ class MaskedAutoencoderViT(nn.Module):
                 "training-mode autograd is not available in this build: run forward under torch.no_grad()")
 
     def _check_supported(self):
-        """what the kernels cover: head dims 32/64 (attention), patch rows of whole 16-B chunks (gather)"""
+        """what the kernels cover: head dims 32 / 64 / 80 (attention)"""
         bad = []
-        p = self.patch_embed.patch_size[0]
-        if p % 8:
-            bad.append(f"patch size {p} (multiple of 8 needed)")
         for name, blocks in (("encoder", self.blocks), ("decoder", self.decoder_blocks)):
             for b in blocks[:1]:
                 dh = b.attn.qkv.in_features // b.attn.num_heads
-                if dh not in (32, 64):
-                    bad.append(f"{name} head dim {dh} (32 or 64 supported)")
+                if dh not in (32, 64, 80):
+                    bad.append(f"{name} head dim {dh} (32, 64 or 80 supported)")
         if bad:
             raise ValueError("MaskedAutoencoderViT configuration not supported by the MI355X kernels: " + "; ".join(bad))
 
@@ -214,8 +211,11 @@ class _MAEExecutor:
         m, dt = self.m, self.dtype
         cast = (lambda t: t.detach().contiguous()) if dt == torch.float32 else (
             lambda t: t.detach().to(dt).contiguous())
-        w = m.patch_embed.proj.weight
-        self.w_pe = cast(w.view(w.shape[0], -1))
+        w = m.patch_embed.proj.weight.detach()
+        w = w.reshape(w.shape[0], -1)
+        if w.shape[1] % 8:  # patch 14: rows of 588 values padded to 592 (tmae_patch_embed_fwd)
+            w = torch.nn.functional.pad(w, (0, 8 - w.shape[1] % 8))
+        self.w_pe = cast(w)
         self.enc_w = [BlockWeights.from_block(b, dt) for b in m.blocks]
         self.dec_w = [BlockWeights.from_block(b, dt) for b in m.decoder_blocks]
         self.w_de = cast(m.decoder_embed.weight)
@@ -278,7 +278,7 @@ def mae_vit_large_patch16_dec512d8b(**kwargs):
 
 
 def mae_vit_huge_patch14_dec512d8b(**kwargs):
-    """models_mae.py:239-244 (patch 14 / head dim 80 are outside the kernels today: forward raises ValueError)"""
+    """models_mae.py:239-244 (patch 14: per-value patch gather; head dim 80: attention tiles padded to 96)"""
     return MaskedAutoencoderViT(patch_size=14, embed_dim=1280, depth=32, num_heads=16, decoder_embed_dim=512,
                                 decoder_depth=8, decoder_num_heads=16, mlp_ratio=4,
                                 norm_layer=partial(nn.LayerNorm, eps=1e-6), **kwargs)

@@ -116,6 +116,8 @@ def patch_embed(imgs, ids_shuffle, w, b, pos, tokens, keep, patch, dtype):
     n, C, H, W = imgs.shape
     D = w.shape[0]
     L = ids_shuffle.shape[1]
+    if w.dim() != 2 or w.shape[1] != -(-C * patch * patch // 8) * 8 or not w.is_contiguous():
+        raise ValueError(f"patch_embed: weight {tuple(w.shape)} must be contiguous [D][C*P*P rounded up to 8]")
     _lib.call("tmae_patch_embed_fwd", _need(imgs, torch.float32, "imgs").data_ptr(), ids_shuffle.data_ptr(),
               w.data_ptr(), b.data_ptr(), pos.data_ptr(), tokens.data_ptr(), n, C, H, W, patch, D, L, keep,
               dtype_code(dtype), _stream())
