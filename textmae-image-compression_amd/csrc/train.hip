@@ -104,15 +104,50 @@ tn_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N, float* 
   if (t >= tot4) {
     const long long m = t - tot4;
     if (!bias_out || m >= M) return;
+    // split order as one add at a time; the loads of 16 (then 4) splits in flight together (a dependent load per
+    // split made these last threads the kernel's tail: ~0.3 us of latency per split)
     float s = 0.0f;
-    for (int k = 0; k < splits; ++k) s += bws[(size_t)k * M + m];
+    int k = 0;
+    for (; k + 16 <= splits; k += 16) {
+      float v[16];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) v[j] = bws[(size_t)(k + j) * M + m];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s += v[j];
+    }
+    for (; k + 4 <= splits; k += 4) {
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = bws[(size_t)(k + j) * M + m];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += v[j];
+    }
+    for (; k < splits; ++k) s += bws[(size_t)k * M + m];
     bias_out[m] = bias_accumulate ? bias_out[m] + s : s;
     return;
   }
   const long long i = 4 * t;
   const int m = (int)(i / N), n = (int)(i - (long long)m * N);
+  // the slabs are summed in split order (bitwise the same as one load and add at a time), but the loads of
+  // 16 (then 4) splits are issued together: with a few dozen splits over a small output (the LIC convs: 36 splits,
+  // ~25 blocks) one dependent load per split left the kernel latency-bound
   f32x4 s = load4f(ws + i);
-  for (int k = 1; k < splits; ++k) s += load4f(ws + (size_t)k * tot + i);
+  int k = 1;
+  for (; k + 16 <= splits; k += 16) {
+    f32x4 v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = load4f(ws + (size_t)(k + j) * tot + i);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += v[j];
+  }
+  for (; k + 4 <= splits; k += 4) {
+    f32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = load4f(ws + (size_t)(k + j) * tot + i);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += v[j];
+  }
+  for (; k < splits; ++k) s += load4f(ws + (size_t)k * tot + i);
   if (sc == 1 && (n % cp) + 4 <= cp) {  // 4 consecutive destinations (dense layouts, and a conv's channel run)
     float* d = out + base + m * sm + (long long)(n % cp) + (long long)(n / cp) * st;
     if (accumulate) {
