@@ -415,6 +415,7 @@ def train_bench(model, args, rank, world, dev, barrier):
     t0 = time.perf_counter()
     for _ in range(args.train_steps):
         out = step()
+    host = time.perf_counter() - t0  # the host's enqueue time: close to the wall time = launch-bound
     torch.cuda.synchronize()
     barrier()
     el = max_over_ranks(time.perf_counter() - t0, world, dev, args.backend)
@@ -422,6 +423,7 @@ def train_bench(model, args, rank, world, dev, barrier):
     fl = 3 * sum(gflop_per_image(model).values())
     return {"metric": "training images/s (fwd + bwd + clip + 2x Adam" + (", RCCL grad all-reduce" if world > 1 else "")
             + ")", "value": round(ips, 2), "unit": "images/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
+            "host_enqueue_ms_per_step": round(host / args.train_steps * 1e3, 3),
             "steps": args.train_steps, "warmup": args.train_warmup, "per_gpu_batch": args.train_batch,
             "global_batch": args.train_batch * world, "parallelism": f"dp{world}", "dtype": "bf16",
             "data": f"DIV2K-shaped: {data.images.shape[0]} seeded uint8 2040x1356 images per rank (seed 2000 + rank), "

@@ -396,9 +396,10 @@ int tmae_conv_dgrad(const tmae_conv_dgrad_args* args, int dtype, void* stream);
 /* weight re-layout: dst (contiguous [d0][d1][d2][d3], dst_dtype) = src[i0*s0 + i1*s1 + i2*s2 + i3*s3] (f32) */
 int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0, int d1, int d2, int d3, long long s0, long long s1,
                   long long s2, long long s3, void* stream);
-/* every relayout of a table in one launch: table[t] = {src, dst, dst_dtype, d1, d2, d3, s0, s1, s2, s3, total,
- * first_chunk} (int64, device memory), first_chunk = the chunks of the tensors before t (a plain or strided
- * copy: ceil(total / 8192); a 2-D transpose: 64 x 64 tiles; a per-row transpose: rows) */
+/* every relayout of a table in one launch: table[t] = {src, dst, dst_dtype | mode << 8, d1, d2, d3, s0, s1, s2, s3,
+ * total, first_chunk} (int64, device memory), first_chunk = the chunks of the tensors before t (mode 0, a plain
+ * or strided copy: ceil(total / 32768); mode 1, a 2-D transpose: 64 x 64 tiles; mode 2, a per-row transpose:
+ * rows), then nchunks more int64: the row t of every chunk (ntensors * 12 + nchunks values in all) */
 int tmae_relayout_multi(const long long* table, int ntensors, long long nchunks, void* stream);
 
 /* bias gradient: out[c] (=/+=) sum over rows r of x[(r/G)*Gs + off + r%G][c]; work >= 256*C floats */

@@ -447,16 +447,17 @@ def test_relayout_multi_dense_and_strided(T, dt):
     from textmae_amd import _lib, ops
 
     dev = "cuda"
-    srcs = [_rnd(5000, seed=1), _rnd(64, 3, 3, 40, seed=2), _rnd(8192 * 2 + 16, seed=3), _rnd(96, 130, seed=4),
-            _rnd(8192 * 2 + 7, seed=5)]
+    srcs = [_rnd(5000, seed=1), _rnd(64, 3, 3, 40, seed=2), _rnd(32768 * 2 + 8200, seed=3), _rnd(96, 130, seed=4),
+            _rnd(32768 * 2 + 7, seed=5)]
     srcs = [s.to(dev) for s in srcs]
-    big = torch.empty(8192 * 2 + 8, dtype=dt, device=dev)
+    big = torch.empty(32768 * 2 + 8, dtype=dt, device=dev)
     jobs = [  # (source, destination, dims, element strides)
         (srcs[0], torch.empty(5000, dtype=dt, device=dev), (5000,), (1,)),
         (srcs[1], torch.empty(64, 40, 3, 3, dtype=dt, device=dev), (64, 40, 3, 3), (360, 1, 120, 40)),
-        (srcs[2], torch.empty(8192 * 2 + 16, dtype=dt, device=dev), (8192 * 2 + 16,), (1,)),  # 3 chunks, ragged last
+        # 3 chunks, the last one ragged inside its second 8192-element round
+        (srcs[2], torch.empty(32768 * 2 + 8200, dtype=dt, device=dev), (32768 * 2 + 8200,), (1,)),
         (srcs[3], torch.empty(130, 96, dtype=dt, device=dev), (130, 96), (1, 130)),
-        (srcs[4], big[1:], (8192 * 2 + 7,), (1,)),   # destination 2 or 4 B past a 16-B boundary
+        (srcs[4], big[1:], (32768 * 2 + 7,), (1,)),   # destination 2 or 4 B past a 16-B boundary
     ]
     rows, chunk = [], 0
     for s, d, dims, st in jobs:
@@ -464,8 +465,9 @@ def test_relayout_multi_dense_and_strided(T, dt):
         ss = list(st) + [0] * (4 - len(st))
         total = dd[0] * dd[1] * dd[2] * dd[3]
         rows.append([s.data_ptr(), d.data_ptr(), ops.dtype_code(dt), dd[1], dd[2], dd[3], *ss, total, chunk])
-        chunk += (total + 8191) // 8192
-    tab = torch.tensor(rows, dtype=torch.int64).to(dev)
+        chunk += (total + 32767) // 32768
+    owner = [t for t, r in enumerate(rows) for _ in range((rows[t + 1][11] if t + 1 < len(rows) else chunk) - r[11])]
+    tab = torch.tensor([v for r in rows for v in r] + owner, dtype=torch.int64).to(dev)
     _lib.call("tmae_relayout_multi", tab.data_ptr(), len(rows), chunk, torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     for s, d, dims, st in jobs:

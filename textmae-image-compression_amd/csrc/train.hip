@@ -414,41 +414,26 @@ extern "C" int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0,
 }
 
 // multi-tensor form: table[t] = {src, dst, dst_dtype | mode << 8, d1, d2, d3, s0, s1, s2, s3, total, first_chunk}
-// (int64); a block finds its tensor by binary search over first_chunk (staged in LDS by one coalesced read when
-// nt <= 1024: a search over the global table was ~9 dependent global-load round trips per block, the bulk of the
-// launch for the plain casts).  One launch re-lays out every weight whose
-// version moved (the optimizer step), instead of one launch per weight and layout.  Modes (host-chosen):
-//   0  8192-element chunks: plain casts as 16-B vectors (4 x 8 elements per thread), anything else as a
-//      strided gather;
+// (int64), followed by the row t of every chunk (a block reads its row index instead of searching first_chunk).
+// One launch re-lays out every weight whose version moved (the optimizer step), instead of one launch per weight
+// and layout.  Modes (host-chosen):
+//   0  32768-element chunks: plain casts as 16-B vectors (4 rounds of 4 x 8 elements per thread), anything else
+//      as a strided gather;
 //   1  2-D transpose dst[c][r] = src[r * s3 + c] (R = d3 source rows, C = total / R): 64 x 64 LDS tiles, coalesced
 //      both ways (nn.Linear data-gradient operands W^T; the conv data-gradient layout [Cin][3][3][Cout], which is
-//      the transpose of the weight seen as [Cout][Cin * 9]);
+//      the transpose of the weight seen as [Cout][Cin * 9]); 16-B loads and 4-row (8-B bf16) stores when the
+//      source rows are 16-B aligned and R % 4 == 0 (scalar 4-B loads / 2-B stores ran at ~2 TB/s);
 //   2  per-row [A][B] -> [B][A] (conv weight [Cout][Cin][3][3] -> [Cout][3][3][Cin]: A = Cin = d3, B = 9): one row
-//      per chunk through LDS (A * B <= 8192).
+//      per chunk through LDS (A * B <= 8192); 16-B loads and 8-B bf16 stores when A % 4 == 0 and aligned.
 template <typename OT>
 __device__ __forceinline__ void relayout_store(void* dst, size_t i, float v) { reinterpret_cast<OT*>(dst)[i] = to_out<OT>(v); }
 
 __global__ void __launch_bounds__(256)
 relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
-  __shared__ float sm[8192];
-  __shared__ long long first[1024];
+  __shared__ __attribute__((aligned(16))) float sm[8192];
   const long long b = blockIdx.x;
-  int lo = 0, hi = nt - 1;
-  if (nt <= 1024) {
-    for (int t = threadIdx.x; t < nt; t += 256) first[t] = tab[12 * t + 11];
-    __syncthreads();
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (first[mid] <= b) lo = mid;
-      else hi = mid - 1;
-    }
-  } else {
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (tab[12 * mid + 11] <= b) lo = mid;
-      else hi = mid - 1;
-    }
-  }
+  // the table's per-chunk row index (after the nt rows): one load instead of a search of the rows
+  const int lo = (int)tab[12 * (long long)nt + b];
   const long long* e = tab + 12 * lo;
   const float* src = (const float*)e[0];
   void* dstp = (void*)e[1];
@@ -464,6 +449,34 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
     const unsigned ntc = (C + 63) / 64;
     const unsigned r0 = (chunk / ntc) * 64, c0 = (chunk % ntc) * 64;
     const int tx = tid & 63, ty = tid >> 6;
+    const bool vec = to_bf16 && (R & 3u) == 0 && (C & 3u) == 0 && (s3 & 3) == 0 && (((unsigned long long)src) & 15) == 0 &&
+                     (((unsigned long long)dstp) & 7) == 0;
+    if (vec) {
+      // loads: a thread reads 4 consecutive columns of rows ty4, ty4 + 16, .. (16 rows of 16 float4 per pass)
+      const int c4 = 4 * (tid & 15), ty4 = tid >> 4;
+#pragma unroll
+      for (int k = ty4; k < 64; k += 16) {
+        const unsigned r = r0 + k, c = c0 + c4;
+        f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (r < R && c < C) v = load4f(src + (size_t)r * s3 + c);  // C % 4 == 0: all 4 columns valid
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sm[k * 65 + c4 + j] = v[j];
+      }
+      __syncthreads();
+      // stores: a thread writes 4 consecutive destination columns (source rows r4..r4+3) of dst row c
+      const int r4 = 4 * (tid & 15), kc = tid >> 4;
+#pragma unroll
+      for (int k = kc; k < 64; k += 16) {
+        const unsigned c = c0 + k, r = r0 + r4;
+        if (c < C && r < R) {  // R % 4 == 0: all 4 rows valid
+          bf16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = (bf16)sm[(r4 + j) * 65 + k];
+          *reinterpret_cast<bf16x4*>((bf16*)dstp + (size_t)c * R + r) = o;
+        }
+      }
+      return;
+    }
 #pragma unroll 4
     for (int k = ty; k < 64; k += 4) {
       const unsigned r = r0 + k, c = c0 + tx;
@@ -482,6 +495,22 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
   }
   if (mode == 2) {
     const unsigned A = d3, B = d1 * d2, n = A * B, r = chunk;
+    if (to_bf16 && (A & 3u) == 0 && (s0 & 3) == 0 && (((unsigned long long)src) & 15) == 0 &&
+        (((unsigned long long)dstp) & 7) == 0) {
+      // 16-B loads into LDS; each store is 4 consecutive destination elements (a..a+3 of tap t, 8 B)
+      for (unsigned i = tid; i < n / 4; i += 256) *reinterpret_cast<f32x4*>(sm + 4 * i) = load4f(src + (size_t)r * s0 + 4 * i);
+      __syncthreads();
+      const unsigned A4 = A / 4;
+      bf16* ob = (bf16*)dstp + (size_t)r * n;
+      for (unsigned idx = tid; idx < B * A4; idx += 256) {
+        const unsigned t = idx / A4, a = 4 * (idx - t * A4);
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = (bf16)sm[(a + j) * B + t];
+        *reinterpret_cast<bf16x4*>(ob + (size_t)t * A + a) = o;
+      }
+      return;
+    }
     for (unsigned i = tid; i < n; i += 256) sm[i] = src[(size_t)r * s0 + i];
     __syncthreads();
     const size_t ob = (size_t)r * n;
@@ -492,29 +521,32 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
       }
     return;
   }
-  const unsigned base = chunk * 8192u;
-  // a plain cast (contiguous source, 16-B aligned ends): 4 x 8 elements per thread, vector loads and stores
+  const unsigned base = chunk * 32768u;
+  // a plain cast (contiguous source, 16-B aligned ends): 16 x 8 elements per thread (4 rounds of 4 x 8 in
+  // flight), vector loads and stores
   const bool dense = (d3 == 1 || s3 == 1) && (d2 == 1 || s2 == (long long)d3) && (d1 == 1 || s1 == (long long)d2 * d3) &&
                      s0 == (long long)d1 * d2 * d3 &&
                      ((((unsigned long long)src) | ((unsigned long long)e[1])) & 15) == 0;
   if (dense && (total & 7u) == 0) {
-    f32x4 lo4[4], hi4[4];
+    for (unsigned rb = base; rb < base + 32768u && rb < total; rb += 8192u) {
+      f32x4 lo4[4], hi4[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const unsigned i = base + 2048u * u + 8u * tid;
-      if (i < total) load8f(src + i, lo4[u], hi4[u]);
-    }
+      for (int u = 0; u < 4; ++u) {
+        const unsigned i = rb + 2048u * u + 8u * tid;
+        if (i < total) load8f(src + i, lo4[u], hi4[u]);
+      }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const unsigned i = base + 2048u * u + 8u * tid;
-      if (i >= total) break;
-      if (to_bf16) store8((bf16*)e[1] + i, lo4[u], hi4[u]);
-      else store8((float*)e[1] + i, lo4[u], hi4[u]);
+      for (int u = 0; u < 4; ++u) {
+        const unsigned i = rb + 2048u * u + 8u * tid;
+        if (i >= total) break;
+        if (to_bf16) store8((bf16*)e[1] + i, lo4[u], hi4[u]);
+        else store8((float*)e[1] + i, lo4[u], hi4[u]);
+      }
     }
     return;
   }
   // general strided gather: 32-bit index arithmetic (64-bit division is a long VALU sequence)
-  for (unsigned k = tid; k < 8192u; k += 256u) {
+  for (unsigned k = tid; k < 32768u; k += 256u) {
     const unsigned i = base + k;
     if (i >= total) break;
     unsigned r = i;

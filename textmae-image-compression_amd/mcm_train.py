@@ -112,7 +112,7 @@ class _Weights:
                   and st[0] == d[1] * d[2] * d[3]):  # per-row [A][B] -> [B][A]
                 mode, n = 2, d[0]
             else:
-                mode, n = 0, (total + 8191) // 8192
+                mode, n = 0, (total + 32767) // 32768
             rows.append([p.data_ptr(), dst.data_ptr(), ops.dtype_code(dst.dtype) | (mode << 8), d[1], d[2], d[3], *st,
                          total, chunk])
             ptrs.append((p.data_ptr(), dst.data_ptr()))
@@ -122,7 +122,10 @@ class _Weights:
         key = tuple(ptrs)
         if self._tab is None or self._tab[0] != key:
             dev = stale[0][1].device
-            self._tab = (key, torch.tensor(rows, dtype=torch.int64).to(dev), chunk)
+            owner = [t for t in range(len(rows)) for _ in range(rows[t + 1][11] - rows[t][11] if t + 1 < len(rows)
+                                                                else chunk - rows[t][11])]
+            flat = [v for r in rows for v in r] + owner  # the rows, then each chunk's row (tmae.h)
+            self._tab = (key, torch.tensor(flat, dtype=torch.int64).to(dev), chunk)
         _lib.call("tmae_relayout_multi", self._tab[1].data_ptr(), len(rows), self._tab[2],
                   torch.cuda.current_stream().cuda_stream)
 
