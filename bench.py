@@ -63,10 +63,21 @@ def parse():
     ap.add_argument("--train-warmup", type=int, default=3)
     ap.add_argument("--train-batch", type=int, default=64)
     ap.add_argument("--no-train", action="store_true")
+    ap.add_argument("--mae-large", action="store_true",
+                    help="add the literal BASELINE config 4 line (MAE ViT-L dec512d8b, batch 128, bf16)")
+    ap.add_argument("--no-dp-rehearsal", dest="dp_rehearsal", action="store_false",
+                    help="skip the one-rank RCCL GradSync overlap measurement at N=1")
+    ap.add_argument("--no-distortion", dest="distortion_line", action="store_false",
+                    help="skip the forward_loss (SSIM + L1 + VGG) line")
     ap.add_argument("--no-k64", dest="k64_line", action="store_false", help="skip the K=64 (config 2') line")
     ap.add_argument("--kernel-reps", type=int, default=0, help="unused (kept for older command lines)")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for a one-GPU rehearsal)")
     return ap.parse_args()
+
+
+def vitb_default(args):
+    """the BASELINE config 2 model (ViT-B encoder, K=144): the side lines run only next to it"""
+    return args.keep == 144 and args.enc_dim == 768 and args.enc_depth == 12
 
 
 def synthetic_inputs(batch, img, L, seed, device):
@@ -384,7 +395,10 @@ def _committed(name):
 def train_bench(model, args, rank, world, dev, barrier):
     """the reference training step (utils/engine.py:72-91): forward, RateDistortionLoss (SSIM + L1 +
     bpp; VGG needs a weight download), aux loss, backward (HIP reverse pass; for world > 1 the RCCL
-    gradient all-reduce runs inside it, bucketed), clip_grad_norm_(1.0), Adam, aux backward, aux Adam"""
+    gradient all-reduce runs inside it, bucketed), clip_grad_norm_(1.0), Adam, aux backward, aux Adam.
+    One rank: the whole step is one HIP graph (engine.GraphedTrainStep), replayed per batch; the crop
+    kernel runs before each replay.  More ranks: eager steps with the overlap timing of the gradient
+    all-reduce (parallel.GradSync.last_timing)."""
     from textmae_amd import engine
     from textmae_amd.data import SyntheticCropSet
     from textmae_amd.optim import configure_optimizers
@@ -394,19 +408,27 @@ def train_bench(model, args, rank, world, dev, barrier):
     model.train()
     model.distortion = "ssim+l1"
     if world > 1:
-        enable_data_parallel(model)
+        enable_data_parallel(model, timing=True)
     opt, aux_opt = configure_optimizers(model, lr=1e-4, aux_lr=1e-4, fused=True)
     crit = RateDistortionLoss(lmbda=1e-2)
     # BASELINE config 3's input: per rank, seeded DIV2K-shaped uint8 images (2040 x 1356) resident in HBM and
     # a fresh random 256^2 crop per sample per step, ToTensor + Normalize on the device (data.py); seed =
     # base + rank as training.py:109 seeds its processes
     data = SyntheticCropSet(dev, seed=2000, rank=rank, crop=args.img,
-                            patch_size=model.encoder_embed.patch_size[0]).plan(args.train_warmup + args.train_steps,
+                            patch_size=model.encoder_embed.patch_size[0]).plan(args.train_warmup + args.train_steps + 1,
                                                                                args.train_batch)
-
-    def step():
+    use_graph = world == 1 and not args.no_graph
+    if use_graph:
         imgs, scores = data.next()
-        return engine.train_step(model, crit, imgs, scores, opt, aux_opt, clip_max_norm=1.0)
+        gstep = engine.GraphedTrainStep(model, crit, opt, aux_opt, imgs, scores, clip_max_norm=1.0, warmup=1)
+
+        def step():
+            imgs, scores = data.next()
+            return gstep(imgs, scores)
+    else:
+        def step():
+            imgs, scores = data.next()
+            return engine.train_step(model, crit, imgs, scores, opt, aux_opt, clip_max_norm=1.0)
 
     for _ in range(args.train_warmup):
         out = step()
@@ -421,15 +443,56 @@ def train_bench(model, args, rank, world, dev, barrier):
     el = max_over_ranks(time.perf_counter() - t0, world, dev, args.backend)
     ips = world * args.train_batch * args.train_steps / el
     fl = 3 * sum(gflop_per_image(model).values())
-    return {"metric": "training images/s (fwd + bwd + clip + 2x Adam" + (", RCCL grad all-reduce" if world > 1 else "")
-            + ")", "value": round(ips, 2), "unit": "images/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
-            "host_enqueue_ms_per_step": round(host / args.train_steps * 1e3, 3),
-            "steps": args.train_steps, "warmup": args.train_warmup, "per_gpu_batch": args.train_batch,
-            "global_batch": args.train_batch * world, "parallelism": f"dp{world}", "dtype": "bf16",
-            "data": f"DIV2K-shaped: {data.images.shape[0]} seeded uint8 2040x1356 images per rank (seed 2000 + rank), "
-                    f"a random {args.img}^2 crop per sample per step, normalised on the device",
-            "loss_last": round(float(out["loss"].detach()), 6), "gflop_per_image": round(fl, 2),
-            "step_mfma_frac": round(ips * fl * 1e9 / (world * PEAK_BF16), 4), "hip_graph": False}
+    rec = {"metric": "training images/s (fwd + bwd + clip + 2x Adam" + (", RCCL grad all-reduce" if world > 1 else "")
+           + ")", "value": round(ips, 2), "unit": "images/s", "ms_per_step": round(el / args.train_steps * 1e3, 3),
+           "host_enqueue_ms_per_step": round(host / args.train_steps * 1e3, 3),
+           "steps": args.train_steps, "warmup": args.train_warmup, "per_gpu_batch": args.train_batch,
+           "global_batch": args.train_batch * world, "parallelism": f"dp{world}", "dtype": "bf16",
+           "data": f"DIV2K-shaped: {data.images.shape[0]} seeded uint8 2040x1356 images per rank (seed 2000 + rank), "
+                   f"a random {args.img}^2 crop per sample per step, normalised on the device",
+           "loss_last": round(float(out["loss"].detach()), 6), "gflop_per_image": round(fl, 2),
+           "step_mfma_frac": round(ips * fl * 1e9 / (world * PEAK_BF16), 4), "hip_graph": use_graph}
+    if use_graph:
+        del gstep
+        torch.cuda.empty_cache()
+    if world > 1:
+        t = model.grad_sync.last_timing()
+        if t:
+            rec["grad_allreduce"] = dict(t, source="last timed step, this rank's compute-stream events")
+    elif args.dp_rehearsal:
+        rec["grad_allreduce"] = dp_rehearsal(model, crit, opt, aux_opt, data, dev)
+    return rec
+
+
+def dp_rehearsal(model, crit, opt, aux_opt, data, dev, steps=3):
+    """the data-parallel step's overlap numbers at N = 1: an RCCL process group of ONE rank
+    with GradSync's world-of-1 short-circuit bypassed, so the bucketed async AVG all-reduces really go through
+    RCCL from inside the backward; a few eager steps, then the last one's events.  A one-rank all-reduce moves
+    no bytes over xGMI: this measures the issue / overlap structure, not link time."""
+    import torch.distributed as dist
+
+    from textmae_amd import engine
+    from textmae_amd.parallel import enable_data_parallel
+
+    own = not dist.is_initialized()
+    try:
+        if own:
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                    device_id=dev)
+        sync = enable_data_parallel(model, always_collective=True, timing=True)
+        for _ in range(steps):
+            imgs, scores = data.next()
+            engine.train_step(model, crit, imgs, scores, opt, aux_opt, clip_max_norm=1.0)
+        torch.cuda.synchronize()
+        t = sync.last_timing()
+        return dict(t or {}, launched_total=sync.launched, world=1,
+                    source="one-rank nccl (RCCL) group, always_collective, last of 3 eager steps")
+    except Exception as e:  # the rehearsal must never cost the bench line
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+    finally:
+        model.grad_sync = None
+        if own and dist.is_initialized():
+            dist.destroy_process_group()
 
 
 def _cpu_model():
@@ -477,7 +540,9 @@ def _cpu_share():
 def cpu_baseline(args, model_kwargs):
     """the oracle (CPU restatement of MCM.forward, fp32) on the host cores over a bounded
     sample of the same workload (batches of 8), timed per batch and reported at the median:
-      * at torch.set_num_threads(os.cpu_count()) -- §8(d)'s setting;
+      * at the thread count of the cgroup's CPU share (cpu.max; os.cpu_count() when there is no quota:
+        §8(d)'s setting -- on the box os.cpu_count() is 256 against a 16-CPU share, and 256 threads never
+        finish a batch);
       * at the thread count the process is given (OMP_NUM_THREADS; the box's CPU share);
       * at 1 thread, the reference eval convention (testing.py:29).
     Each leg runs in its own child process (no GPU use there) under a time limit, so a leg that
@@ -492,8 +557,18 @@ def cpu_baseline(args, model_kwargs):
     nb = args.cpu_batch
     default_threads = torch.get_num_threads()
     legs = {}
-    plan = [("all_host_cpus", os.cpu_count() or default_threads, args.cpu_seconds, 1000),
-            ("process_threads", default_threads, args.cpu_seconds, 1000), ("one_thread", 1, 0.0, 1)]
+    # the box gives this process a cgroup CPU share (cpu.max) far below os.cpu_count(): a leg with one thread per
+    # host CPU oversubscribes the share ~16x and never finishes a batch, so it is sized to the share instead
+    host = os.cpu_count() or default_threads
+    share = _cpu_share()
+    share_threads = max(1, min(host, int(share + 0.5))) if share else host
+    plan = [("cgroup_share", share_threads, args.cpu_seconds, 1000)]
+    if default_threads != share_threads:
+        plan.append(("process_threads", default_threads, args.cpu_seconds, 1000))
+    plan.append(("one_thread", 1, 0.0, 1))
+    if share_threads < host:
+        legs["all_host_cpus"] = {"threads": host, "skipped": f"cgroup cpu.max share is {share} CPUs; "
+                                                             f"{host} threads would oversubscribe it"}
     for name, threads, secs, maxb in plan:
         env = dict(os.environ, OMP_NUM_THREADS=str(threads))
         cmd = [sys.executable, os.path.abspath(__file__), "--cpu-leg", json.dumps([threads, secs, maxb, nb, model_kwargs])]
@@ -506,7 +581,7 @@ def cpu_baseline(args, model_kwargs):
                                                                                    "error": r.stderr[-300:]}
         except subprocess.TimeoutExpired:
             legs[name] = {"threads": threads, "error": f"no batch of {nb} finished within {limit:.0f} s"}
-    ok = [k for k in ("all_host_cpus", "process_threads") if "images_per_s_median" in legs.get(k, {})]
+    ok = [k for k in ("cgroup_share", "process_threads") if "images_per_s_median" in legs.get(k, {})]
     best = max(ok, key=lambda k: legs[k]["images_per_s_median"]) if ok else None
     L = (model_kwargs["img_size"] // 16) ** 2
     s64 = torch.rand(64, L, generator=torch.Generator().manual_seed(5)).numpy().astype(np.float32)
@@ -525,7 +600,7 @@ def cpu_baseline(args, model_kwargs):
             "sample": f"oracle MCM.forward (fp32 torch CPU restatement) on batches of {nb} at "
                       f"{model_kwargs['img_size']}^2, K={model_kwargs['num_keep_patches']}, timed per batch, median; "
                       f"~{args.cpu_seconds:.0f} s per multi-thread leg, one batch at 1 thread; value = the faster of "
-                      f"os.cpu_count() threads and the process's threads",
+                      f"the cgroup CPU share's threads and the process's threads",
             "legs": legs, "value_1thread": legs["one_thread"].get("images_per_s_median"), "cpu_model": _cpu_model(),
             "host_cpus": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_share": _cpu_share(),
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
@@ -599,6 +674,114 @@ def k64_line(args, dev, world, rank, barrier, dtype):
     return {"workload": "MCM forward eval, ViT-B/16, K=64 of 256 patches (g=8)", "value": round(v, 2),
             "unit": "images/s", "ms_per_step": round(el / args.steps * 1e3, 3), "ms_per_step_median": round(med, 3),
             "gflop_per_image": round(gf, 3), "step_mfma_frac": round(v * gf * 1e9 / (world * PEAK_BF16), 4)}
+
+
+def seeded_vgg16_features(seed=0):
+    """VGG16 features[0:16] conv weights of torchvision's layout, seeded (kaiming-normal, zero bias): the
+    pretrained ones need a download (loss/vgg.py:14), so the timing line runs the same architecture on
+    random-init weights, as every other line here does"""
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for i, (ci, co) in zip((0, 2, 5, 7, 10, 12, 14), ((3, 64), (64, 64), (64, 128), (128, 128), (128, 256),
+                                                    (256, 256), (256, 256))):
+        sd[f"features.{i}.weight"] = torch.randn(co, ci, 3, 3, generator=g) * (2.0 / (9 * ci)) ** 0.5
+        sd[f"features.{i}.bias"] = torch.zeros(co)
+    return sd
+
+
+def distortion_line(model, imgs, scores, args, world, dev, barrier):
+    """MCM.forward_loss (MCM.py:690-712: 1 - SSIM, L1, VGG16 relu2_2 / relu3_3 feature loss)
+    timed on its own, apart from the encode + rate + decode metric: one forward gives x_hat, then exactly
+    `steps` replays of a HIP graph of forward_loss(imgs, x_hat) at the bench batch (eval, no_grad)"""
+    model.load_vgg16(seeded_vgg16_features(0))
+    with torch.no_grad():
+        x_hat = model(imgs, scores)["x_hat"].clone()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                model.forward_loss(imgs, x_hat)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = model.forward_loss(imgs, x_hat)
+        for _ in range(args.warmup):
+            graph.replay()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            graph.replay()
+        torch.cuda.synchronize()
+        barrier()
+        el = max_over_ranks(time.perf_counter() - t0, world, dev, args.backend)
+        vals = [round(float(v), 6) for v in out]
+    del graph
+    model.__dict__["_vgg_sd"] = None
+    model.__dict__["_vgg"] = None
+    B, H = imgs.shape[0], imgs.shape[-1]
+    # VGG16 features[0:16] FLOPs for prediction and target (2 MAC per tap)
+    vgg = 0
+    hw = H * H
+    for ci, co, pool_before in ((3, 64, 0), (64, 64, 0), (64, 128, 1), (128, 128, 0), (128, 256, 1), (256, 256, 0),
+                                (256, 256, 0)):
+        hw //= 4 if pool_before else 1
+        vgg += 2 * hw * co * ci * 9
+    gf = 2 * vgg / 1e9
+    v = world * B * args.steps / el
+    return {"workload": "MCM.forward_loss: 1 - SSIM (11x11 Gaussian, 3 channels) + L1 + VGG16 features[0:16] "
+                        "feature MSE on prediction and target (seeded VGG weights), eval, HIP graph",
+            "value": round(v, 2), "unit": "images/s", "ms_per_step": round(el / args.steps * 1e3, 3),
+            "batch": B, "gflop_per_image": round(gf, 3), "step_mfma_frac": round(v * gf * 1e9 / (world * PEAK_BF16), 4),
+            "losses": {"ssim_loss": vals[0], "L1_loss": vals[1], "vgg_loss": vals[2]}}
+
+
+def mae_large_line(args, dev, world, rank, barrier, dtype):
+    """BASELINE config 4 as written: MAE ViT-Large (mae_vit_large_patch16_dec512d8b, models_mae.py:231-236:
+    1024/24/16 encoder, decoder 512/8/16), batch 128, 224^2, mask_ratio 0.75, forward (masking, encoder on the 49
+    kept patches, decoder, masked MSE loss) replayed as a HIP graph; seeded random-init weights"""
+    import textmae_amd
+
+    torch.manual_seed(0)
+    m = textmae_amd.mae_vit_large_patch16_dec512d8b().to(dev).eval()
+    m.compute_dtype = dtype
+    B = 128
+    imgs = torch.randn(B, 3, 224, 224, generator=torch.Generator().manual_seed(2000 + rank)).to(dev)
+    with torch.no_grad():
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                m(imgs, 0.75)
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            m(imgs, 0.75)
+        for _ in range(args.warmup):
+            graph.replay()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            graph.replay()
+        torch.cuda.synchronize()
+        barrier()
+        el = max_over_ranks(time.perf_counter() - t0, world, dev, args.backend)
+    del graph
+    L, keep, E, Dd = 196, 49, 1024, 512
+    fl = 2 * keep * E * 768  # patch embed of the kept patches
+    fl += 24 * (2 * (keep + 1) * E * 12 * E + 4 * (keep + 1) ** 2 * E)
+    fl += 2 * (keep + 1) * E * Dd
+    fl += 8 * (2 * (L + 1) * Dd * 12 * Dd + 4 * (L + 1) ** 2 * Dd)
+    fl += 2 * L * Dd * 768
+    gf = fl / 1e9
+    v = world * B * args.steps / el
+    del m
+    torch.cuda.empty_cache()
+    return {"workload": "BASELINE config 4: MAE ViT-Large/16 dec512d8b forward (mask 0.75, loss), 224^2, HIP graph",
+            "value": round(v, 2), "unit": "images/s", "batch": B, "ms_per_step": round(el / args.steps * 1e3, 3),
+            "dtype": "bf16" if dtype == torch.bfloat16 else "f32", "gflop_per_image": round(gf, 3),
+            "step_mfma_frac": round(v * gf * 1e9 / (world * PEAK_BF16), 4)}
 
 
 def max_over_ranks(el, world, dev, backend):
@@ -686,9 +869,19 @@ def main():
         roof = roofline_report(model, imgs, scores, args.batch, dump=args.dump_launches)
 
     k64 = None
-    if args.k64_line and args.keep == 144 and args.enc_dim == 768 and args.enc_depth == 12:
+    if args.k64_line and vitb_default(args):
         progress("config 2' (K=64) line")
         k64 = k64_line(args, dev, world, rank, barrier, dtype)
+
+    mae_l = None
+    if args.mae_large:
+        progress("config 4 (MAE ViT-L, batch 128) line")
+        mae_l = mae_large_line(args, dev, world, rank, barrier, dtype)
+
+    dist_line = None
+    if args.distortion_line and vitb_default(args):
+        progress("forward_loss line")
+        dist_line = distortion_line(model, imgs, scores, args, world, dev, barrier)
 
     train = None
     if not args.no_train and args.train_steps > 0:
@@ -717,6 +910,10 @@ def main():
     }
     if k64 is not None:
         rec["config2_k64"] = k64
+    if dist_line is not None:
+        rec["forward_loss"] = dist_line
+    if mae_l is not None:
+        rec["config4_mae_large"] = mae_l
     if train is not None:
         rec["train"] = train
     if rank == 0:

@@ -112,6 +112,41 @@ def test_vitl_vs_oracle_and_split_api(tmae):
         m(imgs.to(DEV))  # parameters require grad and grad mode is on: no backward kernels in this build
 
 
+def test_vitl_literal_config4_batch128_bf16_graph(tmae):
+    """BASELINE config 4 as written: mae_vit_large_patch16_dec512d8b (models_mae.py:231-236), batch 128, bf16,
+    forward replayed as a HIP graph (bench.py --mae-large).  Masks are bit-exact for every image; images 0, 64
+    and 127 against the f32 oracle within the bf16 bound (relative L2 of pred); the graph replay equals the
+    eager forward bitwise."""
+    torch.manual_seed(11)
+    m = tmae.mae_vit_large_patch16_dec512d8b().to(DEV).eval()
+    m.compute_dtype = torch.bfloat16
+    imgs = torch.randn(128, 3, 224, 224, generator=torch.Generator().manual_seed(12))
+    noise = torch.rand(128, 196, generator=torch.Generator().manual_seed(13))
+    x, nz = imgs.to(DEV), noise.to(DEV)
+    with torch.no_grad():
+        eager = m(x, 0.75, noise=nz)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            m(x, 0.75, noise=nz)
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = m(x, 0.75, noise=nz)
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out[1], eager[1]) and torch.equal(out[2], eager[2])
+    pick = [0, 64, 127]
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    with torch.no_grad():
+        rl, rp, rm = mae_forward(sd, imgs[pick], noise[pick], 0.75, 16, 16, 16, 24, 8)
+    assert torch.equal(out[2][pick].cpu(), rm)
+    pr = out[1][pick].double().cpu()
+    per = [float((pr[i] - rp[i].double()).norm() / rp[i].double().norm()) for i in range(3)]
+    check("pred_relL2_max_bf16_mae_large_b128", max(per), 1.5e-2)
+
+
 def test_huge_patch14_vs_oracle(tmae):
     """ViT-H factory (models_mae.py:239-244): patch 14 (588-value patch rows, per-value gather), 32 x 1280,
     16 heads of dim 80 (attention tiles padded to 96), dec512d8b; f32 against the oracle at batch 1"""

@@ -349,7 +349,7 @@ def _nccl_w1_worker(port, geom, q):
         for mode in ("plain", "rccl"):
             m, cfg = make()
             sync = enable_data_parallel(m, bucket_mb=8.0 if geom == "vitb" else 0.05,
-                                        always_collective=True) if mode == "rccl" else None
+                                        always_collective=True, timing=True) if mode == "rccl" else None
             opt, aux = configure_optimizers(m, lr=1e-3, aux_lr=1e-3, fused=True)
             batches = [_inputs(cfg, 2, 500 + i) for i in range(2)]
             losses = _train_steps(m, opt, aux, batches, crit)
@@ -361,6 +361,8 @@ def _nccl_w1_worker(port, geom, q):
             g = torch.cat([p.grad.reshape(-1).cpu() for p in m.parameters() if p.requires_grad])
             w = torch.cat([p.detach().reshape(-1).float().cpu() for p in m.parameters()])
             res[mode] = (losses, g.numpy(), w.numpy(), sync.launched if sync is not None else 0)
+            if sync is not None:
+                res["timing"] = sync.last_timing()
         q.put(res)
     finally:
         dist.destroy_process_group()
@@ -382,6 +384,12 @@ def test_rccl_grad_sync_one_rank_bitwise(geom):
     assert p.exitcode == 0
     (l0, g0, w0, _), (l1, g1, w1, launched) = res["plain"], res["rccl"]
     assert launched > 10, launched  # three backwards' worth of buckets really went through RCCL
+    # the overlap is real: most buckets leave from inside the backward (ready() hand-offs), and the first one's
+    # launch point on the compute stream precedes the backward's end
+    t = res["timing"]
+    assert t["buckets_issued_in_backward"] >= t["buckets"] // 2, t
+    assert t["allreduce_issue_ms"] is not None and t["allreduce_issue_ms"] > 0, t
+    assert t["allreduce_exposed_ms"] >= 0, t
     assert l0 == l1
     assert np.array_equal(g0, g1)
     assert np.array_equal(w0, w1)
@@ -405,13 +413,91 @@ def test_bench_spawns_ranks_without_launcher():
     assert rec["n_gpus"] == 2 and rec["train"]["global_batch"] == 4
 
 
-def test_fused_adam_rejects_partial_gradients():
-    """one step count per group (optim.FusedAdam): a group in which only some parameters got a gradient
-    would get torch's per-parameter bias correction wrong, so it raises instead"""
+def test_fused_adam_partial_gradients_match_torch():
+    """per-parameter step counts (torch.optim.Adam's state[p]["step"]): a parameter without a gradient at some
+    step is skipped and keeps its count, so the bias corrections of the two parameters diverge exactly as in
+    torch's loop; the state_dict carries the per-parameter counts"""
     from textmae_amd.optim import FusedAdam
 
-    a, b = torch.nn.Parameter(torch.ones(4, device="cuda")), torch.nn.Parameter(torch.ones(4, device="cuda"))
-    opt = FusedAdam([a, b], lr=1e-3)
-    a.grad = torch.ones(4, device="cuda")
-    with pytest.raises(ValueError, match="every trainable parameter"):
-        opt.step()
+    torch.manual_seed(3)
+    init = [torch.randn(1000, device="cuda"), torch.randn(37, device="cuda")]
+    grads = [[torch.randn(1000, device="cuda"), torch.randn(37, device="cuda")] for _ in range(4)]
+    mask = [(1, 1), (1, 0), (1, 0), (0, 1)]  # which parameter has a gradient at each step
+    runs = []
+    for cls in (FusedAdam, torch.optim.Adam):
+        ps = [torch.nn.Parameter(t.clone()) for t in init]
+        kw = dict(foreach=False) if cls is torch.optim.Adam else {}
+        opt = cls(ps, lr=1e-2, weight_decay=0.01, **kw)
+        for g, mk in zip(grads, mask):
+            for p, gi, on in zip(ps, g, mk):
+                p.grad = gi.clone() if on else None
+            opt.step()
+        runs.append((ps, opt.state_dict()))
+    (pa, sa), (pb, sb) = runs
+    for a, b in zip(pa, pb):
+        assert torch.allclose(a, b, rtol=1e-6, atol=1e-7), float((a - b).abs().max())
+    assert [float(sa["state"][i]["step"]) for i in (0, 1)] == [3.0, 2.0]
+    assert [float(sb["state"][i]["step"]) for i in (0, 1)] == [3.0, 2.0]
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_graphed_train_step_bitwise(dt):
+    """engine.GraphedTrainStep: the whole training step (forward, RateDistortionLoss, aux loss, HIP backward,
+    clip_grad_norm_, both FusedAdam steps, zero_grad) captured once as a HIP graph and replayed per batch gives
+    losses and post-step weights bitwise equal to eager engine.train_step on the same batches and noise; an
+    eager forward after the replays sees the replayed weights (version counters advanced)"""
+    from textmae_amd import engine
+    from textmae_amd.optim import configure_optimizers
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    crit = RateDistortionLoss(lmbda=1e-2)
+    m1, cfg = _model(SMALL, 23, dt)
+    m2, _ = _model(SMALL, 23, dt)
+    m1.distortion = m2.distortion = "ssim+l1"
+    batches = [_inputs(cfg, 2, 300 + i) for i in range(4)]
+    o1 = configure_optimizers(m1, lr=3e-3, aux_lr=1e-3, fused=True)
+    o2 = configure_optimizers(m2, lr=3e-3, aux_lr=1e-3, fused=True)
+    cu = lambda b: tuple(t.cuda() for t in b)  # noqa: E731
+    imgs, scores, zn, yn = cu(batches[0])
+    # construction = one eager warm-up step on batch 0, then the capture
+    g = engine.GraphedTrainStep(m1, crit, *o1, imgs, scores, clip_max_norm=1.0, warmup=1, noise=(zn, yn))
+    la = []
+    for b in batches[1:]:
+        imgs, scores, zn, yn = cu(b)
+        out = g(imgs, scores, noise=(zn, yn))
+        la.append(float(out["loss"]))
+    lb = _train_steps(m2, *o2, batches, crit)[1:]
+    assert la == lb, (la, lb)
+    for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(p, q), n
+    m1.eval()
+    m2.eval()
+    imgs, scores, _, _ = cu(batches[0])
+    with torch.no_grad():
+        assert torch.equal(m1(imgs, scores)["x_hat"], m2(imgs, scores)["x_hat"])
+
+
+def test_graphed_train_step_device_noise_and_lr_change():
+    """without injected noise the graph draws training noise from torch's graph-safe generator (a fresh draw
+    per replay); changing the learning rate re-captures the step"""
+    from textmae_amd import engine
+    from textmae_amd.optim import configure_optimizers
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    crit = RateDistortionLoss(lmbda=1e-2)
+    m, cfg = _model(SMALL, 24, torch.bfloat16)
+    m.distortion = "ssim+l1"
+    opt, aux = configure_optimizers(m, lr=1e-3, aux_lr=1e-3, fused=True)
+    imgs, scores, _, _ = (t.cuda() for t in _inputs(cfg, 2, 400))
+    g = engine.GraphedTrainStep(m, crit, opt, aux, imgs, scores)
+    bpp = []
+    for _ in range(3):
+        bpp.append(float(g(imgs, scores)["bpp_loss"]))
+    first = g.graph
+    assert len(set(bpp)) == 3 and all(np.isfinite(bpp)), bpp
+    for grp in opt.param_groups:
+        grp["lr"] = 5e-4
+    g(imgs, scores)
+    assert g.graph is not first
+    st = opt.state_dict()["state"]
+    assert {float(v["step"]) for v in st.values()} == {5.0}

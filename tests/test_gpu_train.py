@@ -103,6 +103,67 @@ def test_wgrad_conv(T, stride, dt):
     check("_rel:out", _rel(out, ref), (1e-5 if dt == torch.float32 else 2e-3))
 
 
+# bias gradient formed inside the weight-gradient GEMM (bf16: MFMAs against an all-ones fragment, one owner
+# wave per fragment, folded in split order by tn_reduce; f32: column sums after the GEMM).  Shapes: one and
+# many N tiles, M past the last whole M tile, more than 16 K splits (the 16 / 4-split fold), the 8-wave
+# 256 x 256 tile, grouped rows, accumulation into an existing bias.
+@pytest.mark.parametrize("K,M,N,remap", [(300, 72, 64, False), (9280, 72, 200, False), (1000, 200, 1000, False),
+                                         (9280, 768, 3072, False), (2880, 768, 200, True), (16448, 520, 136, False)])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("acc", [False, True])
+def test_wgrad_bias(T, K, M, N, remap, dt, acc):
+    if dt == torch.float32 and K * M * N > 3e9:
+        pytest.skip("f32 parity path checked on the smaller shapes")
+    if remap:
+        G = 144
+        imgs = K // G
+        a_full, b_full = _rnd(imgs * (G + 1), M, seed=31), _rnd(imgs * (G + 1), N, seed=32)
+        rows = torch.tensor([(k // G) * (G + 1) + 1 + k % G for k in range(K)])
+        a, b = a_full[rows], b_full[rows]
+        kw = dict(a_remap=(G, G + 1, 1), b_remap=(G, G + 1, 1))
+        a_in, b_in = a_full, b_full
+    else:
+        a, b = _rnd(K, M, seed=33), _rnd(K, N, seed=34)
+        kw = {}
+        a_in, b_in = a, b
+    ref_w = (a.to(dt).double().t() @ b.to(dt).double()).float()
+    ref_b = a.to(dt).double().sum(0).float()
+    out = torch.full((M, N), 0.25 if acc else 0.0, device="cuda")
+    bias = torch.full((M,), 0.5 if acc else float("nan"), device="cuda")
+    T.wgrad(a_in.cuda().to(dt), b_in.cuda().to(dt), M, N, K, out, dt, accumulate=acc, bias=bias, bias_accumulate=acc,
+            **kw)
+    torch.cuda.synchronize()
+    off = 0.25 if acc else 0.0
+    boff = 0.5 if acc else 0.0
+    tol = 1e-5 if dt == torch.float32 else 2e-3
+    check("_rel:w", _rel(out - off, ref_w), tol)
+    # per element (a wrong fragment owner or split fold shows up as whole wrong columns, not as aggregate noise)
+    db = (bias.cpu().double() - boff - ref_b.double()).abs()
+    scale = a.to(dt).double().abs().sum(0)
+    worst = float((db / scale.clamp_min(1e-30)).max())
+    check("_rel:bias_per_elem", worst, 1e-6 if dt == torch.float32 else 1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_wgrad_conv_bias(T, dt):
+    # the conv layout with the bias column sums of dy (the conv's bias gradient)
+    n, H, cin, cout = 4, 12, 48, 40
+    x, dy = _rnd(n, cin, H, H, seed=35), _rnd(n, cout, H, H, seed=36)
+    xq, dyq = x.to(dt).float(), dy.to(dt).float()
+    ref = torch.nn.grad.conv2d_weight(xq.double(), (cout, cin, 3, 3), dyq.double(), padding=1).float()
+    ref_b = dyq.double().sum((0, 2, 3))
+    x_nhwc = xq.permute(0, 2, 3, 1).contiguous().reshape(-1, cin).cuda().to(dt)
+    dy_nhwc = dyq.permute(0, 2, 3, 1).contiguous().reshape(-1, cout).cuda().to(dt)
+    out = torch.empty(cout, cin, 3, 3, device="cuda")
+    bias = torch.empty(cout, device="cuda")
+    T.wgrad(dy_nhwc, x_nhwc, cout, 9 * cin, n * H * H, out, dt, conv=dict(c1=cin, H=H, W=H, cin=cin), layout="conv",
+            bias=bias)
+    torch.cuda.synchronize()
+    check("_rel:w", _rel(out, ref), 1e-5 if dt == torch.float32 else 2e-3)
+    db = (bias.cpu().double() - ref_b).abs() / dyq.double().abs().sum((0, 2, 3))
+    check("_rel:bias_per_elem", float(db.max()), 1e-6 if dt == torch.float32 else 1e-5)
+
+
 def test_wgrad_conv_two_sources(T):
     # torch.cat([x1, x2], 1) without a copy, written into a channel slice of a wider weight
     n, H, c1, c2, cout = 2, 6, 16, 8, 24

@@ -179,7 +179,7 @@ SIGNATURES = {
     "tmae_decoder_embed_bwd_gather": [P, P, P, I, I, I, I, I, P, P, I, P],
     "tmae_add": [P, P, P, LL, P],
     "tmae_adam": [P, P, P, P, LL, F, F, F, F, F, I, P, P],
-    "tmae_adam_multi": [P, I, LL, F, F, F, F, F, I, P, P],
+    "tmae_adam_multi": [P, I, LL, F, F, F, F, F, P, P],
     "tmae_grad_norm": [P, LL, P, F, P, P],
     "tmae_scale": [P, LL, P, P],
     "tmae_distortion_fwd": [P, P, I, I, I, P, P, P, P, P],

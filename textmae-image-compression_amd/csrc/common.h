@@ -38,6 +38,17 @@ void tmae_set_error(int code, const char* fmt, ...);
     return TMAE_OK;                                                          \
   } while (0)
 
+// the same check between two launches of one entry point (returns only on failure)
+#define TMAE_LAUNCH_CHECK_NORET(name)                                        \
+  do {                                                                       \
+    hipError_t _e = hipGetLastError();                                       \
+    if (_e != hipSuccess) {                                                  \
+      tmae_set_error(TMAE_EHIP, "%s: launch failed: %s", name,               \
+                     hipGetErrorString(_e));                                 \
+      return TMAE_EHIP;                                                      \
+    }                                                                        \
+  } while (0)
+
 // ---------------------------------------------------------------- device helpers
 __device__ __forceinline__ float gelu_erf(float x) {
   // nn.GELU() default (approximate='none'): 0.5 * x * (1 + erf(x / sqrt(2))).

@@ -62,6 +62,15 @@ static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
   // bias column sums: in the bf16 kernel (slab [splits][M] after the partial tiles); the f32 parity path
   // runs the column-sum kernels on A after the GEMM
   float* bws = (a.bias_out && bf) ? a.work + slabs : nullptr;
+  // KDenseSrc::addr_in forms element offsets in 32-bit unsigned arithmetic: the last source row the K range
+  // reaches, times the stride, plus the columns, must stay below 2^32 elements
+  auto last_elem = [&](int G, int Gs, int off, int ld, int cols) -> unsigned long long {
+    const long long k = std::max(a.K - 1, 0);
+    const long long sk = G < a.K ? (k / G) * (long long)Gs + off + (k % G) : (long long)off + k;
+    return (unsigned long long)sk * (unsigned long long)ld + (unsigned long long)cols;
+  };
+  TMAE_REQUIRE(last_elem(a.a_G, a.a_Gs, a.a_off, a.lda, a.M) < (1ull << 32),
+               "tmae_wgrad: operand A spans 2^32 elements or more (32-bit source offsets)");
   KDenseSrc<T> as{(const T*)a.a, a.lda, a.M, a.a_G, a.a_Gs, a.a_off};
   int rc;
   if (a.b_conv) {
@@ -76,6 +85,8 @@ static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
             : launch_tn_f32(p, as, bs, a.work, a.M, a.N, a.K, st);
   } else {
     TMAE_REQUIRE(a.ldb % e == 0 && a.b_G > 0, "tmae_wgrad: ldb");
+    TMAE_REQUIRE(last_elem(a.b_G, a.b_Gs, a.b_off, a.ldb, a.N) < (1ull << 32),
+                 "tmae_wgrad: operand B spans 2^32 elements or more (32-bit source offsets)");
     KDenseSrc<T> bs{(const T*)a.b, a.ldb, a.N, a.b_G, a.b_Gs, a.b_off};
     rc = bf ? launch_tn_bf16(p, as, bs, a.work, bws, a.M, a.N, a.K, st)
             : launch_tn_f32(p, as, bs, a.work, a.M, a.N, a.K, st);
@@ -824,6 +835,7 @@ extern "C" int tmae_layernorm_bwd(const float* x, const float* gamma, const floa
   const int vpl = ceil_div(D / 4, 64);
   const dim3 grid(wgs);
   const size_t lds = (size_t)4 * np * D * sizeof(float);
+  TMAE_REQUIRE(lds <= 160 * 1024, "tmae_layernorm_bwd: D=%d needs %zu B of LDS (160 KiB per workgroup)", D, lds);
 #define TMAE_LNB(OT, V)                                                                                               \
   if (dres_colsum)                                                                                                    \
     hipLaunchKernelGGL((layernorm_bwd_kernel<OT, V, true>), grid, dim3(256), lds, st, x, gamma, dy, dres, dx32,         \
@@ -1431,25 +1443,37 @@ extern "C" int tmae_adam(float* p, const float* g, float* m, float* v, long long
   TMAE_LAUNCH_CHECK("tmae_adam");
 }
 
-// multi-tensor form: table[t] = {p, g, m, v, n, first_chunk} (int64), chunks of 1024 elements; a block
-// finds its tensor by binary search over first_chunk.  One launch updates every parameter of a group.
+// multi-tensor form: table[t] = {p, g, m, v, n, first_chunk, step} (int64; step = address of the tensor's int32
+// step count, torch.optim.Adam's per-parameter ``state["step"]``), chunks of 1024 elements; a block finds its
+// tensor by binary search over first_chunk.  One launch updates every parameter of a group.  The step counts
+// live on the device (advanced by adam_step_kernel right before), so the bias corrections need no host value
+// and a captured HIP graph replays a correct optimizer step every time.
+__global__ void adam_step_kernel(const long long* __restrict__ tab, int nt) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < nt) ++*reinterpret_cast<int*>(tab[7 * t + 6]);
+}
+
 __global__ void __launch_bounds__(256)
 adam_multi_kernel(const long long* __restrict__ tab, int nt, float lr, float b1, float b2, float eps, float wd,
-                  float bc1, float bc2_sqrt, const float* __restrict__ clip) {
+                  const float* __restrict__ clip) {
   const long long b = blockIdx.x;
   int lo = 0, hi = nt - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (tab[6 * mid + 5] <= b) lo = mid;
+    if (tab[7 * mid + 5] <= b) lo = mid;
     else hi = mid - 1;
   }
-  const long long* e = tab + 6 * lo;
+  const long long* e = tab + 7 * lo;
   float* p = (float*)e[0];
   const float* g = (const float*)e[1];
   float* m = (float*)e[2];
   float* v = (float*)e[3];
   const long long n = e[4];
   const long long base = (b - e[5]) * 1024;
+  // bias corrections in f64 from the device step, rounded to f32 as tmae_adam does on the host
+  const int step = *reinterpret_cast<const int*>(e[6]);
+  const float bc1 = (float)(1.0 - pow((double)b1, (double)step));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, (double)step));
   const float cs = clip ? clip[0] : 1.0f;
   for (int k = threadIdx.x; k < 1024; k += 256) {
     const long long i = base + k;
@@ -1466,13 +1490,14 @@ adam_multi_kernel(const long long* __restrict__ tab, int nt, float lr, float b1,
 }
 
 extern "C" int tmae_adam_multi(const long long* table, int ntensors, long long nchunks, float lr, float beta1,
-                               float beta2, float eps, float weight_decay, int step, const float* clip, void* stream) {
-  TMAE_REQUIRE(table && ntensors > 0 && step >= 1, "tmae_adam_multi: bad arguments");
-  if (nchunks <= 0) return TMAE_OK;
-  const double bc1 = 1.0 - pow((double)beta1, (double)step);
-  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+                               float beta2, float eps, float weight_decay, const float* clip, void* stream) {
+  TMAE_REQUIRE(table && ntensors > 0 && nchunks >= 0, "tmae_adam_multi: bad arguments");
+  hipLaunchKernelGGL(adam_step_kernel, dim3((unsigned)((ntensors + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     table, ntensors);
+  TMAE_LAUNCH_CHECK_NORET("tmae_adam_multi (steps)");
+  if (nchunks == 0) return TMAE_OK;
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, table, ntensors,
-                     lr, beta1, beta2, eps, weight_decay, (float)bc1, (float)sqrt(bc2), clip);
+                     lr, beta1, beta2, eps, weight_decay, clip);
   TMAE_LAUNCH_CHECK("tmae_adam_multi");
 }
 

@@ -51,8 +51,11 @@ class SyntheticCropSet:
     def next(self):
         """the next planned batch: (imgs [B, 3, crop, crop] f32 normalised, total_scores [B, L] f32)"""
         crops, scores = self._plan
-        i = self._i % crops.shape[0]
+        n = self._i
         self._i += 1
-        out = self._out[i & 1]  # two buffers: a batch stays valid while the next one is cut
+        i = n % crops.shape[0]
+        # two buffers, alternating on the monotonic call count (not the wrapped plan index, which repeats a
+        # buffer when an odd-length plan wraps): a batch stays valid while the next one is cut
+        out = self._out[n & 1]
         ops.crop_normalize_u8(self.images, crops[i], self.crop, IMAGENET_MEAN, IMAGENET_STD, out=out)
         return out, scores[i]

@@ -40,6 +40,91 @@ def train_step(model, criterion, samples, total_scores, optimizer, aux_optimizer
     return out_criterion
 
 
+class GraphedTrainStep:
+    """The loop body of utils/engine.py:72-91 (``train_step``) captured ONCE into a HIP graph and replayed per
+    batch: forward (HIP kernels, device noise from torch's graph-safe generator), RateDistortionLoss, aux loss,
+    the HIP backward, clip_grad_norm_, both FusedAdam steps and zero_grad are one ``graph.replay()``, so the host
+    enqueues one launch per step instead of ~2500.
+
+    What makes the step capturable: the library never allocates or synchronises; the optimizer's step counts
+    and bias corrections live on the device (optim.FusedAdam); launch tables built during capture come from
+    pinned memory (optim.device_table); the gradient buffer is persistent.  Construction runs ``warmup`` eager
+    training steps on the first batch (ordinary optimizer steps: lazy workspaces and tables are created outside
+    the capture), then captures one more step without running it.
+
+    Each call copies the batch into the graph's static input tensors, replays, and advances the parameters'
+    version counters (the update kernel writes through raw pointers; the executors' weight caches are keyed on
+    the versions, so an eager forward after replays re-lays out the new weights).  The learning rates, betas,
+    eps and weight decays are baked into the graph: when any of them changes, the step is captured again.
+    Data parallelism (a GradSync with more than one rank) is not captured: use ``train_step`` there."""
+
+    def __init__(self, model, criterion, optimizer, aux_optimizer, samples, total_scores, clip_max_norm=1.0,
+                 warmup=1, noise=None):
+        sync = getattr(model, "grad_sync", None)
+        if sync is not None and (sync.world() > 1 or sync.always_collective):
+            raise ValueError("GraphedTrainStep: the data-parallel gradient all-reduce is not captured; "
+                             "use engine.train_step with data parallelism")
+        if not samples.is_cuda:
+            raise ValueError("GraphedTrainStep needs device inputs")
+        self.model, self.criterion = model, criterion
+        self.optimizer, self.aux_optimizer = optimizer, aux_optimizer
+        self.clip_max_norm = clip_max_norm
+        self.samples = samples.detach().clone()
+        self.total_scores = total_scores.detach().clone()
+        # injected quantisation noise (parity tests): static tensors refreshed per call like the batch
+        self.noise = tuple(t.detach().clone() for t in noise) if noise is not None else None
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.graph, self.out = None, None
+        self._capture(warmup)
+
+    def _hyper(self):
+        return tuple((g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"])
+                     for o in (self.optimizer, self.aux_optimizer) for g in o.param_groups)
+
+    def _step(self):
+        return train_step(self.model, self.criterion, self.samples, self.total_scores, self.optimizer,
+                          self.aux_optimizer, self.clip_max_norm, noise=self.noise)
+
+    def _capture(self, warmup):
+        self.graph, self.out = None, None
+        cur = torch.cuda.current_stream(self.samples.device)
+        side = torch.cuda.Stream(device=self.samples.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._step()
+        cur.wait_stream(side)
+        self.optimizer.zero_grad()
+        self.aux_optimizer.zero_grad()
+        # every weight cache stale at capture time, so the graph always carries the per-step weight re-layout
+        from .optim import bump_versions
+
+        bump_versions(self.params)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            out = self._step()
+        self.graph, self.out = g, out
+        self._hyper_at_capture = self._hyper()
+
+    def __call__(self, samples, total_scores, noise=None):
+        """one training step on (samples, total_scores); returns the step's device losses (static tensors,
+        overwritten by the next call)"""
+        if (noise is None) != (self.noise is None):
+            raise ValueError("GraphedTrainStep: noise must be given at every call iff it was given at capture")
+        if self._hyper() != self._hyper_at_capture:
+            self._capture(0)
+        self.samples.copy_(samples, non_blocking=True)
+        self.total_scores.copy_(total_scores, non_blocking=True)
+        if noise is not None:
+            for dst, src in zip(self.noise, noise):
+                dst.copy_(src, non_blocking=True)
+        self.graph.replay()
+        from .optim import bump_versions
+
+        bump_versions(self.params)
+        return self.out
+
+
 def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer, epoch, clip_max_norm=1.0,
                     accum_iter=1, log=None):
     """utils/engine.py:30-156 (without MetricLogger / TensorBoard); returns the per-metric averages"""

@@ -25,6 +25,7 @@ import torch.nn as nn
 from . import _lib, ops
 from . import train_ops as T
 from .ops import ACT_GELU, ACT_NONE
+from .optim import device_table
 
 
 def _convs(seq):
@@ -125,7 +126,8 @@ class _Weights:
             owner = [t for t in range(len(rows)) for _ in range(rows[t + 1][11] - rows[t][11] if t + 1 < len(rows)
                                                                 else chunk - rows[t][11])]
             flat = [v for r in rows for v in r] + owner  # the rows, then each chunk's row (tmae.h)
-            self._tab = (key, torch.tensor(flat, dtype=torch.int64).to(dev), chunk)
+            tab, pinned = device_table(flat, dev)
+            self._tab = (key, tab, chunk, pinned)
         _lib.call("tmae_relayout_multi", self._tab[1].data_ptr(), len(rows), self._tab[2],
                   torch.cuda.current_stream().cuda_stream)
 

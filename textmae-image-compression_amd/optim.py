@@ -1,11 +1,12 @@
 """Optimizer side of the training step (utils/engine.py:81-91; configure_optimizers,
 models/Compression/common/model_utils.py:67-90).
 
-* ``FusedAdam`` — torch.optim.Adam semantics (amsgrad=False, L2 weight decay), every parameter of
-  a group updated by ONE HIP launch (tmae_adam_multi over a device table of tensors).  The moments
-  live in one flat f32 buffer per group; ``state_dict()`` / ``load_state_dict()`` speak torch.optim.Adam's
-  per-parameter format (``step``, ``exp_avg``, ``exp_avg_sq``), so a checkpoint written by the
-  reference's ``save_model`` (model_utils.py:30-55, torch Adam) resumes here and vice versa.
+* ``FusedAdam`` — torch.optim.Adam semantics (amsgrad=False, L2 weight decay, per-parameter step counts),
+  every parameter of a group updated by ONE HIP launch (tmae_adam_multi over a device table of tensors).
+  The moments live in one flat f32 buffer per group, the step counts in a device int32 array;
+  ``state_dict()`` / ``load_state_dict()`` speak torch.optim.Adam's per-parameter format (``step``,
+  ``exp_avg``, ``exp_avg_sq``), so a checkpoint written by the reference's ``save_model``
+  (model_utils.py:30-55, torch Adam) resumes here and vice versa.
 * ``clip_grad_norm_`` — torch.nn.utils.clip_grad_norm_ semantics; when every gradient lives in the
   training executor's flat buffer (the normal case after MCM's backward) it is one f64 reduction +
   one in-place scale over that buffer, with no host synchronisation.
@@ -31,25 +32,47 @@ def bump_versions(params):
         torch._C._autograd._unsafe_set_version_counter(ps, tuple(p._version + 1 for p in ps))
 
 
+def device_table(rows, device):
+    """int64 rows -> a device table for a multi-tensor launch.  While a stream is being captured into a HIP graph
+    the copy comes from pinned host memory (a pageable H2D copy cannot be captured); the pinned source is
+    returned with the table and must stay alive as long as the table (the graph's copy node reads it)."""
+    h = torch.tensor(rows, dtype=torch.int64)
+    if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
+        h = h.pin_memory()
+        return h.to(device, non_blocking=True), h
+    return h.to(device), None
+
+
 class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam (amsgrad=False, L2 weight decay) with one HIP launch per group.
+
+    Step counts are per parameter and live on the device (int32, advanced by the update launch itself), as
+    torch.optim.Adam keeps ``state[p]["step"]`` per parameter: a parameter without a gradient at some step is
+    skipped and keeps its count, exactly like torch's loop.  Nothing on the step path reads a host value that
+    changes from step to step (the bias corrections come from the device counts), so the whole training step
+    -- optimizer included -- can be captured into a HIP graph and replayed (engine.GraphedTrainStep).  The
+    learning rate, betas, eps and weight decay are launch arguments: a graph bakes in the values it was
+    captured with."""
+
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         for group in self.param_groups:
             for p in group["params"]:
                 if p.dtype != torch.float32 or not p.is_cuda or not p.is_contiguous():
                     raise ValueError("FusedAdam needs contiguous f32 device parameters")
-        self._flat = [self._new_flat(g) for g in self.param_groups]  # per group: [m, v, step, offsets]
+        self._flat = [self._new_flat(g) for g in self.param_groups]  # per group: [m, v, steps, offsets]
         self._tabs = [None] * len(self.param_groups)
 
     @staticmethod
     def _new_flat(group):
         off, o = {}, 0
-        for p in group["params"]:
-            off[id(p)] = o
+        for i, p in enumerate(group["params"]):
+            off[id(p)] = (o, i)
             o += p.numel()
         dev = group["params"][0].device if group["params"] else None
         z = torch.zeros(o, dtype=torch.float32, device=dev)
-        return [z, torch.zeros_like(z), 0, off]
+        steps = torch.zeros(max(len(group["params"]), 1), dtype=torch.int32, device=dev)
+        return [z, torch.zeros_like(z), steps, off]
 
     def add_param_group(self, param_group):
         super().add_param_group(param_group)
@@ -62,15 +85,16 @@ class FusedAdam(torch.optim.Optimizer):
         hit = self._tabs[gi]
         if hit is not None and hit[0] == key:
             return hit[1], hit[2]
-        mb, vb, _, off = self._flat[gi]
+        mb, vb, steps, off = self._flat[gi]
         rows, chunk = [], 0
         for p in live:
             n = p.numel()
-            rows.append([p.data_ptr(), p.grad.data_ptr(), mb[off[id(p)]:].data_ptr(), vb[off[id(p)]:].data_ptr(), n,
-                         chunk])
+            o, i = off[id(p)]
+            rows.append([p.data_ptr(), p.grad.data_ptr(), mb[o:].data_ptr(), vb[o:].data_ptr(), n, chunk,
+                         steps[i:].data_ptr()])
             chunk += (n + CHUNK - 1) // CHUNK
-        tab = torch.tensor(rows, dtype=torch.int64).to(mb.device)
-        self._tabs[gi] = (key, tab, chunk)
+        tab, pinned = device_table(rows, mb.device)
+        self._tabs[gi] = (key, tab, chunk, pinned)
         return tab, chunk
 
     @torch.no_grad()
@@ -83,21 +107,13 @@ class FusedAdam(torch.optim.Optimizer):
             live = [p for p in group["params"] if p.grad is not None]
             if not live:
                 continue
-            if len(live) != sum(1 for p in group["params"] if p.requires_grad):
-                # torch.optim.Adam keeps a step count per parameter; FusedAdam keeps one per group (one bias
-                # correction for the whole flat buffer), which equals torch's only if every parameter steps
-                raise ValueError("FusedAdam: every trainable parameter of a group needs a gradient at every step "
-                                 "(one step count per group); use torch.optim.Adam for partial updates")
             for p in live:
                 if p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
                     raise ValueError("FusedAdam needs contiguous f32 gradients")
-            flat = self._flat[gi]
-            flat[2] += 1
             tab, nchunks = self._table(gi, live)
             b1, b2 = group["betas"]
             _lib.call("tmae_adam_multi", tab.data_ptr(), len(live), nchunks, float(group["lr"]), float(b1), float(b2),
-                      float(group["eps"]), float(group["weight_decay"]), flat[2], None,
-                      torch.cuda.current_stream().cuda_stream)
+                      float(group["eps"]), float(group["weight_decay"]), None, torch.cuda.current_stream().cuda_stream)
             bump_versions(live)
         return loss
 
@@ -105,12 +121,13 @@ class FusedAdam(torch.optim.Optimizer):
     def state_dict(self):
         self.state.clear()
         for gi, group in enumerate(self.param_groups):
-            mb, vb, step, off = self._flat[gi]
-            if step == 0:
-                continue  # torch Adam has no state before its first step
+            mb, vb, steps, off = self._flat[gi]
+            counts = steps.cpu().tolist()
             for p in group["params"]:
-                o, n = off[id(p)], p.numel()
-                self.state[p] = {"step": torch.tensor(float(step)), "exp_avg": mb[o:o + n].view_as(p).clone(),
+                (o, i), n = off[id(p)], p.numel()
+                if counts[i] == 0:
+                    continue  # torch Adam has no state for a parameter before its first step
+                self.state[p] = {"step": torch.tensor(float(counts[i])), "exp_avg": mb[o:o + n].view_as(p).clone(),
                                  "exp_avg_sq": vb[o:o + n].view_as(p).clone()}
         try:
             return super().state_dict()
@@ -124,19 +141,17 @@ class FusedAdam(torch.optim.Optimizer):
         self._flat = [self._new_flat(g) for g in self.param_groups]
         self._tabs = [None] * len(self.param_groups)
         for gi, group in enumerate(self.param_groups):
-            mb, vb, _, off = self._flat[gi]
-            steps = set()
+            mb, vb, steps, off = self._flat[gi]
+            counts = [0] * steps.numel()
             for p in group["params"]:
                 st = self.state.get(p)
                 if not st:
                     continue
-                o, n = off[id(p)], p.numel()
+                (o, i), n = off[id(p)], p.numel()
                 mb[o:o + n].copy_(st["exp_avg"].reshape(-1))
                 vb[o:o + n].copy_(st["exp_avg_sq"].reshape(-1))
-                steps.add(int(float(st["step"])))
-            if len(steps) > 1:
-                raise ValueError(f"FusedAdam keeps one step count per group; the checkpoint has {sorted(steps)}")
-            self._flat[gi][2] = steps.pop() if steps else 0
+                counts[i] = int(float(st["step"]))
+            steps.copy_(torch.tensor(counts, dtype=torch.int32))
         self.state.clear()
 
 

@@ -25,16 +25,23 @@ class GradSync:
     ``Work.wait()`` ordering against the compute stream -- on a single GPU."""
 
     def __init__(self, process_group=None, bucket_mb: float = 64.0, average: bool = True,
-                 always_collective: bool = False):
+                 always_collective: bool = False, timing: bool = False):
         self.group = process_group
         self.bucket_elems = max(1, int(bucket_mb * (1 << 20) // 4))
         self.average = average
         self.always_collective = always_collective
         self.launched = 0  # collectives issued (tests check the buckets really went out)
+        self.launched_in_backward = 0  # of those, issued by ready() while the backward was still running
         self.flat = None
         self._bounds = None
         self._next = 0
         self._work = []
+        # timing (observability of the overlap, no host sync): HIP events on the compute stream at the first
+        # bucket's launch point, at the end of the backward (finish() called) and after the last collective's
+        # completion is ordered before the compute stream
+        self.timing = timing
+        self._ev = None
+        self._first = None
 
     def world(self):
         return dist.get_world_size(self.group) if dist.is_initialized() else 1
@@ -46,6 +53,13 @@ class GradSync:
         self.flat = flat
         self._next = 0
         self._work = []
+        self._first = None
+        self.launched_in_backward = 0
+
+    def _event(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream(self.flat.device))
+        return e
 
     def attach(self, flat):
         """start a backward over `flat` (called by the executor before the first ready())"""
@@ -58,6 +72,8 @@ class GradSync:
         if W <= 1 and not (self.always_collective and dist.is_initialized()):
             return
         self.launched += 1
+        if self.timing and self.flat.is_cuda and self._first is None:
+            self._first = self._event()
         if dist.get_backend(self.group) == "nccl":
             op = dist.ReduceOp.AVG if self.average else dist.ReduceOp.SUM
             self._work.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
@@ -66,18 +82,40 @@ class GradSync:
             if self.average:
                 t.div_(W)
 
-    def ready(self, upto: int):
+    def ready(self, upto: int, _in_backward: bool = True):
         """gradients [0, upto) of the flat buffer are final: launch every bucket they complete"""
         while self._next < len(self._bounds) - 1 and self._bounds[self._next + 1] <= upto:
+            n0 = self.launched
             self._launch(self._next)
+            if _in_backward:
+                self.launched_in_backward += self.launched - n0
             self._next += 1
 
     def finish(self):
         """launch the remaining buckets and order the compute stream after every collective"""
-        self.ready(self._bounds[-1])
+        timed = self.timing and self.flat is not None and self.flat.is_cuda
+        end = self._event() if timed else None  # the backward's last kernel is enqueued before this point
+        self.ready(self._bounds[-1], _in_backward=False)
         for w in self._work:
             w.wait()
         self._work = []
+        if timed:
+            self._ev = (self._first, end, self._event(), len(self._bounds) - 1, self.flat.numel() * 4,
+                        self.launched_in_backward)
+
+    def last_timing(self):
+        """the last backward's overlap numbers (synchronises on its events): ``allreduce_exposed_ms`` = end of the
+        backward's kernels -> every collective complete on the compute stream's timeline; ``allreduce_issue_ms`` =
+        first bucket's launch point -> end of the backward (how long the collectives ran under backward kernels);
+        bucket count and bytes; how many buckets were issued from inside the backward"""
+        if self._ev is None:
+            return None
+        first, end, done, nb, nbytes, inb = self._ev
+        done.synchronize()
+        return {"allreduce_exposed_ms": round(end.elapsed_time(done), 3),
+                "allreduce_issue_ms": round(first.elapsed_time(end), 3) if first is not None else None,
+                "buckets": nb, "bucket_bytes": self.bucket_elems * 4, "grad_bytes": nbytes,
+                "buckets_issued_in_backward": inb}
 
 
 def _host_all_reduce_sum(t, group):
@@ -110,8 +148,9 @@ def broadcast_parameters(model, src: int = 0, group=None):
     bump_versions(model.parameters())
 
 
-def enable_data_parallel(model, process_group=None, bucket_mb: float = 64.0, always_collective: bool = False):
+def enable_data_parallel(model, process_group=None, bucket_mb: float = 64.0, always_collective: bool = False,
+                         timing: bool = False):
     """attach a GradSync to `model` (MCM): its backward then all-reduces (averages) the gradients"""
-    model.grad_sync = GradSync(process_group, bucket_mb, always_collective=always_collective)
+    model.grad_sync = GradSync(process_group, bucket_mb, always_collective=always_collective, timing=timing)
     broadcast_parameters(model, group=process_group)
     return model.grad_sync

@@ -42,13 +42,16 @@ def main():
     for f in sorted(set(fetch) | set(write)):
         n = max(fetch[f][0], 1)
         byts = (2 * fetch[f][1] + write[f][1]) * 1024
-        out["per_family"][f] = {"launches": fetch[f][0], "fetch_kib_raw": round(fetch[f][1], 1),
-                                "write_kib": round(write[f][1], 1), "hbm_bytes_per_fwd": int(byts / nf),
-                                "hbm_bytes_per_launch": int(byts / n)}
+        # the profiled run holds only whole forwards (tools/pmc_bench.sh: --no-roofline, no replays), so a
+        # family's launches per forward = its launches / forwards, and per-forward bytes = per-launch bytes x that
+        lpf = fetch[f][0] / nf
+        out["per_family"][f] = {"launches": fetch[f][0], "launches_per_fwd": round(lpf, 3),
+                                "fetch_kib_raw": round(fetch[f][1], 1), "write_kib": round(write[f][1], 1),
+                                "hbm_bytes_per_launch": int(byts / n), "hbm_bytes_per_fwd": int(byts / n * lpf)}
     d = out["per_family"].get(fam)
     out["hbm_bytes_per_launch"] = d["hbm_bytes_per_launch"] if d else None
     out["note"] = ("FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, summed over the family's dispatches of an "
-                   "eager (--no-graph) bench run, divided by its launch count; Infinity-Cache hits are counted as "
+                   "eager (--no-graph --no-roofline) bench run of whole forwards, divided by its launch count; Infinity-Cache hits are counted as "
                    "fetches by these counters")
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 4:
