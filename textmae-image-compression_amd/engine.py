@@ -97,9 +97,10 @@ class GraphedTrainStep:
         self.optimizer.zero_grad()
         self.aux_optimizer.zero_grad()
         # every weight cache stale at capture time, so the graph always carries the per-step weight re-layout
-        from .optim import bump_versions
+        from .optim import bump_versions, reserve_capture_staging
 
         bump_versions(self.params)
+        reserve_capture_staging()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             out = self._step()

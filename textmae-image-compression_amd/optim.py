@@ -32,14 +32,47 @@ def bump_versions(params):
         torch._C._autograd._unsafe_set_version_counter(ps, tuple(p._version + 1 for p in ps))
 
 
+class _PinnedArena:
+    """pinned host staging for launch tables built while a stream is being captured: neither a pageable H2D copy
+    nor a pinned allocation may happen during a capture, so the pinned buffer is reserved before it
+    (``reserve_capture_staging``) and handed out by a bump allocator.  The graph's copy nodes read their slices
+    at every replay, so nothing is reused until the next ``reserve_capture_staging`` (a new capture)."""
+
+    def __init__(self):
+        self.buf, self.off = None, 0
+
+    def reserve(self, nbytes):
+        n = (int(nbytes) + 7) // 8
+        if self.buf is None or self.buf.numel() < n:
+            self.buf = torch.empty(n, dtype=torch.int64).pin_memory()
+        self.off = 0
+
+    def take(self, n):
+        if self.buf is None or self.off + n > self.buf.numel():
+            raise RuntimeError("launch table built during a HIP graph capture without enough pinned staging: call "
+                               "optim.reserve_capture_staging() before capturing")
+        v = self.buf[self.off:self.off + n]
+        self.off += (n + 7) // 8 * 8  # 64-B aligned slices
+        return v
+
+
+_ARENA = _PinnedArena()
+
+
+def reserve_capture_staging(nbytes=8 << 20):
+    """reserve (and reset) the pinned staging that launch tables built inside a graph capture are copied from"""
+    _ARENA.reserve(nbytes)
+
+
 def device_table(rows, device):
     """int64 rows -> a device table for a multi-tensor launch.  While a stream is being captured into a HIP graph
-    the copy comes from pinned host memory (a pageable H2D copy cannot be captured); the pinned source is
-    returned with the table and must stay alive as long as the table (the graph's copy node reads it)."""
-    h = torch.tensor(rows, dtype=torch.int64)
+    the copy comes from the pinned staging arena (a pageable H2D copy or a pinned allocation cannot be captured);
+    returns (table, pinned slice or None)."""
+    h = torch.tensor(rows, dtype=torch.int64).reshape(-1)
     if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
-        h = h.pin_memory()
-        return h.to(device, non_blocking=True), h
+        p = _ARENA.take(h.numel())
+        p.copy_(h)
+        return p.to(device, non_blocking=True), p
     return h.to(device), None
 
 
