@@ -77,6 +77,15 @@ int tmae_cls_rows(float* tokens, const float* cls, const float* pos, int n, int 
  * softmax((q k^T) * scale) v, dh in {32, 64, 80} (80: ViT-H, models_mae.py:239-244), T <= 512. */
 int tmae_mha_fwd(const void* qkv, void* out, int B, int T, int H, int dh, float scale, int dtype, void* stream);
 
+/* qkv Linear + multi-head attention in one launch (bf16 inference; timm Attention qkv + core, MCM.py:629-630,
+ * 678-679): out [B*T][H*dh] = attention of [q | k | v] = x W_qkv^T + b_qkv, x [B*T][H*dh] bf16, W_qkv
+ * [3*H*dh][H*dh] bf16 (nn.Linear layout), b_qkv [3*H*dh] f32.  Q / K / V stay in LDS (no qkv tensor in HBM);
+ * output bit-identical to tmae_linear_fwd(qkv) + tmae_mha_fwd.  Shapes with a fused kernel:
+ * tmae_qkv_attn_supported (dh 64 with T in (128, 160] or (64, 96]; dh 32 with T in (256, 288], H even). */
+int tmae_qkv_attn_supported(int T, int H, int dh);
+int tmae_qkv_attn_fwd(const void* x, const void* w_qkv, const float* b_qkv, void* out, int B, int T, int H, int dh,
+                      float scale, int dtype, void* stream);
+
 /* decoder_embed + mask-token unshuffle + decoder_pos_embed (MCM.py:657-675):
  * x [n*ntok][Din] -> out [n][L+1][D]; token k -> row 0 (k=0) or 1 + ids_shuffle[b][k-1].
  * ntok = K for MCM (cls already dropped: the reference's off-by-one), K+1 for MAE. */

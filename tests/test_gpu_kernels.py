@@ -131,6 +131,31 @@ def test_mha(tmae, B, T, H, dh, dtype):
     check("rel:out_float", rel(out.float(), _ref_attn(qkv.to(dtype).float(), B, T, H, dh)), (1e-4 if dtype == torch.float32 else 7e-3))
 
 
+@pytest.mark.parametrize("B,T,H,dh", [(64, 145, 12, 64), (64, 257, 16, 32), (64, 65, 12, 64), (3, 145, 12, 64),
+                                      (2, 257, 16, 32), (1, 129, 2, 64), (2, 288, 4, 32), (2, 160, 1, 64)])
+def test_qkv_attn_fused_bitwise(tmae, B, T, H, dh):
+    """tmae_qkv_attn_fwd (qkv Linear + attention in one launch, Q / K / V kept in LDS) equals the unfused
+    tmae_linear_fwd(qkv) + tmae_mha_fwd bit for bit (same MFMA accumulation order, same bias rounding, same
+    attention core), and both are within the bf16 bound of the fp32 reference"""
+    if not tmae.ops.qkv_attn_supported(T, H, dh, torch.bfloat16):
+        pytest.skip("no fused kernel for this shape")
+    torch.manual_seed(T + H)
+    D = H * dh
+    x = (torch.randn(B * T, D) * 1.5).to(torch.bfloat16).to(DEV)
+    w = (torch.randn(3 * D, D) / D ** 0.5).to(torch.bfloat16).to(DEV)
+    b = (torch.randn(3 * D) * 0.1).to(DEV)
+    scale = dh ** -0.5
+    qkv = tmae.ops.linear(x, w, b, torch.bfloat16)
+    ref = tmae.ops.mha(qkv, B, T, H, dh, scale, torch.bfloat16)
+    out = torch.full((B * T, D), float("nan"), dtype=torch.bfloat16, device=DEV)
+    tmae.ops.qkv_attn(x, w, b, B, T, H, dh, scale, torch.bfloat16, out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref), float((out.float() - ref.float()).abs().max())
+    if B <= 3:
+        r32 = _ref_attn((x.float() @ w.float().t() + b).cpu(), B, T, H, dh)
+        check("rel:out_float", rel(out.float(), r32), 1.5e-2)
+
+
 # ------------------------------------------------------------------------------------ convs
 def _nhwc(x, dtype):
     return x.permute(0, 2, 3, 1).contiguous().to(dtype).to(DEV)

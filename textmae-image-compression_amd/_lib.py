@@ -107,6 +107,7 @@ SIGNATURES = {
     "tmae_patch_embed_fwd": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
     "tmae_cls_rows": [P, P, P, I, I, I, P],
     "tmae_mha_fwd": [P, P, I, I, I, I, F, I, P],
+    "tmae_qkv_attn_fwd": [P, P, P, P, I, I, I, I, F, I, P],
     "tmae_decoder_embed_fwd": [P, I, P, P, P, P, P, I, I, I, I, I, I, P],
     "tmae_mask_rows": [P, P, P, P, I, I, I, I, P],
     "tmae_decoder_pred_fwd": [P, P, P, P, I, I, I, I, I, I, I, I, P],
@@ -189,7 +190,8 @@ SIGNATURES = {
 # entry points that return a value rather than a status
 VALUE_FUNCS = {"tmae_wgrad_workspace": ([I, I, I, I], ctypes.c_longlong),
                "tmae_metrics_workspace": ([I, I, I, I], ctypes.c_longlong),
-               "tmae_image_scores_workspace": ([I, I, I, I], ctypes.c_longlong)}
+               "tmae_image_scores_workspace": ([I, I, I, I], ctypes.c_longlong),
+               "tmae_qkv_attn_supported": ([I, I, I], ctypes.c_int)}
 
 _lib = None
 

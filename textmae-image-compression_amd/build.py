@@ -24,7 +24,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{INCLUDE}",
 HOST_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"-I{INCLUDE}", "-Wall"]
 # per-source extras.  attention.hip: the softmax max trees take MFMA results through loop phis, where IEEE-mode
 # fmaxf would first quiet each operand (one v_max_f32 x, x per score); scores are finite or the -inf mask.
-EXTRA = {"attention.hip": ["-fno-honor-nans"]}
+EXTRA = {"attention.hip": ["-fno-honor-nans"], "qkv_attn.hip": ["-fno-honor-nans"]}
 
 
 def _sources():

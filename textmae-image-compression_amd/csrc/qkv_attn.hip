@@ -1,0 +1,183 @@
+// Fused qkv projection + multi-head attention for the bf16 inference forward (timm Block attention branch,
+// MCM.py:629-630 encoder, 678-679 decoder):   O = softmax(Q K^T * dh^-0.5) V,   [Q | K | V] = X W_qkv^T + b.
+//
+// Unfused, the qkv GEMM writes [B*T][3D] bf16 to HBM and the attention kernel reads it straight back
+// (85 MB per encoder layer, 101 MB per decoder layer at batch 64), and the GEMM's store burst is the
+// slowest part of its epilogue.  Here ONE workgroup owns (image b, head group g of HG heads):
+//   1. GEMM: the tile is all Tpad (= T rounded up to 32) token rows of image b x the 3 * HG * dh weight rows
+//      of its heads' q, k and v (192 columns for ViT-B dh 64 x 1 head and the decoder's dh 32 x 2 heads),
+//      K = D; the same LDS-DMA ring, swizzle and swapped 16x16x32 MFMA step as gemm_core.h, so every
+//      accumulator sums its products in the same order as the unfused GEMM;
+//   2. epilogue: + bias, round to bf16, written into LDS as the attention core's Q / K / V images (row-major
+//      [Tpad][dh + 8] for Q and K, [Tpad][LDV] for V) -- the ring is reused, nothing goes to HBM;
+//   3. attention: the waves walk (head, 32-query block) items with the shared core (attn_core.h), O -> HBM.
+// Q, K, V and O are bit-identical to the unfused qkv GEMM + mha_fwd_bf16_kernel (tests/test_gpu_kernels.py).
+// Rows past T are copies of row T - 1 (clamped DMA rows): masked as keys, never stored as queries.
+// One workgroup per CU (8 waves; 88-126 KiB of LDS); workgroups of one image run back to back on one XCD
+// (xcd_remap), so its X rows are fetched into that L2 once for all heads.
+#include "attn_core.h"
+#include "gemm_core.h"
+
+namespace qa {
+constexpr int NW = 8, WGN = 4, WGM = 2;  // waves: 4 along the 192 weight columns, 2 along the tokens
+template <int DH, int HG, int TPAD> struct Cfg {
+  static constexpr int NC = 3 * HG * DH;            // GEMM columns (weight rows) of the workgroup
+  static constexpr int ROWS = NC + TPAD;            // LDS rows per ring stage (128 B each)
+  static constexpr int PIECES = ROWS / 8;           // 1-KiB LDS-DMA pieces per stage
+  static constexpr int PPW = (PIECES + NW - 1) / NW;  // pieces per wave (the last round partial)
+  static constexpr int WN = NC / WGN, WM = TPAD / WGM;
+  static constexpr int TN = WN / 16, TM = WM / 16;
+  static constexpr int LDQ = DH + 8, LDV = AttnTr<DH>::LDV;
+  static constexpr int QK_BYTES = TPAD * LDQ * 2, V_BYTES = TPAD * LDV * 2;
+  static constexpr int HEAD_BYTES = 2 * QK_BYTES + V_BYTES;  // Q, K, V images of one head
+  static constexpr int RING = 2 * ROWS * 128;
+  static constexpr int LDS = RING > HG * HEAD_BYTES ? RING : HG * HEAD_BYTES;
+  static_assert(ROWS % 8 == 0 && WN % 16 == 0 && WM % 16 == 0 && TPAD % 32 == 0, "qkv_attn tile");
+  static_assert(LDV > 0 && DH % 32 == 0, "qkv_attn: head dim with a lean attention core");
+  static_assert(LDS <= 160 * 1024, "qkv_attn: LDS");
+};
+}  // namespace qa
+
+template <int DH, int HG, int TPAD>
+__global__ void __launch_bounds__(qa::NW * 64, 1)
+qkv_attn_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, const float* __restrict__ bias,
+                bf16* __restrict__ out, int T, int H, float scale_log2e) {
+  using C = qa::Cfg<DH, HG, TPAD>;
+  constexpr int NW = qa::NW, WGN = qa::WGN;
+  constexpr int NC = C::NC, TN = C::TN, TM = C::TM, WN = C::WN, WM = C::WM, LDQ = C::LDQ, LDV = C::LDV;
+  __shared__ __attribute__((aligned(16))) uint4 lds[C::LDS / 16];
+
+  const int ngroups = H / HG;
+  const int item = xcd_remap(blockIdx.x, gridDim.x), b = item / ngroups, g = item - b * ngroups;
+  const int D = H * DH, HD = HG * DH;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave % WGN, wm = wave / WGN;
+  const bf16* xb = x + (size_t)b * T * D;
+
+  // ---- 1. GEMM: acc[n][m] = sum_k W[row(n)][k] X[b, m][k]; weight row of column n (q | k | v parts, each the
+  // HD rows of this head group): part * D + g * HD + n % HD
+  const int pch = lane & 7;
+  const bf16* src[C::PPW];
+  int swz[C::PPW];
+#pragma unroll
+  for (int j = 0; j < C::PPW; ++j) {
+    const int r = 8 * (wave + NW * j) + (lane >> 3);  // LDS row this lane fills
+    const int rr = min(r, C::ROWS - 1);
+    if (rr < NC) {
+      const int part = rr / HD;
+      src[j] = w + (size_t)(part * D + g * HD + (rr - part * HD)) * D;
+    } else {
+      src[j] = xb + (size_t)min(rr - NC, T - 1) * D;  // rows past T: the last row (masked later)
+    }
+    swz[j] = pch ^ ((r >> 1) & 7);
+  }
+  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
+  const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
+  auto issue = [&](int stage, int kt) {
+    const unsigned sb = lds_base + (unsigned)stage * C::ROWS * 128u;
+#pragma unroll
+    for (int j = 0; j < C::PPW; ++j) {
+      if (C::PIECES % NW == 0 || (int)wave_u + NW * j < C::PIECES)  // wave-uniform: the last round is partial
+        glds16(src[j] + kt * 64 + swz[j] * 8, sb + (wave_u + NW * j) * 1024u);
+    }
+  };
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = D / 64;
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int stage = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) issue(stage ^ 1, kt + 1);
+    mfma_tile<bf16, NC, WN, WM, TN, TM>(lds + stage * C::ROWS * 8, wn, wm, lane, acc);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    stage ^= 1;
+  }
+
+  // ---- 2. + bias, bf16, into the per-head Q / K / V images (the ring is free after the last barrier)
+  // acc[i][j]: columns n = wn*WN + 16 i + 4 fq + 0..3 (never crossing a head), token m = wm*WM + 16 j + fr
+  unsigned char* lb = reinterpret_cast<unsigned char*>(lds);
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = wn * WN + 16 * i + 4 * fq;
+    const int part = n / HD, within = n - part * HD, hj = within / DH, d = within - hj * DH;
+    const f32x4 bv = load4f(bias + part * D + g * HD + within);
+    unsigned char* head = lb + hj * C::HEAD_BYTES;
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int m = wm * WM + 16 * j + fr;
+      const f32x4 v = acc[i][j] + bv;
+      bf16x4 o;
+      o[0] = (bf16)v[0]; o[1] = (bf16)v[1]; o[2] = (bf16)v[2]; o[3] = (bf16)v[3];
+      bf16* dst = part == 2 ? reinterpret_cast<bf16*>(head + 2 * C::QK_BYTES) + (size_t)m * LDV + d
+                            : reinterpret_cast<bf16*>(head + part * C::QK_BYTES) + (size_t)m * LDQ + d;
+      *reinterpret_cast<bf16x4*>(dst) = o;
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. attention: (head, 32-query block) items over the waves
+  constexpr int NQB = TPAD / 32;
+  for (int it = wave; it < HG * NQB; it += NW) {
+    const int hj = it / NQB, q0 = 32 * (it - hj * NQB);
+    if (q0 >= T) continue;  // wave-uniform
+    const unsigned char* head = lb + hj * C::HEAD_BYTES;
+    const bf16* Qs = reinterpret_cast<const bf16*>(head);
+    const bf16* Ks = reinterpret_cast<const bf16*>(head + C::QK_BYTES);
+    const bf16* Vs = reinterpret_cast<const bf16*>(head + 2 * C::QK_BYTES);
+    bf16x8 qf[DH / 16];
+    const bf16* qrow = Qs + (size_t)(q0 + (lane & 31)) * LDQ + 8 * (lane >> 5);
+#pragma unroll
+    for (int s2 = 0; s2 < DH / 16; ++s2) qf[s2] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s2);
+    mha_bf16_item<DH>(Ks, Vs, qf, T, TPAD, scale_log2e, lane, q0, nullptr,
+                      out + (size_t)b * T * D + (size_t)(g * HG + hj) * DH, D);
+  }
+}
+
+template <int DH, int HG, int TPAD>
+static int qkv_attn_launch(const bf16* x, const bf16* w, const float* b, bf16* out, int B, int T, int H, float scale,
+                           hipStream_t st) {
+  hipLaunchKernelGGL((qkv_attn_kernel<DH, HG, TPAD>), dim3(B * (H / HG)), dim3(qa::NW * 64), 0, st, x, w, b, out, T, H,
+                     scale * 1.4426950408889634f);
+  TMAE_LAUNCH_CHECK("tmae_qkv_attn_fwd");
+}
+
+// the (head dim, sequence) shapes with a fused instantiation; others take the unfused qkv GEMM + tmae_mha_fwd
+static bool qkv_attn_shape(int T, int H, int dh, int& hg, int& tpad) {
+  tpad = (T + 31) / 32 * 32;
+  if (dh == 64 && tpad == 160) { hg = 1; return true; }                     // ViT-B encoder, K = 144 (T 145)
+  if (dh == 64 && tpad == 96) { hg = 1; return true; }                      // ViT-B encoder, K = 64 (T 65)
+  if (dh == 32 && tpad == 288 && H % 2 == 0) { hg = 2; return true; }      // decoder 512 / 16 heads (T 257)
+  return false;
+}
+
+extern "C" int tmae_qkv_attn_supported(int T, int H, int dh) {
+  int hg, tpad;
+  return T >= 1 && H >= 1 && qkv_attn_shape(T, H, dh, hg, tpad) ? 1 : 0;
+}
+
+extern "C" int tmae_qkv_attn_fwd(const void* x, const void* w_qkv, const float* b_qkv, void* out, int B, int T, int H,
+                                 int dh, float scale, int dtype, void* stream) {
+  TMAE_REQUIRE(dtype == TMAE_BF16, "tmae_qkv_attn_fwd: bf16 operands only (the f32 path runs unfused)");
+  TMAE_REQUIRE(x && w_qkv && b_qkv && out, "tmae_qkv_attn_fwd: null pointer");
+  TMAE_REQUIRE(B >= 0 && T >= 1 && H >= 1, "tmae_qkv_attn_fwd: B=%d T=%d H=%d", B, T, H);
+  TMAE_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)w_qkv & 15) == 0 && ((uintptr_t)b_qkv & 15) == 0 &&
+               ((uintptr_t)out & 7) == 0, "tmae_qkv_attn_fwd: misaligned operand");
+  int hg, tpad;
+  TMAE_REQUIRE(qkv_attn_shape(T, H, dh, hg, tpad), "tmae_qkv_attn_fwd: no fused kernel for T=%d, %d heads of dim %d",
+               T, H, dh);
+  if (B == 0) return TMAE_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const bf16* xp = (const bf16*)x;
+  const bf16* wp = (const bf16*)w_qkv;
+  bf16* op = (bf16*)out;
+  if (dh == 64 && tpad == 160) return qkv_attn_launch<64, 1, 160>(xp, wp, b_qkv, op, B, T, H, scale, st);
+  if (dh == 64 && tpad == 96) return qkv_attn_launch<64, 1, 96>(xp, wp, b_qkv, op, B, T, H, scale, st);
+  return qkv_attn_launch<32, 2, 288>(xp, wp, b_qkv, op, B, T, H, scale, st);
+}

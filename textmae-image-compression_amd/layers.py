@@ -116,8 +116,13 @@ def run_block(resid, w: BlockWeights, B, T, dtype, s: BlockScratch):
     """timm Block forward on the f32 residual stream `resid` [B*T, D], in place (7 launches)."""
     rows = B * T
     ops.layernorm(resid, w.n1w, w.n1b, w.eps1, dtype, rows=rows, out=s.a)
-    ops.linear(s.a, w.qkv_w, w.qkv_b, dtype, out=s.qkv)
-    ops.mha(s.qkv, B, T, w.heads, w.dim // w.heads, w.scale, dtype, out=s.att)
+    dh = w.dim // w.heads
+    if w.qkv_b is not None and ops.qkv_attn_supported(T, w.heads, dh, dtype):
+        # qkv Linear + attention in one launch: Q / K / V never leave the chip (csrc/qkv_attn.hip)
+        ops.qkv_attn(s.a, w.qkv_w, w.qkv_b, B, T, w.heads, dh, w.scale, dtype, out=s.att)
+    else:
+        ops.linear(s.a, w.qkv_w, w.qkv_b, dtype, out=s.qkv)
+        ops.mha(s.qkv, B, T, w.heads, dh, w.scale, dtype, out=s.att)
     ops.linear_residual(s.att, w.proj_w, w.proj_b, resid, dtype)
     ops.layernorm(resid, w.n2w, w.n2b, w.eps2, dtype, rows=rows, out=s.a)
     ops.linear(s.a, w.fc1_w, w.fc1_b, dtype, act=ops.ACT_GELU, out=s.h)

@@ -135,6 +135,26 @@ def mha(qkv, B, T, H, dh, scale, dtype, out=None):
     return out
 
 
+_QKV_ATTN_OK = {}
+
+
+def qkv_attn_supported(T, H, dh, dtype):
+    """a fused qkv + attention kernel exists for this shape (bf16 only); TMAE_QKV_ATTN=0 turns it off"""
+    if dtype != torch.bfloat16 or os.environ.get("TMAE_QKV_ATTN", "1") == "0":
+        return False
+    key = (T, H, dh)
+    if key not in _QKV_ATTN_OK:
+        _QKV_ATTN_OK[key] = bool(_lib.value("tmae_qkv_attn_supported", T, H, dh))
+    return _QKV_ATTN_OK[key]
+
+
+def qkv_attn(x, w, b, B, T, H, dh, scale, dtype, out):
+    """out = attention(x W_qkv^T + b_qkv) in one launch, Q / K / V kept on chip (tmae_qkv_attn_fwd)"""
+    _lib.call("tmae_qkv_attn_fwd", x.data_ptr(), w.data_ptr(), b.data_ptr(), out.data_ptr(), B, T, H, dh, float(scale),
+              dtype_code(dtype), _stream())
+    return out
+
+
 def decoder_embed(x, w, b, pos, ids_shuffle, out, n, ntok, L, dtype):
     D, Din = w.shape
     _lib.call("tmae_decoder_embed_fwd", x.data_ptr(), int(x.dtype == torch.float32), w.data_ptr(), b.data_ptr(),
