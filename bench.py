@@ -19,7 +19,8 @@ the stream they run on, giving the family's kernel time per forward (DESIGN.md Â
 family mapping; tools/family_summary.py gives the same split from a rocprofv3 kernel trace):
   * ``roofline`` = the family with the most kernel time (the dominant kernel), FLOPs / time;
   * ``roofline.attention_block`` = encoder / decoder (qkv GEMM + attention core + proj GEMM);
-  * ``roofline.attention_core`` = the fused attention kernels alone (HBM/LDS-bound by AI, SURVEY (v)).
+  * ``roofline.attention_core`` = the attention kernels alone (HBM/LDS-bound by AI, SURVEY (v)) where they run as
+    their own launch; the bf16 forward fuses the qkv GEMM and the core into one launch (``qkv_attn_fused``).
 """
 import argparse
 import json
@@ -177,6 +178,12 @@ class LaunchTimer:
                     if name == "tmae_linear_residual_fwd":
                         return f"{side}_fc2", fl
             return "lic_1x1_gemm", fl
+        if name == "tmae_qkv_attn_fwd":
+            Bq, T, H, dh = a[4], a[5], a[6], a[7]
+            D = H * dh
+            fam = "enc_qkv_attn" if T == self.Te else "dec_qkv_attn"
+            self._hbm(fam, Bq * T * D * 2 * 2 + 3 * D * D * 2 + 3 * D * 4)  # x in, O out (bf16), W, bias
+            return fam, 2.0 * Bq * T * D * 3 * D + 4.0 * Bq * H * T * T * dh
         if name == "tmae_mha_fwd":
             Bq, T, H, dh = a[2], a[3], a[4], a[5]
             fam = "enc_attn_core" if T == Te else "dec_attn_core"
@@ -303,6 +310,8 @@ def roofline_report(m, imgs, scores, batch, dump=None):
             json.dump({"batch": batch, "launches": rows}, fh, indent=0)
     mf = {k: v for k, v in fam.items() if v[2] > 0}
     agg = {"token_gemm": [k for k in mf if k.split("_")[-1] in ("qkv", "proj", "fc1", "fc2")],
+           "token_gemm_with_qkv_attn": [k for k in mf if k.split("_")[-1] in ("qkv", "proj", "fc1", "fc2")
+                                        or k.endswith("qkv_attn")],
            "lic_conv3x3": ["lic_conv3x3"], "lic_3x3_all": ["lic_conv3x3", "lic_stack"]}
 
     def stat(keys):
@@ -329,8 +338,12 @@ def roofline_report(m, imgs, scores, batch, dump=None):
             "share_of_kernel_time": round(fam[dom][1] / total_t, 4),
             "kernel_time_per_step_us": round(total_t * 1e6, 1)}
     for side in ("enc", "dec"):
-        roof[f"attention_block_{side}"] = stat([f"{side}_qkv", f"{side}_attn_core", f"{side}_proj"])
-        roof[f"attention_core_{side}"] = stat([f"{side}_attn_core"])
+        # qkv GEMM + attention core + proj; the bf16 forward runs qkv + core as ONE fused launch ({side}_qkv_attn)
+        roof[f"attention_block_{side}"] = stat([f"{side}_qkv", f"{side}_attn_core", f"{side}_qkv_attn", f"{side}_proj"])
+        if f"{side}_attn_core" in fam:
+            roof[f"attention_core_{side}"] = stat([f"{side}_attn_core"])
+        if f"{side}_qkv_attn" in fam:
+            roof[f"qkv_attn_fused_{side}"] = stat([f"{side}_qkv_attn"])
     roof["families"] = per
     roof["aggregates"] = {k: stat(v) for k, v in agg.items()}
     if dom in ("lic_conv3x3", "lic_stack"):

@@ -341,17 +341,10 @@ __device__ __forceinline__ void attn_stage2(bf16* A0, const bf16* g0, int ld0, b
 // so 2-3 workgroups share a CU): phase 1 stages Q and dO (all queries) and reads this wave's 32 keys of K / V
 // from global; phase 2 re-stages K and V (all keys) and reads this wave's 32 queries of Q / dO from global.
 // The transposed operands (dO^T, Q^T, K^T) are ds_read_b64_tr_b16 reads of the same row-major arrays.
-// dh 32 (the decoder: 9 waves per workgroup at T = 257): at most 96 VGPRs, i.e. 5 waves per SIMD, so two
-// workgroups share a CU (115 VGPRs allowed only one: four rounds of workgroups instead of two)
-template <int DH> struct AttnBwdOcc { static constexpr int WPE = 1; };
-#ifndef TMAE_BWD32_WPE
-#define TMAE_BWD32_WPE 5  // A/B builds (tools/build_variant.sh)
-#endif
-template <> struct AttnBwdOcc<32> { static constexpr int WPE = TMAE_BWD32_WPE; };
-
+// (dh 32 capped at 96 VGPRs, five waves per SIMD, so that two 9-wave workgroups share a CU: 17 VGPRs spilled
+// and the decoder backward went 133 -> 147 us per launch, profiles/r04/c3_at_*.log; not kept)
 template <int DH>
 __global__ void __launch_bounds__(DH == 32 ? 1024 : 512)  // dh 64 / 80: <= 256 keys, 256 VGPRs
-__attribute__((amdgpu_waves_per_eu(AttnBwdOcc<DH>::WPE)))
 mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
                     const float* __restrict__ lse, bf16* __restrict__ dqkv, int Tn, int H, int Tpad, float scale) {
   constexpr int LDR = AttnBwd<DH>::LDR;

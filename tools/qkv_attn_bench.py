@@ -41,7 +41,7 @@ def main():
         t_fused = timeit(lambda: ops.qkv_attn(x, w, b, B, T, H, dh, s, bf, out=o))
         gf = (2 * B * T * D * 3 * D + 4 * B * H * T * T * dh) / 1e9
         print(f"{name}: qkv GEMM {t_gemm:.1f} us + core {t_core:.1f} us = {t_gemm + t_core:.1f} us | fused "
-              f"{t_fused:.1f} us ({gf / t_fused * 1e-3:.0f} TF/s, {gf / t_fused * 1e-3 / 2500:.3f} of peak)", flush=True)
+              f"{t_fused:.1f} us ({gf / t_fused * 1e3:.0f} TF/s, {gf / t_fused * 1e3 / 2500:.3f} of peak)", flush=True)
 
 
 if __name__ == "__main__":
