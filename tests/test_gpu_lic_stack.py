@@ -6,12 +6,10 @@ lrp_transform, MCM.py:165-293 applied at MCM.py:761-784) per workgroup.
   two input sources (torch.cat without a copy), the layer-0 addend, batched problems with strides, the
   f32 (mu / sigma) and the lrp (y_hat_pre + 0.5 tanh) outputs, the 12x12 and 8x8 grids, an empty
   layer-0 input (slice 0's mean / scale stacks);
-* the MCM eval forward with the fused stacks against the layer-by-layer launches (TMAE_LIC_STACK=0) on
+* the MCM eval forward with the fused stacks against the layer-by-layer launches (_Executor.USE_LIC_STACK) on
   the same weights, bf16, at the benched geometry.
 Tolerance: bf16 operands, f32 accumulation -> max|a-b| / max|b| <= 6e-3 per output (2x the measured 3.0e-3).
 """
-import os
-
 import pytest
 import torch
 import torch.nn.functional as F
@@ -128,12 +126,13 @@ def test_mcm_fused_stacks_match_layerwise(tmae):
     imgs = torch.randn(8, 3, 256, 256, device=DEV)
     scores = torch.rand(8, 256, device=DEV)
     outs = {}
-    old = os.environ.get("TMAE_LIC_STACK")
-    old_chain = os.environ.get("TMAE_LIC_CHAIN")
-    os.environ["TMAE_LIC_CHAIN"] = "0"  # MUSIG holds the batched slices' mu / sigma only without the chain
+    from textmae_amd import mcm as mcm_mod
+
+    ex_cls = mcm_mod._Executor
     try:
+        ex_cls.USE_LIC_CHAIN = False  # MUSIG holds the batched slices' mu / sigma only without the chain
         for flag in ("1", "0"):
-            os.environ["TMAE_LIC_STACK"] = flag
+            ex_cls.USE_LIC_STACK = flag == "1"
             m._exec = None
             with torch.no_grad():
                 o = m(imgs, scores)
@@ -144,14 +143,8 @@ def test_mcm_fused_stacks_match_layerwise(tmae):
                           "yh": ex.YH.float().clone(), "musig": ex.MUSIG.clone(),
                           "lrp": (ex.YH.float() - ex.YPRE).clone()}
     finally:
-        if old is None:
-            os.environ.pop("TMAE_LIC_STACK", None)
-        else:
-            os.environ["TMAE_LIC_STACK"] = old
-        if old_chain is None:
-            os.environ.pop("TMAE_LIC_CHAIN", None)
-        else:
-            os.environ["TMAE_LIC_CHAIN"] = old_chain
+        ex_cls.USE_LIC_STACK = True
+        ex_cls.USE_LIC_CHAIN = True
         m._exec = None
     a, b = outs["1"], outs["0"]
     flips = int(((a["yh"] - b["yh"]).abs() > 0.5).sum())
@@ -170,11 +163,13 @@ def test_mcm_fused_stacks_match_layerwise(tmae):
     check("log_ylik_meandiff", float(ly.mean()), 1e-3)
 
 
-@pytest.mark.parametrize("training,batched", [(False, "0"), (True, "0"), (False, "1")])
-def test_mcm_chained_slices_bitwise(tmae, training, batched, monkeypatch):
+@pytest.mark.parametrize("training", [False, True])
+def test_mcm_chained_slices_bitwise(tmae, training):
     """serial slices chained (mean stack -> y_hat_pre -> lrp stack in one launch, likelihoods deferred) against
     the separate mean/scale, Gaussian and lrp launches: the same arithmetic in the same order, so x_hat, both
     likelihoods and y_hat are bitwise equal (eval, and train-mode quantisation noise injected)"""
+    from textmae_amd import mcm as mcm_mod
+
     torch.manual_seed(4)
     m = tmae.MCM(img_size=256, num_keep_patches=144).to(DEV).eval()
     m.compute_dtype = torch.bfloat16
@@ -182,12 +177,11 @@ def test_mcm_chained_slices_bitwise(tmae, training, batched, monkeypatch):
     imgs = torch.randn(6, 3, 256, 256, device=DEV)
     scores = torch.rand(6, 256, device=DEV)
     noise = (torch.rand(6, 192, 3, 3, device=DEV) - 0.5, torch.rand(6, 384, 12, 12, device=DEV) - 0.5)
-    monkeypatch.setenv("TMAE_LIC_CHAIN_B", batched)  # slices 6..11 chained as well
     outs = {}
-    old = os.environ.get("TMAE_LIC_CHAIN")
+    ex_cls = mcm_mod._Executor
     try:
         for flag in ("1", "0"):
-            os.environ["TMAE_LIC_CHAIN"] = flag
+            ex_cls.USE_LIC_CHAIN = flag == "1"
             m._exec = None
             m.train(training)
             with torch.no_grad():
@@ -195,10 +189,7 @@ def test_mcm_chained_slices_bitwise(tmae, training, batched, monkeypatch):
             outs[flag] = (o["x_hat"].clone(), o["likelihoods"]["y"].clone(), o["likelihoods"]["z"].clone(),
                           m._exec.YH.clone())
     finally:
-        if old is None:
-            os.environ.pop("TMAE_LIC_CHAIN", None)
-        else:
-            os.environ["TMAE_LIC_CHAIN"] = old
+        ex_cls.USE_LIC_CHAIN = True
         m._exec = None
         m.eval()
     for a, b in zip(outs["1"], outs["0"]):

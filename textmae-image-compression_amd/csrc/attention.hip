@@ -241,7 +241,7 @@ static int mha_launch(const void* qkv, void* out, int B, int Tn, int H, float sc
   const int Tpad = (Tn + 31) / 32 * 32;
   constexpr bool lean_ok = sizeof(T) == 2 && DH % 32 == 0;  // the VALU-lean kernel takes whole 32-wide tiles
   constexpr int DHP = (DH + 31) / 32 * 32;
-  const bool lean = lean_ok && !getenv("TMAE_MHA_PLAIN");
+  const bool lean = lean_ok;  // the plain kernel: f32 and the ViT-H head dim 80 (lean: 18 vs 23 us enc, 30 vs 44 dec)
   const int nthr = 64 * (Tpad / 32);
   const size_t lds = lean ? ((size_t)Tpad * (DH + 8) + (size_t)Tpad * AttnTr<DH>::LDV) * 2
                           : ((size_t)Tpad * (DH + AttnCfg<T>::KPAD) + (size_t)DHP * (Tpad + AttnCfg<T>::VPAD)) * sizeof(T);

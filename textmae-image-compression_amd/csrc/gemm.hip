@@ -368,11 +368,6 @@ extern "C" int tmae_gemm_plan(int M, int N, int K, int batch, int dtype, char* o
   TMAE_REQUIRE(out != nullptr && len > 0 && M >= 0 && N >= 0 && K >= 0 && batch >= 1, "tmae_gemm_plan: bad arguments");
   const bool bf = dtype == TMAE_BF16;
   const TileChoice tc = choose_tile(M, N, K, batch, bf);
-  if (tc.nw == 8 && gemm_knob("TMAE_GEMM_RING", 0))
-    snprintf(out, len, "ring<bf16,%dx%d,8w,BK32x4>", tc.bn, tc.bm);
-  else if (tc.nw == 8 && gemm_knob("TMAE_GEMM_PHASED", 0))
-    snprintf(out, len, "phased<bf16,%dx%d,8w,BK64,4ph>", tc.bn, tc.bm);
-  else
-    snprintf(out, len, "glds<%s,%dx%d,%dw,BK%dx2>", bf ? "bf16" : "f32", tc.bn, tc.bm, tc.nw, bf ? 64 : 32);
+  snprintf(out, len, "glds<%s,%dx%d,%dw,BK%dx2>", bf ? "bf16" : "f32", tc.bn, tc.bm, tc.nw, bf ? 64 : 32);
   return TMAE_OK;
 }

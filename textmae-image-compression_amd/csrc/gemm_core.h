@@ -391,7 +391,7 @@ __device__ __forceinline__ void gemm_ring_wait(int younger) {
 // whole DMA latency every step): NS - 1 steps in flight.
 template <typename T, int BN, int BM, int WGN, int NW, class WS, class XS, class EPI, int NS = 2>
 __global__ void __launch_bounds__(64 * NW, NW == 8 ? 1 : 2)
-gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
+gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
   constexpr int BKE = 8 * Elt<T>::EPC;
   constexpr int WGM = NW / WGN;
   constexpr int WN = BN / WGN, WM = BM / WGM;
@@ -431,7 +431,6 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
   const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
   auto issue = [&](int stage, int kt) {
-    if (diag & 4) return;  // timing diagnostic: no staging
     const unsigned sb = lds_base + (unsigned)stage * ROWS * 128u;
     if (kt * BKE + BKE <= K) {  // whole K-step: sources with addr_full skip the per-lane bounds select
 #pragma unroll
@@ -465,9 +464,7 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
     int stage = 0;
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) issue(stage ^ 1, kt + 1);
-      if (diag & 8) __builtin_amdgcn_s_setprio(1);
-      if (!(diag & 2)) mfma_tile<T, BN, WN, WM, TN, TM>(lds + stage * ROWS * 8, wn, wm, lane, acc);
-      if (diag & 8) __builtin_amdgcn_s_setprio(0);
+      mfma_tile<T, BN, WN, WM, TN, TM>(lds + stage * ROWS * 8, wn, wm, lane, acc);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       stage ^= 1;
@@ -488,333 +485,8 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
     }
   }
   static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= NS * ROWS * 128, "epilogue region exceeds the LDS ring");
-  if (!(diag & 1))
-    epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
-                             tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
-}
-
-// ------------------------------------------------------------------ phased kernel (8 waves, 256x256, bf16)
-// cdna_hip_programming.md §5 "256^2 8-phase template", restated for this core's sources and epilogues.
-// A K-tile (64 deep) runs as 4 phases, one per output quadrant of every wave (W-half qa x X-half qb of the
-// wave's 128 x 64 block): (qa0,qb0) (qa0,qb1) (qa1,qb0) (qa1,qb1); fragments are read once per tile
-// (W-qa0 + X-qb0 in phase 0, X-qb1 in 1, W-qa1 in 2, nothing in 3) and kept in registers.
-// The tile image is cut into four "half-tiles" of 128 LDS rows each (W-qa0, X-qb0, X-qb1, W-qa1, the order
-// their regions are released); every phase issues ONE half-tile (2 LDS-DMA per thread) of the tile two
-// ahead into the region the previous phase released, so 5 half-tiles stay in flight: a uniform counted
-// s_waitcnt vmcnt(10) + raw s_barrier closes every phase (never vmcnt(0) in the loop).
-//   issue order: p0(t): W-qa1(t+1)  p1(t): W-qa0(t+2)  p2(t): X-qb0(t+2)  p3(t): X-qb1(t+2)
-// RAW: a half-tile read in phase p was retired by the vmcnt before the barrier closing phase p-1.
-// WAR: each region is restaged one phase after the phase whose barrier follows its last ds_read.
-__device__ __forceinline__ void s_barrier_raw() { __builtin_amdgcn_s_barrier(); }
-
-template <class WS, class XS, class EPI>
-__global__ void __launch_bounds__(512, 1)
-gemm_phased_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
-  constexpr int BN = 256, BM = 256, NW = 8, WGN = 2;
-  constexpr int WN = 128, WM = 64, TN = 8, TM = 4;
-  constexpr int IMG_W = BN * 128, STAGE = (BN + BM) * 128;  // bytes
-  __shared__ __attribute__((aligned(16))) uint4 lds[2 * STAGE / 16];
-
-  const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
-  ws.batch(b1, b2);
-  xs.batch(b1, b2);
-  epi.batch(b1, b2);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave % WGN, wm = wave / WGN;
-  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
-  const int nk = (K + 63) / 64;
-  int tn, tm;
-  tile_order(xcd_remap(blockIdx.x, gridDim.x), ntn, ntm, tn, tm);
-
-  // DMA slots: half-tile h (0 W-qa0, 1 X-qb0, 2 X-qb1, 3 W-qa1), round r: this wave's 8 image rows
-  const int w8 = 8 * wave, lr = lane >> 3, pch = lane & 7;
-  int row0[4][2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    row0[0][r] = 128 * r + w8;                                  // W rows {0-63, 128-191}
-    row0[3][r] = 128 * r + 64 + w8;                             // W rows {64-127, 192-255}
-    row0[1][r] = 128 * r + 64 * (wave >> 2) + 8 * (wave & 3);    // X rows {0-31,64-95 | 128-159,192-223}
-    row0[2][r] = row0[1][r] + 32;
-  }
-  typename WS::Row wrow[2][2];
-  typename XS::Row xrow[2][2];
-  int chk[4][2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-#pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int row = row0[h][r] + lr;
-      chk[h][r] = pch ^ ((row >> 1) & 7);
-    }
-    wrow[0][r] = ws.row(tn * BN + row0[0][r] + lr);
-    wrow[1][r] = ws.row(tn * BN + row0[3][r] + lr);
-    xrow[0][r] = xs.row(tm * BM + row0[1][r] + lr);
-    xrow[1][r] = xs.row(tm * BM + row0[2][r] + lr);
-  }
-  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
-  const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // rows 8*wave.. of each half-tile round, as LDS byte offsets (wave-uniform)
-  auto issue = [&](int h, int kt) {
-    const unsigned sb = lds_base + (unsigned)(kt & 1) * STAGE;
-    const bool live = kt < nk;
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      unsigned rowu;
-      const void* src;
-      if (h == 0 || h == 3) {
-        rowu = (h == 0 ? 128u * r : 128u * r + 64u) + 8u * wave_u;
-        src = live ? ws.addr(wrow[h == 3][r], kt, chk[h][r]) : (const void*)g_tmae_zero_page;
-        glds16(src, sb + rowu * 128u);
-      } else {
-        rowu = 128u * r + 64u * (wave_u >> 2) + 8u * (wave_u & 3) + (h == 2 ? 32u : 0u);
-        src = live ? xs.addr(xrow[h == 2][r], kt, chk[h][r]) : (const void*)g_tmae_zero_page;
-        glds16(src, sb + IMG_W + rowu * 128u);
-      }
-    }
-  };
-
-  f32x4 acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fq = lane >> 4;
-  bf16x8 wa[4][2], xb0[2][2], xb1[2][2];
-  auto read_w = [&](const uint4* base, int qa) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int r = wn * WN + 16 * (4 * qa + i) + fr;
-        const int c = 4 * s + fq;
-        uint4 u = base[r * 8 + (c ^ ((r >> 1) & 7))];
-        wa[i][s] = *reinterpret_cast<bf16x8*>(&u);
-      }
-  };
-  auto read_x = [&](const uint4* base, int qb, bf16x8 (&xb)[2][2]) {
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int r = wm * WM + 16 * (2 * qb + j) + fr;
-        const int c = 4 * s + fq;
-        uint4 u = base[(BN + r) * 8 + (c ^ ((r >> 1) & 7))];
-        xb[j][s] = *reinterpret_cast<bf16x8*>(&u);
-      }
-  };
-  auto mfma_q = [&](int qa, int qb, const bf16x8 (&xb)[2][2]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[4 * qa + i][2 * qb + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[i][s], xb[j][s], acc[4 * qa + i][2 * qb + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto close_phase = [&]() {
-    asm volatile("s_waitcnt vmcnt(10)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
-    s_barrier_raw();
-  };
-
-  if (nk > 0) {
-    // prologue: tile 0 complete, tile 1's first three half-tiles (the steady-state picture at a tile start)
-    issue(0, 0); issue(1, 0); issue(2, 0); issue(3, 0);
-    issue(0, 1); issue(1, 1); issue(2, 1);
-    close_phase();
-    for (int kt = 0; kt < nk; ++kt) {
-      const uint4* base = lds + (kt & 1) * (STAGE / 16);
-      // phase 0: (qa0, qb0)
-      issue(3, kt + 1);
-      read_w(base, 0);
-      read_x(base, 0, xb0);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_q(0, 0, xb0);
-      close_phase();
-      // phase 1: (qa0, qb1)
-      issue(0, kt + 2);
-      read_x(base, 1, xb1);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_q(0, 1, xb1);
-      close_phase();
-      // phase 2: (qa1, qb0)
-      issue(1, kt + 2);
-      read_w(base, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_q(1, 0, xb0);
-      close_phase();
-      // phase 3: (qa1, qb1)
-      issue(2, kt + 2);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_q(1, 1, xb1);
-      close_phase();
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the look-ahead DMA lands before the ring is reused
-  s_barrier_raw();
-  static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= 2 * STAGE, "epilogue region exceeds the LDS ring");
   epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
                            tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
-}
-
-// ------------------------------------------------------------------ ring kernel (8 waves, bf16)
-// BK = 32 (64-B LDS rows, 4 x 16-B chunks), a 4-slot LDS ring of (BN+BM) x 64 B, up to 4 K-steps of
-// LDS-DMA in flight, and the MFMA fragments register-double-buffered: right after the barrier that
-// certifies step k+1 has landed, every wave issues step k+1's ds_reads and only then runs step k's
-// MFMAs (from registers read one iteration earlier), so the LDS latency hides under the MFMAs
-// instead of draining the pipe at every barrier (the 2-stage kernel above runs its MFMA phase alone
-// at ~60 % of peak, all waves waiting on their first fragments together).  The slot of step k is
-// refilled with step k+4 once every wave holds step k's fragments.  Counted s_waitcnt vmcnt and a
-// raw s_barrier: a __syncthreads fence would drain every DMA in flight.
-// Chunk c of row r sits in slot c ^ (((r >> 3) & 1) << 1): the 16-row x 4-chunk ds_read_b128
-// fragment reads are conflict-free in all four lane groups (exhaustive search over the
-// MI355X_MICROARCH.md lane-group table).
-template <int N>
-__device__ __forceinline__ void wait_vm_barrier() {
-  static_assert(N == 0 || N == 4 || N == 8 || N == 12, "ring depth");
-  if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-
-__device__ __forceinline__ int ring_slot(int r, int c) { return c ^ (((r >> 3) & 1) << 1); }
-
-template <int BN, int BM, int WGN, class WS, class XS, class EPI>
-__global__ void __launch_bounds__(512, 1)
-gemm_ring_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2, int diag) {
-  constexpr int NW = 8, BK = 32, NS = 4;
-  constexpr int WGM = NW / WGN;
-  constexpr int WN = BN / WGN, WM = BM / WGM;
-  constexpr int TN = WN / 16, TM = WM / 16;
-  constexpr int ROWS = BN + BM;
-  constexpr int PIECES = ROWS / 16 / NW;  // 1-KiB DMA pieces per wave per stage (16 rows x 64 B)
-  constexpr int WP = BN / 16 / NW;        // of which weight pieces
-  constexpr int STAGE = ROWS * 64;        // bytes
-  static_assert(TN >= 1 && TM >= 1 && PIECES == 4 && BN % (16 * NW) == 0 && BM % (16 * NW) == 0, "bad tile");
-  static_assert(TN % 2 == 0, "MFMA halves split over the weight fragments");
-  __shared__ __attribute__((aligned(16))) uint4 lds[NS * STAGE / 16];
-
-  const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
-  ws.batch(b1, b2);
-  xs.batch(b1, b2);
-  epi.batch(b1, b2);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave % WGN, wm = wave / WGN;
-  const int ntn = (N + BN - 1) / BN, ntm = (M + BM - 1) / BM;
-  const int nk = (K + BK - 1) / BK;
-  int tn, tm;
-  tile_order(xcd_remap(blockIdx.x, gridDim.x), ntn, ntm, tn, tm);
-
-  // DMA piece p of this wave: rows 16 * (wave + NW p) + (lane >> 2), slot lane & 3
-  const int prow = lane >> 2, pslot = lane & 3;
-  typename WS::Row wrow[WP];
-  typename XS::Row xrow[PIECES - WP];
-  int koff[PIECES];
-#pragma unroll
-  for (int p = 0; p < PIECES; ++p) {
-    const int r = 16 * (wave + NW * p) + prow;  // tile row (weights first)
-    koff[p] = 8 * ring_slot(r, pslot);           // source chunk for this LDS slot
-    if (p < WP) wrow[p] = ws.row(tn * BN + r);
-    else xrow[p - WP] = xs.row(tm * BM + r - BN);
-  }
-  const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
-  const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool dma = !(diag & 4);
-  auto issue = [&](int p, int kt) {
-    const unsigned dst = lds_base + (unsigned)(kt & (NS - 1)) * STAGE + (wave_u + NW * p) * 1024u;
-    if (p < WP) glds16(ws.addr_k(wrow[p], kt * BK + koff[p]), dst);
-    else glds16(xs.addr_k(xrow[p - WP], kt * BK + koff[p]), dst);
-  };
-
-  f32x4 acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fq = lane >> 4;
-  int aoff[TN], boff[TM];  // byte offsets of this lane's fragments inside a stage
-#pragma unroll
-  for (int i = 0; i < TN; ++i) {
-    const int r = wn * WN + 16 * i + fr;
-    aoff[i] = r * 64 + 16 * ring_slot(r, fq);
-  }
-#pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    const int r = BN + wm * WM + 16 * j + fr;
-    boff[j] = r * 64 + 16 * ring_slot(r, fq);
-  }
-  bf16x8 a[2][TN], b[2][TM];
-  auto read_frags = [&](int kt, int set) {
-    const char* stage = reinterpret_cast<const char*>(lds) + (kt & (NS - 1)) * STAGE;
-#pragma unroll
-    for (int i = 0; i < TN; ++i) a[set][i] = *reinterpret_cast<const bf16x8*>(stage + aoff[i]);
-#pragma unroll
-    for (int j = 0; j < TM; ++j) b[set][j] = *reinterpret_cast<const bf16x8*>(stage + boff[j]);
-  };
-  auto mfma_half = [&](int set, int i0) {
-#pragma unroll
-    for (int i = i0; i < i0 + TN / 2; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[set][i], b[set][j], acc[i][j], 0, 0, 0);
-  };
-
-  if (nk > 0) {
-    if (dma) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s)
-        if (s < nk) {
-#pragma unroll
-          for (int p = 0; p < PIECES; ++p) issue(p, s);
-        }
-    }
-    const int ahead = dma ? min(NS - 1, nk - 1) : 0;  // stages allowed in flight once stage 0 landed
-    if (ahead == 3) wait_vm_barrier<3 * PIECES>();
-    else if (ahead == 2) wait_vm_barrier<2 * PIECES>();
-    else if (ahead == 1) wait_vm_barrier<PIECES>();
-    else wait_vm_barrier<0>();
-    read_frags(0, 0);
-  }
-  // two iterations per loop trip so the fragment sets are compile-time indices
-  auto step = [&](int kt, int cur) {
-    if (kt + 1 < nk) {
-      const int after = dma ? min(kt + NS - 1, nk - 1) - (kt + 1) : 0;
-      if (after >= 2) wait_vm_barrier<2 * PIECES>();
-      else if (after == 1) wait_vm_barrier<PIECES>();
-      else wait_vm_barrier<0>();
-      read_frags(kt + 1, cur ^ 1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (diag & 8) __builtin_amdgcn_s_setprio(1);
-    if (!(diag & 2)) mfma_half(cur, 0);
-    if (diag & 8) __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    if (dma && kt + NS < nk) {
-#pragma unroll
-      for (int p = 0; p < PIECES; ++p) issue(p, kt + NS);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (diag & 8) __builtin_amdgcn_s_setprio(1);
-    if (!(diag & 2)) mfma_half(cur, TN / 2);
-    if (diag & 8) __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    step(kt, 0);
-    step(kt + 1, 1);
-  }
-  if (kt < nk) step(kt, 0);
-  wait_vm_barrier<0>();  // every wave is done with the ring before it becomes the epilogue buffer
-  static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= NS * STAGE, "epilogue region exceeds the LDS ring");
-  if (!(diag & 1))
-    epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
-                             tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
 }
 
 // ------------------------------------------------------------------ register-staged kernel
@@ -889,25 +561,17 @@ gemm_reg_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
 }
 
 // ------------------------------------------------------------------ launch with tile selection
-// host-side tuning knobs (environment, read once): experiments without rebuilding
-static inline int gemm_knob(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-
 struct TileChoice { int bn, bm, nw; };
 
-// Tile candidates: 4-wave tiles run 2 workgroups per CU, the 8-wave 256x256 tile one (128 KiB LDS).
+// Tile candidates: 4-wave tiles run 2 workgroups per CU, the 8-wave 256x256 / 256x192 tiles one (128 KiB LDS).
 // Score = (useful fraction of the padded MFMA work) x (tail quantisation: tiles / (rounds x slots))
-// x (relative per-CU throughput of the tile shape at full occupancy).  TMAE_GEMM_TILE=<index>
-// forces a candidate (tuning experiments without rebuilding).
+// x (relative per-CU throughput of the tile shape at full occupancy).
 // The 8-wave 256 x 192 tile (waves 2 x 4, 128 x 48 each) exists for the tail: 9280- and 16448-row token
 // GEMMs whose 256 x 256 tile count lands just past a multiple of 256 CUs (enc qkv 333 tiles = 1.3
 // rounds, dec fc1 520 = 2.03, dec proj/fc2 130 = 0.5).
-static constexpr int kNumTiles = 10;
-static constexpr int kTileCand[kNumTiles][3] = {{256, 256, 8}, {128, 128, 4}, {64, 128, 4}, {32, 128, 4},
-                                                {64, 64, 4},   {32, 64, 4},   {256, 192, 8}, {128, 160, 4},
-                                                {192, 128, 4}, {128, 192, 4}};
+static constexpr int kNumTiles = 9;
+static constexpr int kTileCand[kNumTiles][3] = {{256, 256, 8}, {128, 128, 4}, {64, 128, 4}, {32, 128, 4}, {64, 64, 4},
+                                                {32, 64, 4},   {256, 192, 8}, {128, 160, 4}, {128, 192, 4}};
 // candidates only the bf16 LDS-DMA path instantiates
 static inline bool tile_bf16_only(int i) { return kTileCand[i][2] == 8 || i >= 7; }
 // eff = per-CU throughput relative to two 128 x 128 workgroups.  Forced-tile runs of the bench's token
@@ -924,24 +588,23 @@ static inline bool tile_bf16_only(int i) { return kTileCand[i][2] == 8 || i >= 7
 // 1.35, 7824 without the tile).
 // 128 x 192 (waves 2 x 2, 64 x 96 each; 80 KiB LDS, exactly two per CU): enc qkv 42.2 us vs 49.6 on
 // 256 x 192, dec fc1 54.6 vs 56.4 on 128 x 160; e = 1.25 inside the (1.10, 1.46) window those runs
-// leave (whole forward 8108 img/s vs 8041 without it).  192 x 128 was never the best tile (off).
+// leave (whole forward 8108 img/s vs 8041 without it).  Round 3 re-check at HEAD (profiles/r03/
+// s2_gemm_tiles_c13.log, s2_knob_c13_*): the pick within 3 % of the best forced tile on every token GEMM;
+// the efficiencies moved by +-20 % changed the forward by -2 % .. +0.3 %.  (192 x 128 never won: dropped.)
+// Tuning experiments override these with a variant build (tools/build_variant.sh -DTMAE_GEMM_TILE=<i>).
+#ifndef TMAE_GEMM_TILE
+#define TMAE_GEMM_TILE -1
+#endif
 static inline TileChoice choose_tile(int M, int N, int K, int batch, bool allow_big) {
   const double kf = 1.0 + 0.12 * std::log2(std::max(K, 768) / 768.0);
-  static const double e256 = gemm_knob("TMAE_GEMM_E256", 110) / 100.0;  // knobs: percent, for A/B runs
-  static const double e192 = gemm_knob("TMAE_GEMM_E192", 108) / 100.0;
-  static const double e160 = gemm_knob("TMAE_GEMM_E160", 122) / 100.0;
-  static const double e192n = gemm_knob("TMAE_GEMM_E192N", 0) / 100.0;  // 192 x 128: never best, off
-  static const double e192m = gemm_knob("TMAE_GEMM_E192M", 125) / 100.0;
-  const double eff[kNumTiles] = {e256 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, e192 * kf, e160, e192n, e192m};
-  const int forced = gemm_knob("TMAE_GEMM_TILE", -1);
+  const double eff[kNumTiles] = {1.10 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, 1.08 * kf, 1.22, 1.25};
+  constexpr int forced = TMAE_GEMM_TILE;
   if (forced >= 0 && forced < kNumTiles && (allow_big || !tile_bf16_only(forced)))
     return TileChoice{kTileCand[forced][0], kTileCand[forced][1], kTileCand[forced][2]};
-  const bool t192 = gemm_knob("TMAE_GEMM_T192", 1) != 0;
   double best = -1.0;
   TileChoice tc{128, 128, 4};
   for (int i = 0; i < kNumTiles; ++i) {
     if (tile_bf16_only(i) && !allow_big) continue;
-    if (i == 6 && !t192) continue;
     const int bn = kTileCand[i][0], bm = kTileCand[i][1];
     const double tn = ceil_div(N, bn), tm = ceil_div(M, bm);
     const double useful = ((double)N / (tn * bn)) * ((double)M / (tm * bm));
@@ -961,42 +624,22 @@ static int launch_one(const char* name, const WS& ws, const XS& xs, const EPI& e
   if (tiles == 0 || n1 * n2 == 0) return TMAE_OK;
   if constexpr (GLDS) {
     // small tiles over a long K take a 4-stage (<= 160 LDS rows) or 3-stage (<= 213 rows) ring: either stays
-    // within 80 KB, two workgroups per CU (TMAE_GEMM_DEEP=0 disables)
+    // within 80 KB, two workgroups per CU (LIC conv family 1129 -> 1095 us per forward)
     constexpr int DNS = (BN + BM) * 128 * 4 <= 80 * 1024 ? 4 : (BN + BM) * 128 * 3 <= 80 * 1024 ? 3 : 2;
     constexpr bool deep_ok = sizeof(T) == 2 && NW == 4 && DNS > 2;
     if constexpr (deep_ok) {
-      if (ceil_div(K, 8 * Elt<T>::EPC) >= 8 && gemm_knob("TMAE_GEMM_DEEP", 1)) {
+      if (ceil_div(K, 8 * Elt<T>::EPC) >= 8) {
         hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, NW, WS, XS, EPI, DNS>), dim3(tiles, n1 * n2),
-                           dim3(64 * NW), 0, st, ws, xs, epi, M, N, K, n2, 0);
+                           dim3(64 * NW), 0, st, ws, xs, epi, M, N, K, n2);
         TMAE_LAUNCH_CHECK(name);
       }
     }
     hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, NW, WS, XS, EPI>), dim3(tiles, n1 * n2), dim3(64 * NW), 0,
-                       st, ws, xs, epi, M, N, K, n2, gemm_knob("TMAE_GEMM_DIAG", 0));
+                       st, ws, xs, epi, M, N, K, n2);
   } else {
     hipLaunchKernelGGL((gemm_reg_kernel<T, BN, BM, WGN, WS, XS, EPI>), dim3(tiles, n1 * n2), dim3(256), 0, st, ws, xs,
                        epi, M, N, K, n2);
   }
-  TMAE_LAUNCH_CHECK(name);
-}
-
-template <int BN, int BM, int WGN, class WS, class XS, class EPI>
-static int launch_ring(const char* name, const WS& ws, const XS& xs, const EPI& epi, int M, int N, int K, int n1,
-                       int n2, hipStream_t st) {
-  const int tiles = ceil_div(N, BN) * ceil_div(M, BM);
-  if (tiles == 0 || n1 * n2 == 0) return TMAE_OK;
-  hipLaunchKernelGGL((gemm_ring_kernel<BN, BM, WGN, WS, XS, EPI>), dim3(tiles, n1 * n2), dim3(512), 0, st, ws, xs, epi,
-                     M, N, K, n2, gemm_knob("TMAE_GEMM_DIAG", 0));
-  TMAE_LAUNCH_CHECK(name);
-}
-
-template <class WS, class XS, class EPI>
-static int launch_phased(const char* name, const WS& ws, const XS& xs, const EPI& epi, int M, int N, int K, int n1,
-                         int n2, hipStream_t st) {
-  const int tiles = ceil_div(N, 256) * ceil_div(M, 256);
-  if (tiles == 0 || n1 * n2 == 0) return TMAE_OK;
-  hipLaunchKernelGGL((gemm_phased_kernel<WS, XS, EPI>), dim3(tiles, n1 * n2), dim3(512), 0, st, ws, xs, epi, M, N, K,
-                     n2);
   TMAE_LAUNCH_CHECK(name);
 }
 
@@ -1009,13 +652,8 @@ static int launch_gemm(const char* name, const T* w, long long ws1, long long ws
   if constexpr (GLDS && sizeof(T) == 2) {
     if (tc.nw == 8 && tc.bm == 192) return launch_one<GLDS, T, 256, 192, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 4 && tc.bm == 160) return launch_one<GLDS, T, 128, 160, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
-    if (tc.nw == 4 && tc.bn == 192) return launch_one<GLDS, T, 192, 128, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 4 && tc.bm == 192) return launch_one<GLDS, T, 128, 192, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
-    if (tc.nw == 8) {
-      if (gemm_knob("TMAE_GEMM_RING", 0)) return launch_ring<256, 256, 2>(name, ws, xs, epi, M, N, K, n1, n2, st);
-      if (gemm_knob("TMAE_GEMM_PHASED", 0)) return launch_phased(name, ws, xs, epi, M, N, K, n1, n2, st);
-      return launch_one<GLDS, T, 256, 256, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
-    }
+    if (tc.nw == 8) return launch_one<GLDS, T, 256, 256, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
   }
   if (tc.bn == 128) return launch_one<GLDS, T, 128, 128, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
   if (tc.bn == 64 && tc.bm == 128) return launch_one<GLDS, T, 64, 128, 1, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);

@@ -90,15 +90,9 @@ static int ln_launch(const float* x, const float* g, const float* b, void* y, in
                      float eps, hipStream_t st) {
   if (rows == 0) return TMAE_OK;
   const int vpl = ceil_div(D / 4, 64);
-  // several rows per wave (opt-in) only when that still leaves >= 2 waves per SIMD
-  static const int rpw_max = [] {
-    const char* e = getenv("TMAE_LN_RPW");
-    return e ? atoi(e) : 1;
-  }();
-  const int rpw = (rpw_max >= 4 && vpl <= 4 && rows >= 4 * 2048) ? 4
-                  : (rpw_max >= 2 && rows >= 2 * 2048)             ? 2
-                                                                   : 1;
-  const int grid = ceil_div(rows, 4 * rpw);
+  // one row per wave: 2 or 4 rows per wave (gamma / beta loaded once per wave) measured slower (390 vs 348 us per
+  // forward, profiles/r02/bench_call40_ln_rpw*.log) -- fewer waves hide less latency
+  const int grid = ceil_div(rows, 4);
 #define TMAE_LN(V, R) hipLaunchKernelGGL((layernorm_kernel<OT, V, R>), dim3(grid), dim3(256), 0, st, x, g, b, (OT*)y, rows, D, G, Gs, off, eps)
 #define TMAE_LN_V(R)            \
   if (vpl <= 1) TMAE_LN(1, R);  \
@@ -106,13 +100,7 @@ static int ln_launch(const float* x, const float* g, const float* b, void* y, in
   else if (vpl <= 3) TMAE_LN(3, R); \
   else if (vpl <= 4) TMAE_LN(4, R); \
   else TMAE_LN(8, R);
-  if (rpw == 4) {
-    TMAE_LN_V(4)
-  } else if (rpw == 2) {
-    TMAE_LN_V(2)
-  } else {
-    TMAE_LN_V(1)
-  }
+  TMAE_LN_V(1)
 #undef TMAE_LN_V
 #undef TMAE_LN
   TMAE_LAUNCH_CHECK("tmae_layernorm_fwd");

@@ -321,6 +321,11 @@ class _Executor:
         so their mean/scale stacks, Gaussian likelihoods and lrp stacks run batched (12 / 6 problems).
     """
 
+    # reference paths the tests compare the fused LIC launches against (bitwise / bounded): False selects the
+    # per-layer conv launches (the f32 parity path's structure) or the unchained serial slices
+    USE_LIC_STACK = True
+    USE_LIC_CHAIN = True
+
     def __init__(self, m: MCM, batch, dtype, device):
         self.m, self.batch, self.dtype, self.device = m, batch, dtype, device
         self._sig = None
@@ -375,8 +380,8 @@ class _Executor:
         c0 = self.mid[0]
         self.PW = 3 * S * c0  # partial sums: [mean (S*c0) | lrp (S*c0) | scale (S*c0)]
         self.Pbuf = z(Mp, self.PW)
-        # side stream for the partial sums under the serial slice steps (_slices); TMAE_LIC_OVERLAP=0 disables
-        self.overlap = os.environ.get("TMAE_LIC_OVERLAP", "1") != "0" and torch.device(dev).type == "cuda"
+        # side stream for the partial sums under the serial slice steps (_slices)
+        self.overlap = torch.device(dev).type == "cuda"
         self.side_stream = torch.cuda.Stream(device=dev) if self.overlap else None
         self.SUPY = z(Mp, M, dtype=dt)    # y_hat slices (post-LRP for i < maxsup; pre-LRP for the batched ones)
         self.YPRE = z(Mp, M)              # f32 pre-LRP y_hat = round(y - mu) + mu
@@ -474,7 +479,7 @@ class _Executor:
         # fused slice-transform stacks (lic_stack.hip): every layer packed in MFMA fragment order, problems
         # stacked like the per-layer launches above; bf16 only, shapes that fit one workgroup's LDS
         self.lstk = None
-        if (dt == torch.bfloat16 and os.environ.get("TMAE_LIC_STACK", "1") != "0" and sw % 8 == 0
+        if (dt == torch.bfloat16 and self.USE_LIC_STACK and sw % 8 == 0
                 and ops.lic_stack_fits(self.g, sw * (ms + 1), self.mid)):
             pk = ops.pack_lic_stack_weight
 
@@ -840,10 +845,10 @@ class _Executor:
 
         # slices 0..ms-1: serial (slice i conditions on y_hat 0..i-1)
         fused = self.lstk is not None
-        # serial slices as ONE launch each (TMAE_LIC_CHAIN=0 disables): the mean stack's workgroups go on with
-        # the slice's lrp stack (y_hat_pre = round(y - mu) + mu in between), the scale stacks run beside them;
-        # the slices' Gaussian likelihoods follow the loop in one launch (nothing in the chain reads them)
-        chain = fused and chain_ok and os.environ.get("TMAE_LIC_CHAIN", "1") != "0"
+        # serial slices as ONE launch each: the mean stack's workgroups go on with the slice's lrp stack
+        # (y_hat_pre = round(y - mu) + mu in between), the scale stacks run beside them; the slices' Gaussian
+        # likelihoods follow the loop in one launch (nothing in the chain reads them)
+        chain = fused and chain_ok and self.USE_LIC_CHAIN
         ms_ser = self.MS_SER.data_ptr()
         yv = self.Y32.data_ptr()
 
@@ -876,27 +881,9 @@ class _Executor:
                 lrp_fused(i, 1)
             else:
                 lrp_stack(self.lrp_first[i], self.lrp_layers[i], i, 1)
-        # slices ms..S-1: batched on the fixed support y_hat 0..ms-1
-        chain_b = chain and os.environ.get("TMAE_LIC_CHAIN_B", "0") != "0"
-        if nb > 0 and chain_b:  # 2 x nb problems, the mean ones chained into their lrp stacks
-            wait_pre(ms)
-            bw, (first, layers) = self.lstk["b_ms"], (self.b_ms_first, self.b_ms_layers)
-            bs_ = [first[1]] + [b for _, b in layers]
-            st = {"a": (off_scale - off_mean, c0), "y": (S * Mp * sw, Mp * sw)}
-            for l, (w, b) in enumerate(zip(bw, bs_)):
-                st[f"w{l}"] = (w[0].numel(), w[0][0].numel())
-                st[f"b{l}"] = (b[0].numel(), b.shape[-1])
-            lw = self.lstk["b_lrp"]
-            lb_ = [self.b_lrp_first[1]] + [b for _, b in self.b_lrp_layers]
-            cst = {"y": sw, "ypre": sw, "add": c0, "out": sw}
-            for l, (w, b) in enumerate(zip(lw, lb_)):
-                cst[f"w{l}"], cst[f"b{l}"] = w[0].numel(), b.shape[-1]
-            ch = dict(w=lw, b=lb_, couts=mid, x1=supy, c1=sw * ms, ld1=M, y=yv + ms * sw * e4, ldy=M,
-                      add=pbase + (off_lrp + ms * c0) * eP, ld_add=Pw, ypre=ypre + ms * sw * e4, ld_ypre=M,
-                      out=yh + ms * sw * esz, ld_out=M, strides=cst)
-            ops.lic_stack(B, g, supy, sw * ms, M, bw, bs_, mid, ms_ser + ms * Mp * sw * e4, sw, True,
-                          addend=pbase + (off_mean + ms * c0) * eP, ld_add=Pw, nb=(2, nb), strides=st, chain=ch)
-        elif nb > 0:
+        # slices ms..S-1: batched on the fixed support y_hat 0..ms-1 (chaining them into their lrp stacks as
+        # well measured slower, round 3)
+        if nb > 0:
             wait_pre(ms)
             if fused:
                 ms_fused(ms, nb)
@@ -908,6 +895,6 @@ class _Executor:
             else:
                 lrp_stack(self.b_lrp_first, self.b_lrp_layers, ms, nb, x2=supy + ms * sw * esz)
         if chain:  # likelihoods of the chained slices (overwrites their dead SUPY / YPRE slots)
-            gc_step(0, S if (nb > 0 and chain_b) else ms, ms_ser, ms_ser + S * Mp * sw * e4, Mp * sw)
+            gc_step(0, ms, ms_ser, ms_ser + S * Mp * sw * e4, Mp * sw)
         for k in list(ready):  # join the side stream in every case
             wait_pre(k)

@@ -139,8 +139,8 @@ _QKV_ATTN_OK = {}
 
 
 def qkv_attn_supported(T, H, dh, dtype):
-    """a fused qkv + attention kernel exists for this shape (bf16 only); TMAE_QKV_ATTN=0 turns it off"""
-    if dtype != torch.bfloat16 or os.environ.get("TMAE_QKV_ATTN", "1") == "0":
+    """a fused qkv + attention kernel exists for this shape (bf16 only)"""
+    if dtype != torch.bfloat16:
         return False
     key = (T, H, dh)
     if key not in _QKV_ATTN_OK:

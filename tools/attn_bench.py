@@ -1,5 +1,5 @@
 """Attention-core micro-benchmark at the bench shapes (batch 64): encoder T=145, 12 heads x 64;
-decoder T=257, 16 heads x 32.  Forward (new VALU-lean kernel vs TMAE_MHA_PLAIN=1) and backward;
+decoder T=257, 16 heads x 32.  Forward and backward;
 MFMA utilisation = algorithmic flops (4 B H T^2 dh fwd, 2.5x that bwd incl. recompute) / time / 2.5 PF."""
 import json
 import os
@@ -40,15 +40,9 @@ def main():
         dq = torch.empty_like(qkv)
         fl = 4.0 * B * H * T * T * dh
         res = {}
-        for plain in ("0", "1"):
-            if plain == "1":
-                os.environ["TMAE_MHA_PLAIN"] = "1"
-            else:
-                os.environ.pop("TMAE_MHA_PLAIN", None)
-            t = ev(lambda: ops.mha(qkv, B, T, H, dh, dh ** -0.5, dt, out=o))
-            res[f"fwd{'_plain' if plain == '1' else ''}_us"] = round(t * 1e6, 1)
-            res[f"fwd{'_plain' if plain == '1' else ''}_mfma_frac"] = round(fl / t / PEAK, 4)
-        os.environ.pop("TMAE_MHA_PLAIN", None)
+        t = ev(lambda: ops.mha(qkv, B, T, H, dh, dh ** -0.5, dt, out=o))
+        res["fwd_us"] = round(t * 1e6, 1)
+        res["fwd_mfma_frac"] = round(fl / t / PEAK, 4)
         train_ops.mha_lse(qkv, B, T, H, dh, dh ** -0.5, dt, o, lse)
         t = ev(lambda: train_ops.mha_bwd(qkv, o, do, lse, dq, B, T, H, dh, dh ** -0.5, dt))
         res["bwd_us"] = round(t * 1e6, 1)

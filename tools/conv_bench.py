@@ -1,6 +1,6 @@
 """Micro-benchmark of the LIC 3x3 convs at the bench shapes (batch 64, 12x12 latent grid, bf16): the
-serial slice-stack layers (2 problems: mean + scale) and h_a's first layer, on the halo-staged kernel
-(default) and on the implicit GEMM (TMAE_CONV_HALO=0, set by the caller).  Prints us per launch and
+serial slice-stack layers (2 problems: mean + scale) and h_a's first layer, on the halo-staged kernel.
+Prints us per launch and
 TFLOP/s.  Under rocprofv3 --pmc each launch is one dispatch of the listed shape."""
 import json
 import sys

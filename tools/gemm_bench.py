@@ -1,7 +1,7 @@
 """Micro-benchmark of the MFMA GEMM on the hot path's token-GEMM shapes, beside torch.matmul
-(hipBLASLt) on the same shapes as an achievable-speed reference.  Interleaved rounds, one process."""
+(hipBLASLt) on the same shapes as an achievable-speed reference.  Interleaved rounds, one process.
+Forced tiles: a variant library (tools/build_variant.sh <name> gemm.hip -DTMAE_GEMM_TILE=<index>, TMAE_LIB=...)."""
 import json
-import os
 import sys
 import time
 
@@ -53,23 +53,9 @@ def main():
         reps = 20 if name != "big" else 5
         fl = 2.0 * M * N * K
         res = {}
-        for ph in os.environ.get("GEMM_PHASED", "1").split(","):
-          os.environ["TMAE_GEMM_PHASED"] = ph
-          for tile in os.environ.get("GEMM_TILES", "auto").split(","):
-            if tile == "auto":
-                os.environ.pop("TMAE_GEMM_TILE", None)
-            else:
-                os.environ["TMAE_GEMM_TILE"] = tile
-            for diag in os.environ.get("GEMM_DIAG", "0").split(","):
-                os.environ["TMAE_GEMM_DIAG"] = diag
-                tm = [ev_time(mine, reps) for _ in range(5)]
-                key = f"p{ph}t{tile}" + (f"d{diag}" if diag != "0" else "")
-                res[key + "_us"] = round(min(tm) * 1e6, 1)
-                if diag == "0":
-                    res[key + "_tf"] = round(fl / min(tm) / 1e12, 1)
-        os.environ.pop("TMAE_GEMM_TILE", None)
-        os.environ.pop("TMAE_GEMM_DIAG", None)
-        os.environ.pop("TMAE_GEMM_PHASED", None)
+        tm = [ev_time(mine, reps) for _ in range(5)]
+        res["us"] = round(min(tm) * 1e6, 1)
+        res["tf"] = round(fl / min(tm) / 1e12, 1)
         tr = [ev_time(ref, reps) for _ in range(5)]
         res["torch_tf"] = round(fl / min(tr) / 1e12, 1)
         out[name] = res
