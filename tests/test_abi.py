@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol(tmae):
     for name in declared_functions():
         assert hasattr(lib, name), name
         if name != "tmae_last_error_string":
-            assert name in _lib.SIGNATURES, f"{name} has no ctypes signature"
+            assert name in _lib.SIGNATURES or name in _lib.VALUE_FUNCS, f"{name} has no ctypes signature"
 
 
 def test_abi_version(tmae):
