@@ -268,6 +268,63 @@ gc_slices_kernel(const float* __restrict__ y, int ldy, int yoff, const float* __
   }
 }
 
+// The same per element, one workgroup per (image, slice) over its HW x sw block (bench: 144 x 32), so that BOTH
+// layouts are written whole-line: y / mu / sigma are read and y_hat / y_hat f32 written in the NHWC order
+// (channel fastest), then y, mu and the bounded scale go through LDS and the likelihood (NCHW), the training
+// noise (NCHW) and the compress symbols / indexes ([slice][N][sw][H][W]) are read / written pixel fastest.
+// The element kernel above wrote the NCHW likelihoods 4 B per lane at a 576-B stride, a line's 32 pixels from
+// ~24 workgroups spread over the XCDs (PMC: 1.92x the algorithmic bytes, partial lines written back by
+// several L2s).  Same arithmetic per element: bitwise the same outputs.
+constexpr int GC_TILE_MAX = 4800;  // HW * (sw + 1) floats per LDS array (3 arrays, 57.6 KB)
+template <typename YT, bool CODE>
+__global__ void __launch_bounds__(256)
+gc_slices_tiled_kernel(const float* __restrict__ y, int ldy, int yoff, const float* __restrict__ mu,
+                       const float* __restrict__ sigma, long long ms_stride, int ld_ms, const float* __restrict__ noise,
+                       float* __restrict__ lik, int Mtot, YT* __restrict__ yhat, int ld_yhat, float* __restrict__ yhat32,
+                       int ld32, int n, int HW, int nslices, int sw, int* __restrict__ sym, int* __restrict__ idx,
+                       const float* __restrict__ scale_table, int nscale) {
+  __shared__ float ys[GC_TILE_MAX], ms[GC_TILE_MAX], ss[GC_TILE_MAX];
+  const int b = blockIdx.x / nslices, j = blockIdx.x - b * nslices;
+  const int ld = sw + 1, tot = HW * sw;
+  // phase 1: NHWC order
+  for (int e = threadIdx.x; e < tot; e += 256) {
+    const int pix = e / sw, c = e - pix * sw;
+    const int m = b * HW + pix, ch = yoff + j * sw + c;
+    const float yv = y[(size_t)m * ldy + ch];
+    const float mv = mu[j * ms_stride + (size_t)m * ld_ms + c];
+    const float sv = sigma[j * ms_stride + (size_t)m * ld_ms + c];
+    const float q = rintf(yv - mv) + mv;
+    if (yhat) yhat[(size_t)m * ld_yhat + ch] = to_out<YT>(q);
+    if (yhat32) yhat32[(size_t)m * ld32 + ch] = q;
+    ys[pix * ld + c] = yv;
+    ms[pix * ld + c] = mv;
+    ss[pix * ld + c] = fmaxf(sv, 0.11f);
+  }
+  __syncthreads();
+  // phase 2: NCHW order (pixel fastest)
+  for (int e = threadIdx.x; e < tot; e += 256) {
+    const int c = e / HW, pix = e - c * HW;
+    const int ch = yoff + j * sw + c;
+    const float yv = ys[pix * ld + c], mv = ms[pix * ld + c], s = ss[pix * ld + c];
+    const size_t nchw = ((size_t)b * Mtot + ch) * HW + pix;
+    const float qi = rintf(yv - mv);
+    const float q = qi + mv;
+    const float xt = noise ? yv + noise[nchw] : q;
+    const float val = fabsf(xt - mv);
+    const float k = -0.70710678118654752440f;
+    const float up = 0.5f * erfcf(k * ((0.5f - val) / s));
+    const float lo = 0.5f * erfcf(k * ((-0.5f - val) / s));
+    lik[nchw] = fmaxf(up - lo, 1e-9f);
+    if constexpr (CODE) {
+      const size_t pos = (size_t)j * n * sw * HW + ((size_t)b * sw + c) * HW + pix;
+      sym[pos] = (int)qi;
+      int id = nscale - 1;
+      for (int t = 0; t < nscale - 1; ++t) id -= (s <= scale_table[t]) ? 1 : 0;
+      idx[pos] = id;
+    }
+  }
+}
+
 template <bool CODE>
 static int gc_slices_launch(const float* y, int ldy, int yoff, const float* mu, const float* sigma,
                             long long ms_stride, int ld_ms, const float* noise, float* lik, int Mtot, void* yhat,
@@ -275,6 +332,19 @@ static int gc_slices_launch(const float* y, int ldy, int yoff, const float* mu, 
                             int* sym, int* idx, const float* scale_table, int nscale, hipStream_t st) {
   const int total = n * HW * nslices * sw;
   if (total <= 0) return TMAE_OK;
+  if (HW * (sw + 1) <= GC_TILE_MAX) {
+    const dim3 tg(n * nslices);
+    if (yhat_dtype == TMAE_BF16)
+      hipLaunchKernelGGL((gc_slices_tiled_kernel<bf16, CODE>), tg, dim3(256), 0, st, y, ldy, yoff, mu, sigma, ms_stride,
+                         ld_ms, noise, lik, Mtot, (bf16*)yhat, ld_yhat, yhat32, ld32, n, HW, nslices, sw, sym, idx,
+                         scale_table, nscale);
+    else
+      hipLaunchKernelGGL((gc_slices_tiled_kernel<float, CODE>), tg, dim3(256), 0, st, y, ldy, yoff, mu, sigma,
+                         ms_stride, ld_ms, noise, lik, Mtot, (float*)yhat, ld_yhat, yhat32, ld32, n, HW, nslices, sw,
+                         sym, idx, scale_table, nscale);
+    TMAE_LAUNCH_CHECK(CODE ? "tmae_gc_slices_code" : "tmae_gc_slices_fwd");
+  }
+  // maps past the LDS tile (HW * (sw + 1) > 4800 floats): one element per thread
   const dim3 grid(ceil_div(total, 256));
   if (yhat_dtype == TMAE_BF16)
     hipLaunchKernelGGL((gc_slices_kernel<bf16, CODE>), grid, dim3(256), 0, st, y, ldy, yoff, mu, sigma, ms_stride,
