@@ -261,6 +261,9 @@ def _dp_worker(rank, world, port, q):
 
         g_deferred = grads(Deferred(bucket_mb=0.05))
         q.put((rank, g_early.numpy(), g_deferred.numpy(), nb))  # plain arrays: no shared-memory fds to outlive us
+    except BaseException as e:  # report instead of leaving the parent waiting on the queue
+        q.put((rank, None, repr(e)[:2000], 0))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -274,9 +277,11 @@ def test_dp_two_ranks_match_full_batch():
     procs = [ctx.Process(target=_dp_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    res = sorted([q.get(timeout=150) for _ in procs], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
+    errs = [b for _, a, b, _ in res if a is None]
+    assert not errs, errs
     assert all(p.exitcode == 0 for p in procs)
     (_, e0, d0, nb), (_, e1, d1, _) = [(r, torch.from_numpy(a), torch.from_numpy(b), n) for r, a, b, n in res]
     assert nb > 10
@@ -364,6 +369,9 @@ def _nccl_w1_worker(port, geom, q):
             if sync is not None:
                 res["timing"] = sync.last_timing()
         q.put(res)
+    except BaseException as e:  # report instead of leaving the parent waiting on the queue
+        q.put({"error": repr(e)[:2000]})
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -379,8 +387,9 @@ def test_rccl_grad_sync_one_rank_bitwise(geom):
     q = ctx.Queue()
     p = ctx.Process(target=_nccl_w1_worker, args=(_port(), geom, q))
     p.start()
-    res = q.get(timeout=400)
+    res = q.get(timeout=170)
     p.join(timeout=60)
+    assert "error" not in res, res.get("error")
     assert p.exitcode == 0
     (l0, g0, w0, _), (l1, g1, w1, launched) = res["plain"], res["rccl"]
     assert launched > 10, launched  # three backwards' worth of buckets really went through RCCL

@@ -42,6 +42,7 @@ class GradSync:
         self.timing = timing
         self._ev = None
         self._first = None
+        self._finishing = False
 
     def world(self):
         return dist.get_world_size(self.group) if dist.is_initialized() else 1
@@ -82,12 +83,12 @@ class GradSync:
             if self.average:
                 t.div_(W)
 
-    def ready(self, upto: int, _in_backward: bool = True):
+    def ready(self, upto: int):
         """gradients [0, upto) of the flat buffer are final: launch every bucket they complete"""
         while self._next < len(self._bounds) - 1 and self._bounds[self._next + 1] <= upto:
             n0 = self.launched
             self._launch(self._next)
-            if _in_backward:
+            if not self._finishing:
                 self.launched_in_backward += self.launched - n0
             self._next += 1
 
@@ -95,7 +96,11 @@ class GradSync:
         """launch the remaining buckets and order the compute stream after every collective"""
         timed = self.timing and self.flat is not None and self.flat.is_cuda
         end = self._event() if timed else None  # the backward's last kernel is enqueued before this point
-        self.ready(self._bounds[-1], _in_backward=False)
+        self._finishing = True
+        try:
+            self.ready(self._bounds[-1])
+        finally:
+            self._finishing = False
         for w in self._work:
             w.wait()
         self._work = []
