@@ -268,7 +268,8 @@ gc_slices_kernel(const float* __restrict__ y, int ldy, int yoff, const float* __
   }
 }
 
-// The same per element, one workgroup per (image, slice) over its HW x sw block (bench: 144 x 32), so that BOTH
+// The same per element, one 1024-thread workgroup per (image, slice) over its HW x sw block (bench: 144 x 32; 256
+// threads left 6 waves per CU and ran 48 vs 34 us per forward), so that BOTH
 // layouts are written whole-line: y / mu / sigma are read and y_hat / y_hat f32 written in the NHWC order
 // (channel fastest), then y, mu and the bounded scale go through LDS and the likelihood (NCHW), the training
 // noise (NCHW) and the compress symbols / indexes ([slice][N][sw][H][W]) are read / written pixel fastest.
@@ -277,7 +278,7 @@ gc_slices_kernel(const float* __restrict__ y, int ldy, int yoff, const float* __
 // several L2s).  Same arithmetic per element: bitwise the same outputs.
 constexpr int GC_TILE_MAX = 4800;  // HW * (sw + 1) floats per LDS array (3 arrays, 57.6 KB)
 template <typename YT, bool CODE>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(1024)
 gc_slices_tiled_kernel(const float* __restrict__ y, int ldy, int yoff, const float* __restrict__ mu,
                        const float* __restrict__ sigma, long long ms_stride, int ld_ms, const float* __restrict__ noise,
                        float* __restrict__ lik, int Mtot, YT* __restrict__ yhat, int ld_yhat, float* __restrict__ yhat32,
@@ -287,7 +288,7 @@ gc_slices_tiled_kernel(const float* __restrict__ y, int ldy, int yoff, const flo
   const int b = blockIdx.x / nslices, j = blockIdx.x - b * nslices;
   const int ld = sw + 1, tot = HW * sw;
   // phase 1: NHWC order
-  for (int e = threadIdx.x; e < tot; e += 256) {
+  for (int e = threadIdx.x; e < tot; e += 1024) {
     const int pix = e / sw, c = e - pix * sw;
     const int m = b * HW + pix, ch = yoff + j * sw + c;
     const float yv = y[(size_t)m * ldy + ch];
@@ -302,7 +303,7 @@ gc_slices_tiled_kernel(const float* __restrict__ y, int ldy, int yoff, const flo
   }
   __syncthreads();
   // phase 2: NCHW order (pixel fastest)
-  for (int e = threadIdx.x; e < tot; e += 256) {
+  for (int e = threadIdx.x; e < tot; e += 1024) {
     const int c = e / HW, pix = e - c * HW;
     const int ch = yoff + j * sw + c;
     const float yv = ys[pix * ld + c], mv = ms[pix * ld + c], s = ss[pix * ld + c];
@@ -335,11 +336,11 @@ static int gc_slices_launch(const float* y, int ldy, int yoff, const float* mu, 
   if (HW * (sw + 1) <= GC_TILE_MAX) {
     const dim3 tg(n * nslices);
     if (yhat_dtype == TMAE_BF16)
-      hipLaunchKernelGGL((gc_slices_tiled_kernel<bf16, CODE>), tg, dim3(256), 0, st, y, ldy, yoff, mu, sigma, ms_stride,
+      hipLaunchKernelGGL((gc_slices_tiled_kernel<bf16, CODE>), tg, dim3(1024), 0, st, y, ldy, yoff, mu, sigma, ms_stride,
                          ld_ms, noise, lik, Mtot, (bf16*)yhat, ld_yhat, yhat32, ld32, n, HW, nslices, sw, sym, idx,
                          scale_table, nscale);
     else
-      hipLaunchKernelGGL((gc_slices_tiled_kernel<float, CODE>), tg, dim3(256), 0, st, y, ldy, yoff, mu, sigma,
+      hipLaunchKernelGGL((gc_slices_tiled_kernel<float, CODE>), tg, dim3(1024), 0, st, y, ldy, yoff, mu, sigma,
                          ms_stride, ld_ms, noise, lik, Mtot, (float*)yhat, ld_yhat, yhat32, ld32, n, HW, nslices, sw,
                          sym, idx, scale_table, nscale);
     TMAE_LAUNCH_CHECK(CODE ? "tmae_gc_slices_code" : "tmae_gc_slices_fwd");
