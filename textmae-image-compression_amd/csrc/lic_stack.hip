@@ -284,38 +284,11 @@ __device__ __forceinline__ void lstk_dispatch(int nkc, const LstkLayer& L, bool 
 #undef LSTK_CASE
 }
 
-// runtime (NF, MF) -> the instantiated item: MF in {1, 2, 3, 4, 5, 9} (pixel chunks of 9 / 5 / 4 / 3 / 2 / 1 of the
-// 16-pixel fragments, LstkPlan), NF = 1 / 2 output fragments per B read
-__device__ __forceinline__ void lstk_run_item(int nf, int mf, int nkc, const LstkLayer& L, bool first, bool last,
-                                              const LstkOut& o, int img, int f0, int j0, unsigned char* lb,
-                                              unsigned in_off, unsigned out_off, int npix, int G, int lane) {
-#define LSTK_MF(NF, MF) \
-  case MF: lstk_dispatch<NF, MF>(nkc, L, first, last, o, img, f0, j0, lb, in_off, out_off, npix, G, lane); break;
-  if (nf == 2) {
-    switch (mf) { LSTK_MF(2, 9) LSTK_MF(2, 5) LSTK_MF(2, 4) LSTK_MF(2, 3) LSTK_MF(2, 2) LSTK_MF(2, 1) default: break; }
-  } else {
-    switch (mf) { LSTK_MF(1, 5) LSTK_MF(1, 4) LSTK_MF(1, 3) LSTK_MF(1, 2) LSTK_MF(1, 1) default: break; }
-  }
-#undef LSTK_MF
-}
-
-// Per-layer work split, chosen on the host (lstk_plan below) and passed by value: scheme byte = chunk size cs
-// (pixel fragments per item, low 4 bits) | singles flag (0x10).  Items: pairs of output fragments (NF = 2, every
-// B read feeds two MFMAs) x pixel chunks, chunk-major, then -- for an odd fragment count -- that last fragment
-// alone (NF = 1) x chunks; with the singles flag every fragment alone x chunks.  Items go round-robin to the
-// 8 waves.  The old fixed split (pairs x all 9 pixel fragments / pairs x halves / singles x halves) left waves
-// idle on the 176-, 80- and 32-wide layers (a duplicated 12th fragment at 176, 10 items for 8 waves at 80, 4 at
-// 32) and ran K = 64's 4 pixel fragments as 9.
-struct LstkPlan {
-  unsigned char scheme[2][TMAE_LIC_STACK_MAXL];  // [pass][layer]
-};
-constexpr unsigned char LSTK_SINGLES = 0x10;
-
 // the argument block is read in place from the kernarg segment (scalar loads, layer fields indexed at
 // run time): a by-value copy indexed by the layer number would live in scratch
 typedef const __attribute__((address_space(4))) tmae_lic_stack_args LstkArgs;
 
-__global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack_args, LstkPlan plan) {
+__global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack_args) {
   using namespace lstk;
   LstkArgs* a = (LstkArgs*)__builtin_amdgcn_kernarg_segment_ptr();
   __shared__ __attribute__((aligned(16))) uint4 lds[LDS_BYTES / 16];
@@ -440,26 +413,38 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
       const unsigned in_off = (l & 1) ? (unsigned)BUF : 0u, out_off = (l & 1) ? 0u : (unsigned)BUF;
       const int nfr = (L.cout + 15) >> 4;
       const int nkc = pad32(L.cin) >> 5;
-      // wave items (LstkPlan): pairs x chunks, then singles x chunks, round-robin over the waves
-      const unsigned sch = plan.scheme[pass][l];
-      const int cs = sch & 15, nch = (nmf + cs - 1) / cs;
-      const int npair = (sch & LSTK_SINGLES) ? 0 : nfr >> 1;
-      const int nsing = (sch & LSTK_SINGLES) ? nfr : nfr & 1;
-      const int npi = npair * nch, nitems = npi + nsing * nch;
-      for (int it = wave; it < nitems; it += NW) {
-        int nf, f0, k;
-        if (it < npi) {
-          k = it / npair;
-          nf = 2;
-          f0 = 2 * (it - k * npair);
+      // (Round 4 measured a host-planned split with finer items -- pairs / singles x pixel chunks of 1..5, chosen
+      // per layer to balance the waves -- at 2x the time per launch: ms_3 114.7 vs 63.3 us, profiles/r04/
+      // c6_ls_*.log.  Each item streams its weight fragments from L2 for its own pixel chunk, so a chunk of 3
+      // fragments or fewer needs >= 46 TB/s of L2 at the MFMA rate, and every item restarts the weight ring.)
+      // wave items.  LDS bandwidth binds first: one 1-KiB B read per 16-cycle MFMA on every SIMD is the
+      // whole 256 B/clk array, so every wide layer shares each B read between two output fragments
+      // (NF = 2); the pixel fragments are split in halves (5 + 4) where that balances the four SIMDs better:
+      //   >= 14 output fragments (224): fragment pairs x all pixel fragments (7 items);
+      //   8..13 (176, 128): fragment pairs x pixel halves, all first halves dealt before the second ones;
+      //   < 8 (80, 32): single fragments x pixel halves.
+      const bool halves = nmf > 5;
+      if (nfr >= 8) {
+        const int ng = (nfr + 1) >> 1;
+        if (nfr >= 14 || !halves) {
+          for (int it = wave; it < ng; it += NW)
+            lstk_dispatch<2, 9>(nkc, L, first, last, o, img, 2 * it, 0, lb, in_off, out_off, npix, G, lane);
         } else {
-          const int s1 = it - npi;
-          k = s1 / nsing;
-          nf = 1;
-          f0 = (sch & LSTK_SINGLES) ? s1 - k * nsing : nfr - 1;
+          for (int it = wave; it < 2 * ng; it += NW) {
+            const int g = it < ng ? it : it - ng;
+            if (it < ng) lstk_dispatch<2, 5>(nkc, L, first, last, o, img, 2 * g, 0, lb, in_off, out_off, npix, G, lane);
+            else lstk_dispatch<2, 4>(nkc, L, first, last, o, img, 2 * g, 5, lb, in_off, out_off, npix, G, lane);
+          }
         }
-        const int j0 = k * cs, mf = min(cs, nmf - j0);
-        lstk_run_item(nf, mf, nkc, L, first, last, o, img, f0, j0, lb, in_off, out_off, npix, G, lane);
+      } else if (!halves) {
+        for (int it = wave; it < nfr; it += NW)
+          lstk_dispatch<1, 5>(nkc, L, first, last, o, img, it, 0, lb, in_off, out_off, npix, G, lane);
+      } else {
+        for (int it = wave; it < 2 * nfr; it += NW) {
+          const int f = it < nfr ? it : it - nfr;
+          if (it < nfr) lstk_dispatch<1, 5>(nkc, L, first, last, o, img, f, 0, lb, in_off, out_off, npix, G, lane);
+          else lstk_dispatch<1, 4>(nkc, L, first, last, o, img, f, 5, lb, in_off, out_off, npix, G, lane);
+        }
       }
       if (!last) {
         // zero the channel padding [cout, pad32(cout)) the next layer's 32-wide K steps read
@@ -475,41 +460,6 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
       __syncthreads();
     }
   }
-}
-
-// the split with the least work on the busiest wave: every (pairs | singles) x chunk size whose chunks are
-// instantiated, items dealt exactly as the kernel deals them; cost per item = MFMAs per K-step, a single
-// fragment's weighted 1.3x (it reads one B fragment per MFMA: at four waves per CU that alone fills the LDS
-// array); ties go to fewer items
-static unsigned char lstk_plan(int nfr, int nmf) {
-  static const int kChunks[] = {9, 5, 4, 3, 2, 1};
-  double best = 1e30;
-  int best_items = 1 << 30;
-  unsigned char pick = 1 | LSTK_SINGLES;
-  for (int singles = 0; singles < 2; ++singles)
-    for (int cs : kChunks) {
-      if (cs > nmf && cs != 1) continue;
-      const int nch = (nmf + cs - 1) / cs, last = nmf - (nch - 1) * cs;
-      if (cs == 9 && singles) continue;  // NF = 1 is instantiated up to 5 pixel fragments
-      if (cs == 9 && nmf != 9) continue;
-      const int npair = singles ? 0 : nfr / 2, nsing = singles ? nfr : nfr & 1;
-      const int nitems = npair * nch + nsing * nch;
-      double wave[lstk::NW] = {};
-      for (int it = 0; it < nitems; ++it) {
-        const bool pair = it < npair * nch;
-        const int k = pair ? it / npair : (it - npair * nch) / nsing;
-        const int mf = k == nch - 1 ? last : cs;
-        wave[it % lstk::NW] += pair ? 2.0 * mf : 1.3 * mf;
-      }
-      double mx = 0;
-      for (double w : wave) mx = std::max(mx, w);
-      if (mx < best - 1e-9 || (mx < best + 1e-9 && nitems < best_items)) {
-        best = mx;
-        best_items = nitems;
-        pick = (unsigned char)(cs | (singles ? LSTK_SINGLES : 0));
-      }
-    }
-  return pick;
 }
 
 extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
@@ -545,12 +495,7 @@ extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
                    "tmae_lic_stack: chain layer %d", l);
   }
   if (a.addend) TMAE_REQUIRE(a.ld_add % 4 == 0, "tmae_lic_stack: addend stride %d", a.ld_add);
-  const int nmf = (a.G * a.G + 15) >> 4;
-  LstkPlan plan{};
-  for (int l = 0; l < a.nlayers; ++l) plan.scheme[0][l] = lstk_plan((a.cout[l] + 15) >> 4, nmf);
-  if (a.flags & TMAE_LIC_STACK_CHAIN)
-    for (int l = 0; l < a.cn; ++l) plan.scheme[1][l] = lstk_plan((a.ccout[l] + 15) >> 4, nmf);
   const int nwg = a.n * a.nb1 * a.nb2;
-  hipLaunchKernelGGL(lic_stack_kernel, dim3(nwg), dim3(NW * 64), 0, (hipStream_t)stream, a, plan);
+  hipLaunchKernelGGL(lic_stack_kernel, dim3(nwg), dim3(NW * 64), 0, (hipStream_t)stream, a);
   TMAE_LAUNCH_CHECK("tmae_lic_stack");
 }
