@@ -246,7 +246,8 @@ def test_layernorm_bwd_remap(T):
 
 
 # ------------------------------------------------------------------------------ attention
-@pytest.mark.parametrize("T_,H,dh", [(145, 12, 64), (257, 16, 32), (20, 2, 64), (65, 4, 80), (161, 2, 80)])
+@pytest.mark.parametrize("T_,H,dh", [(145, 12, 64), (257, 16, 32), (20, 2, 64), (65, 4, 80), (161, 2, 80), (32, 2, 32),
+                                     (33, 3, 32), (288, 4, 32), (160, 2, 64), (1, 2, 32)])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_mha_bwd(T, T_, H, dh, dt):
     from textmae_amd import ops
@@ -267,8 +268,11 @@ def test_mha_bwd(T, T_, H, dh, dt):
     T.mha_lse(qg, B, T_, H, dh, scale, dt, out, lse)
     dq = torch.empty(B * T_, 3 * D, device="cuda", dtype=dt)
     T.mha_bwd(qg, out, do.cuda().to(dt), lse, dq, B, T_, H, dh, scale, dt)
+    dq2 = torch.empty_like(dq)
+    T.mha_bwd(qg, out, do.cuda().to(dt), lse, dq2, B, T_, H, dh, scale, dt)
     o_plain = ops.mha(qg, B, T_, H, dh, scale, dt)
     torch.cuda.synchronize()
+    assert torch.equal(dq, dq2)  # fixed summation order: bitwise reproducible
     assert torch.equal(out, o_plain)  # the lse variant computes the same output
     if dt == torch.float32:
         check("_rel:out", _rel(out, o), 1e-5)

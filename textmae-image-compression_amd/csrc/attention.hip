@@ -508,6 +508,186 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
   }
 }
 
+// One-pass form: each wave owns 32 keys (dK^T, dV^T in registers) and walks the query tiles in a STAGGERED order --
+// wave w takes tile (w + it) mod nw at step it -- so at every step each query tile belongs to exactly one wave.
+// That wave's dQ contribution dS K (dS through a per-wave LDS scratch, the only operand crossing lanes) is added
+// into the tile's f32 accumulator in LDS, one barrier per step; every tile receives the waves' contributions in a
+// fixed order (bitwise reproducible), and nothing is recomputed: the two-phase form above computed S and dP twice
+// (the exp and dS VALU of phase 2) and restaged K / V.  LDS: Q, dO, K [Tpad][LDR] bf16, dS 32 x 32 bf16 per wave,
+// dQ [DH][Tpad + 4] f32 (row stride 4 mod 32 dwords: the 16-B read-modify-writes of a half-wave hit 64 banks).
+template <int DH>
+__global__ void __launch_bounds__(DH == 32 ? 1024 : 512)  // dh 64: <= 256 keys, up to 256 VGPRs
+mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
+                     const float* __restrict__ lse, bf16* __restrict__ dqkv, int Tn, int H, int Tpad, float scale) {
+  constexpr int LDR = AttnBwd<DH>::LDR;
+  constexpr int NDT = (DH + 31) / 32;
+  constexpr int CPR = DH / 8;
+  static_assert(DH % 32 == 0, "one-pass backward: whole 32-wide head-dim tiles");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int nw = Tpad / 32, LDQ = Tpad + 4;
+  bf16* Qs = reinterpret_cast<bf16*>(smem);
+  bf16* Gs = Qs + (size_t)Tpad * LDR;
+  bf16* Ks = Gs + (size_t)Tpad * LDR;
+  bf16* dSs = Ks + (size_t)Tpad * LDR;                     // nw x [32 keys][32 queries]
+  float* dQs = reinterpret_cast<float*>(dSs + (size_t)nw * 1024);  // [DH][LDQ]
+  float* lse_s = dQs + (size_t)DH * LDQ;
+  float* dl_s = lse_s + Tpad;
+
+  const int bh = xcd_remap(blockIdx.x, gridDim.x), b = bh / H, h = bh - b * H;
+  const int D = H * DH, ld = 3 * D;
+  const bf16* base = qkv + (size_t)b * Tn * ld + h * DH;
+  const bf16* obase = o + (size_t)b * Tn * D + h * DH;
+  const bf16* gbase = dout + (size_t)b * Tn * D + h * DH;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+
+  attn_stage2<DH, LDR>(Qs, base, ld, Gs, gbase, D, Tn, Tpad, tid, nthr);  // Q, dO
+  for (int i = tid; i < Tpad * CPR; i += nthr) {                          // K
+    const int r = i / CPR, c = i - r * CPR;
+    uint4 x = uint4{0, 0, 0, 0};
+    if (r < Tn) x = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + D + c * 8);
+    *reinterpret_cast<uint4*>(Ks + (size_t)r * LDR + c * 8) = x;
+  }
+  for (int i = tid; i < DH * LDQ / 4; i += nthr) reinterpret_cast<f32x4*>(dQs)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int r = tid; r < Tpad; r += nthr) {  // delta = rowsum(dO * O), lse
+    float d = 0.0f, l = 0.0f;
+    if (r < Tn) {
+      const bf16* orow = obase + (size_t)r * D;
+      const bf16* grow = gbase + (size_t)r * D;
+#pragma unroll
+      for (int c = 0; c < CPR; ++c) {
+        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(orow + 8 * c);
+        const bf16x8 gv = *reinterpret_cast<const bf16x8*>(grow + 8 * c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += (float)ov[e] * (float)gv[e];
+      }
+      l = lse[(size_t)bh * Tn + r];
+    }
+    dl_s[r] = d;
+    lse_s[r] = l;
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, hh = lane >> 5;
+  const float c2 = scale * 1.4426950408889634f;
+  const bool ragged = (Tn & 31) != 0;
+  const int kb = 32 * wave;
+  const int kr = min(kb + col, Tn - 1);
+  bf16x8 kf[DH / 16], vf[DH / 16];
+#pragma unroll
+  for (int s = 0; s < DH / 16; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)kr * ld + D + 16 * s + 8 * hh);
+    vf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)kr * ld + 2 * D + 16 * s + 8 * hh);
+  }
+  f32x16 dV[NDT], dK[NDT];
+#pragma unroll
+  for (int t = 0; t < NDT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dV[t][r] = dK[t][r] = 0.0f;
+  const bool kmask = ragged && wave == nw - 1;  // wave-uniform: this wave holds the keys past Tn
+  const bool kok = kb + col < Tn;
+  bf16* dsw = dSs + (size_t)wave * 1024;
+
+  for (int it = 0; it < nw; ++it) {
+    int qt = wave + it;
+    if (qt >= nw) qt -= nw;
+    f32x16 S, G;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) S[r] = G[r] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < DH / 16; ++s) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(Qs + (size_t)(qt * 32 + col) * LDR + 16 * s + 8 * hh);
+      S = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, kf[s], S, 0, 0, 0);
+      const bf16x8 g = *reinterpret_cast<const bf16x8*>(Gs + (size_t)(qt * 32 + col) * LDR + 16 * s + 8 * hh);
+      G = __builtin_amdgcn_mfma_f32_32x32x16_bf16(g, vf[s], G, 0, 0, 0);
+    }
+    // lse / delta of this lane's 16 queries: four runs of 4 consecutive rows (16-B LDS reads)
+    const int q0 = qt * 32 + 4 * hh;
+    f32x4 lq[4], dq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      lq[k] = *reinterpret_cast<const f32x4*>(lse_s + q0 + 8 * k);
+      dq[k] = *reinterpret_cast<const f32x4*>(dl_s + q0 + 8 * k);
+    }
+    const bool qmask = ragged && qt == nw - 1;  // wave-uniform: this tile holds the queries past Tn
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float p = exp2f(S[r] * c2 - lq[r >> 2][r & 3]);
+      if (kmask || qmask) p = (kok && q0 + (r & 3) + 8 * (r >> 2) < Tn) ? p : 0.0f;
+      S[r] = p;
+      G[r] = p * (G[r] - dq[r >> 2][r & 3]) * scale;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 pa, da;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { pa[j] = (bf16)S[8 * s + j]; da[j] = (bf16)G[8 * s + j]; }
+      const int k0 = qt * 32 + 16 * s;
+#pragma unroll
+      for (int t = 0; t < NDT; ++t) {
+        dV[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, attn_tr_frag<LDR>(Gs, k0, 32 * t, lane), dV[t], 0, 0, 0);
+        dK[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(da, attn_tr_frag<LDR>(Qs, k0, 32 * t, lane), dK[t], 0, 0, 0);
+      }
+      // dS of this wave's keys (rows) x the tile's queries (columns) -> the wave's scratch, bf16 (the same
+      // rounding the dK product above consumes)
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        bf16x4 v;
+        v[0] = da[4 * k]; v[1] = da[4 * k + 1]; v[2] = da[4 * k + 2]; v[3] = da[4 * k + 3];
+        *reinterpret_cast<bf16x4*>(dsw + col * 32 + 16 * s + 8 * k + 4 * hh) = v;
+      }
+    }
+    // the scratch is read back across lanes by this wave only: LDS executes a wave's operations in order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // dQ[tile] += dS K: A = dS (queries on the lanes, keys k), B = K rows of this wave's keys
+    f32x16 dQp[NDT];
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dQp[t][r] = 0.0f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 a = attn_tr_frag<32>(dsw, 16 * s, 0, lane);
+#pragma unroll
+      for (int t = 0; t < NDT; ++t)
+        dQp[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, attn_tr_frag<LDR>(Ks, kb + 16 * s, 32 * t, lane), dQp[t],
+                                                         0, 0, 0);
+    }
+    // lane holds dQ[q = qt*32 + (r&3) + 8(r>>2) + 4hh][d = 32t + col]: four 16-B runs of the [d][q] accumulator
+#pragma unroll
+    for (int t = 0; t < NDT; ++t)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        f32x4* pq = reinterpret_cast<f32x4*>(dQs + (size_t)(32 * t + col) * LDQ + q0 + 8 * k);
+        f32x4 v = *pq;
+        v += f32x4{dQp[t][4 * k], dQp[t][4 * k + 1], dQp[t][4 * k + 2], dQp[t][4 * k + 3]};
+        *pq = v;
+      }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int t = 0; t < NDT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kb + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (key < Tn) {
+        bf16* row = dqkv + ((size_t)b * Tn + key) * ld + h * DH + 32 * t + col;
+        row[D] = (bf16)dK[t][r];
+        row[2 * D] = (bf16)dV[t][r];
+      }
+    }
+  // dQ rows -> dqkv (8 head-dim values per thread, one 16-B store)
+  for (int i = tid; i < Tn * CPR; i += nthr) {
+    const int q = i / CPR, c = i - q * CPR;
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (bf16)dQs[(size_t)(8 * c + e) * LDQ + q];
+    *reinterpret_cast<bf16x8*>(dqkv + ((size_t)b * Tn + q) * ld + h * DH + 8 * c) = v;
+  }
+}
+
 // f32 (parity) form: same two phases on v_mfma_f32_32x32x2_f32, operands read straight from global memory
 // (L2-resident per head); exact f32 products.
 template <int DH>
@@ -630,6 +810,13 @@ mha_bwd_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ o, c
   }
 }
 
+// head dims on the one-pass backward (dh 80 keeps the two-phase form: its padded head-dim tile); A/B builds set
+// TMAE_BWD1_DH64=0 to put the encoder's dh 64 back on the two-phase form
+#ifndef TMAE_BWD1_DH64
+#define TMAE_BWD1_DH64 1
+#endif
+template <int DH> struct AttnBwdOnePass { static constexpr bool value = DH == 32 || (DH == 64 && TMAE_BWD1_DH64); };
+
 template <int DH>
 static int mha_bwd_launch(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv, int B, int Tn,
                           int H, float scale, int dtype, hipStream_t st) {
@@ -639,7 +826,15 @@ static int mha_bwd_launch(const void* qkv, const void* o, const void* dout, cons
   if (B * H == 0 || Tn == 0) return TMAE_OK;
   if (dtype == TMAE_BF16) {
     TMAE_REQUIRE(DH == 32 || nthr <= 512, "tmae_mha_bwd: sequence length %d too long for head dim %d", Tn, DH);
-    const size_t lds = (size_t)2 * Tpad * AttnBwd<DH>::LDR * 2 + (size_t)2 * Tpad * 4;
+    constexpr int LDR = AttnBwd<DH>::LDR;
+    const size_t lds1 = (size_t)3 * Tpad * LDR * 2 + (size_t)(Tpad / 32) * 2048 + (size_t)DH * (Tpad + 4) * 4 +
+                        (size_t)2 * Tpad * 4;
+    if (AttnBwdOnePass<DH>::value && lds1 <= 160 * 1024) {
+      hipLaunchKernelGGL((mha_bwd1_bf16_kernel<AttnBwdOnePass<DH>::value ? DH : 32>), dim3(B * H), dim3(nthr), lds1,
+                         st, (const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, (bf16*)dqkv, Tn, H, Tpad, scale);
+      TMAE_LAUNCH_CHECK("tmae_mha_bwd");
+    }
+    const size_t lds = (size_t)2 * Tpad * LDR * 2 + (size_t)2 * Tpad * 4;
     TMAE_REQUIRE(lds <= 160 * 1024, "tmae_mha_bwd: sequence length %d needs %zu B of LDS", Tn, lds);
     hipLaunchKernelGGL((mha_bwd_bf16_kernel<DH>), dim3(B * H), dim3(nthr), lds, st, (const bf16*)qkv, (const bf16*)o,
                        (const bf16*)dout, lse, (bf16*)dqkv, Tn, H, Tpad, scale);
