@@ -20,29 +20,63 @@
 
 namespace qa {
 constexpr int NW = 8, WGN = 4, WGM = 2;  // waves: 4 along the 192 weight columns, 2 along the tokens
-template <int DH, int HG, int TPAD> struct Cfg {
+// BK = 64: 128-B LDS rows (8 chunks), 2 stages, one workgroup per CU.  BK = 32: 64-B rows (4 chunks), 3 stages
+// (counted vmcnt), the rows padded to whole rounds of 16-row pieces so every wave issues the same count; the ring
+// then fits beside nothing else but stays under the attention images, so two workgroups share a CU.
+template <int DH, int HG, int TPAD, int BK = 64> struct Cfg {
   static constexpr int NC = 3 * HG * DH;            // GEMM columns (weight rows) of the workgroup
-  static constexpr int ROWS = NC + TPAD;            // LDS rows per ring stage (128 B each)
-  static constexpr int PIECES = ROWS / 8;           // 1-KiB LDS-DMA pieces per stage
-  static constexpr int PPW = (PIECES + NW - 1) / NW;  // pieces per wave (the last round partial)
+  static constexpr int RB = 2 * BK;                 // bytes per LDS row
+  static constexpr int PROWS = 1024 / RB;           // rows per 1-KiB LDS-DMA piece
+  static constexpr int NS = BK == 64 ? 2 : 3;       // ring stages
+  static constexpr int ROWS0 = NC + TPAD;
+  static constexpr int ROWS = BK == 64 ? ROWS0 : (ROWS0 + NW * PROWS - 1) / (NW * PROWS) * (NW * PROWS);
+  static constexpr int PIECES = ROWS / PROWS;       // LDS-DMA pieces per stage
+  static constexpr int PPW = (PIECES + NW - 1) / NW;  // pieces per wave (the last round partial at BK = 64)
   static constexpr int WN = NC / WGN, WM = TPAD / WGM;
   static constexpr int TN = WN / 16, TM = WM / 16;
   static constexpr int LDQ = DH + 8, LDV = AttnTr<DH>::LDV;
   static constexpr int QK_BYTES = TPAD * LDQ * 2, V_BYTES = TPAD * LDV * 2;
   static constexpr int HEAD_BYTES = 2 * QK_BYTES + V_BYTES;  // Q, K, V images of one head
-  static constexpr int RING = 2 * ROWS * 128;
+  static constexpr int RING = NS * ROWS * RB;
   static constexpr int LDS = RING > HG * HEAD_BYTES ? RING : HG * HEAD_BYTES;
+  static constexpr int WG_PER_CU = BK == 64 ? 1 : 2;
   static_assert(ROWS % 8 == 0 && WN % 16 == 0 && WM % 16 == 0 && TPAD % 32 == 0, "qkv_attn tile");
   static_assert(LDV > 0 && DH % 32 == 0, "qkv_attn: head dim with a lean attention core");
-  static_assert(LDS <= 160 * 1024, "qkv_attn: LDS");
+  static_assert(LDS * WG_PER_CU <= 160 * 1024, "qkv_attn: LDS");
+  static_assert(BK == 64 || ROWS % (NW * PROWS) == 0, "qkv_attn: BK 32 rows in whole rounds");
 };
+
+// 64-B LDS rows: chunk c of row r at slot c ^ (((r >> 3) & 1) << 1) -- the ds_read_b128 fragment reads of 16
+// consecutive rows x 4 chunks are conflict-free in all four lane groups
+__device__ __forceinline__ int slot32(int r, int c) { return c ^ (((r >> 3) & 1) << 1); }
+
+// one 32-deep K-step of the swapped 16x16x32 MFMA tile over 64-B rows (A = weight rows [0, BN), B = token rows)
+template <int BN, int WN, int WM, int TN, int TM>
+__device__ __forceinline__ void mfma_tile32(const unsigned char* stage, int wn, int wm, int lane, f32x4 (&acc)[TN][TM]) {
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8 a[TN], b[TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int r = wn * WN + 16 * i + fr;
+    a[i] = *reinterpret_cast<const bf16x8*>(stage + r * 64 + 16 * slot32(r, fq));
+  }
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int r = BN + wm * WM + 16 * j + fr;
+    b[j] = *reinterpret_cast<const bf16x8*>(stage + r * 64 + 16 * slot32(r, fq));
+  }
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+}
 }  // namespace qa
 
-template <int DH, int HG, int TPAD>
-__global__ void __launch_bounds__(qa::NW * 64, 1)
+template <int DH, int HG, int TPAD, int BK>
+__global__ void __launch_bounds__(qa::NW * 64, BK == 64 ? 1 : 2)
 qkv_attn_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, const float* __restrict__ bias,
                 bf16* __restrict__ out, int T, int H, float scale_log2e) {
-  using C = qa::Cfg<DH, HG, TPAD>;
+  using C = qa::Cfg<DH, HG, TPAD, BK>;
   constexpr int NW = qa::NW, WGN = qa::WGN;
   constexpr int NC = C::NC, TN = C::TN, TM = C::TM, WN = C::WN, WM = C::WM, LDQ = C::LDQ, LDV = C::LDV;
   __shared__ __attribute__((aligned(16))) uint4 lds[C::LDS / 16];
@@ -56,29 +90,30 @@ qkv_attn_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, const fl
 
   // ---- 1. GEMM: acc[n][m] = sum_k W[row(n)][k] X[b, m][k]; weight row of column n (q | k | v parts, each the
   // HD rows of this head group): part * D + g * HD + n % HD
-  const int pch = lane & 7;
+  constexpr int LPR = BK / 8;                      // 16-B chunks per LDS row
+  const int pch = lane % LPR;
   const bf16* src[C::PPW];
   int swz[C::PPW];
 #pragma unroll
   for (int j = 0; j < C::PPW; ++j) {
-    const int r = 8 * (wave + NW * j) + (lane >> 3);  // LDS row this lane fills
+    const int r = C::PROWS * (wave + NW * j) + lane / LPR;  // LDS row this lane fills
     const int rr = min(r, C::ROWS - 1);
     if (rr < NC) {
       const int part = rr / HD;
       src[j] = w + (size_t)(part * D + g * HD + (rr - part * HD)) * D;
     } else {
-      src[j] = xb + (size_t)min(rr - NC, T - 1) * D;  // rows past T: the last row (masked later)
+      src[j] = xb + (size_t)min(rr - NC, T - 1) * D;  // rows past T (and the BK-32 round padding): the last row
     }
-    swz[j] = pch ^ ((r >> 1) & 7);
+    swz[j] = BK == 64 ? pch ^ ((r >> 1) & 7) : qa::slot32(r, pch);  // source chunk of this lane's LDS slot
   }
   const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
   const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto issue = [&](int stage, int kt) {
-    const unsigned sb = lds_base + (unsigned)stage * C::ROWS * 128u;
+    const unsigned sb = lds_base + (unsigned)stage * C::ROWS * C::RB;
 #pragma unroll
     for (int j = 0; j < C::PPW; ++j) {
       if (C::PIECES % NW == 0 || (int)wave_u + NW * j < C::PIECES)  // wave-uniform: the last round is partial
-        glds16(src[j] + kt * 64 + swz[j] * 8, sb + (wave_u + NW * j) * 1024u);
+        glds16(src[j] + kt * BK + swz[j] * 8, sb + (wave_u + NW * j) * 1024u);
     }
   };
   f32x4 acc[TN][TM];
@@ -86,17 +121,32 @@ qkv_attn_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, const fl
   for (int i = 0; i < TN; ++i)
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = D / 64;
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int stage = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) issue(stage ^ 1, kt + 1);
-    mfma_tile<bf16, NC, WN, WM, TN, TM>(lds + stage * C::ROWS * 8, wn, wm, lane, acc);
+  const int nk = D / BK;
+  if constexpr (BK == 64) {
+    issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    stage ^= 1;
+    int stage = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) issue(stage ^ 1, kt + 1);
+      mfma_tile<bf16, NC, WN, WM, TN, TM>(lds + stage * C::ROWS * 8, wn, wm, lane, acc);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      stage ^= 1;
+    }
+  } else {
+    // 3-stage ring: step kt reads stage kt % 3 and issues step kt + 2 into the stage step kt - 1 read (retired by
+    // the barrier that closed step kt - 1); counted waits keep the younger stage in flight
+    constexpr int PER = C::PPW;
+    const unsigned char* lb0 = reinterpret_cast<const unsigned char*>(lds);
+    issue(0, 0);
+    if (nk > 1) issue(1, 1);
+    gemm_ring_wait<PER, 3>(min(1, nk - 1));
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 2 < nk) issue((kt + 2) % 3, kt + 2);
+      qa::mfma_tile32<NC, WN, WM, TN, TM>(lb0 + (kt % 3) * C::ROWS * C::RB, wn, wm, lane, acc);
+      gemm_ring_wait<PER, 3>(min(kt + 2, nk - 1) - (kt + 1));
+    }
   }
 
   // ---- 2. + bias, bf16, into the per-head Q / K / V images (the ring is free after the last barrier)
@@ -140,11 +190,14 @@ qkv_attn_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, const fl
   }
 }
 
-template <int DH, int HG, int TPAD>
+#ifndef TMAE_QA_ENC_BK
+#define TMAE_QA_ENC_BK 32  // A/B builds (tools/build_variant.sh qkv_attn.hip -DTMAE_QA_ENC_BK=64)
+#endif
+template <int DH, int HG, int TPAD, int BK = (DH == 64 ? TMAE_QA_ENC_BK : 64)>
 static int qkv_attn_launch(const bf16* x, const bf16* w, const float* b, bf16* out, int B, int T, int H, float scale,
                            hipStream_t st) {
-  hipLaunchKernelGGL((qkv_attn_kernel<DH, HG, TPAD>), dim3(B * (H / HG)), dim3(qa::NW * 64), 0, st, x, w, b, out, T, H,
-                     scale * 1.4426950408889634f);
+  hipLaunchKernelGGL((qkv_attn_kernel<DH, HG, TPAD, BK>), dim3(B * (H / HG)), dim3(qa::NW * 64), 0, st, x, w, b, out, T,
+                     H, scale * 1.4426950408889634f);
   TMAE_LAUNCH_CHECK("tmae_qkv_attn_fwd");
 }
 
