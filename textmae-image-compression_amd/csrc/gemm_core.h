@@ -397,9 +397,13 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
   constexpr int WN = BN / WGN, WM = BM / WGM;
   constexpr int TN = WN / 16, TM = WM / 16;
   constexpr int PR = 8 * NW;                 // rows covered by one glds round of all waves
-  constexpr int WJ = BN / PR, XJ = BM / PR;  // glds instructions per wave per stage
+  // glds instructions per wave per stage; a token-side row count that is not a whole number of rounds (the
+  // 8-wave 256 x 160 tile: 2.5 rounds of 64 rows) ends in a partial round issued by the first waves only
+  constexpr int WJ = BN / PR, XJ = (BM + PR - 1) / PR;
+  constexpr bool XPART = BM % PR != 0;
   constexpr int ROWS = BN + BM;
-  static_assert(TN >= 1 && TM >= 1 && WJ >= 1 && XJ >= 1 && BN % PR == 0 && BM % PR == 0, "bad tile");
+  static_assert(TN >= 1 && TM >= 1 && WJ >= 1 && XJ >= 1 && BN % PR == 0 && BM % 8 == 0, "bad tile");
+  static_assert(!XPART || NS == 2, "partial DMA rounds need the uncounted 2-stage ring");
   static_assert(NS >= 2 && NS <= 4, "stages");
   __shared__ __attribute__((aligned(16))) uint4 lds[NS * ROWS * 8];
 
@@ -438,13 +442,15 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
         glds16(src_addr_full(ws, wrow[j], kt, wc[j]), sb + (unsigned)(PR * j + 8 * wave_u) * 128u);
 #pragma unroll
       for (int j = 0; j < XJ; ++j)
-        glds16(src_addr_full(xs, xrow[j], kt, xc[j]), sb + (unsigned)(BN + PR * j + 8 * wave_u) * 128u);
+        if (!XPART || PR * j + 8 * (int)wave_u < BM)
+          glds16(src_addr_full(xs, xrow[j], kt, xc[j]), sb + (unsigned)(BN + PR * j + 8 * wave_u) * 128u);
     } else {
 #pragma unroll
       for (int j = 0; j < WJ; ++j) glds16(ws.addr(wrow[j], kt, wc[j]), sb + (unsigned)(PR * j + 8 * wave_u) * 128u);
 #pragma unroll
       for (int j = 0; j < XJ; ++j)
-        glds16(xs.addr(xrow[j], kt, xc[j]), sb + (unsigned)(BN + PR * j + 8 * wave_u) * 128u);
+        if (!XPART || PR * j + 8 * (int)wave_u < BM)
+          glds16(xs.addr(xrow[j], kt, xc[j]), sb + (unsigned)(BN + PR * j + 8 * wave_u) * 128u);
     }
   };
 
@@ -569,9 +575,10 @@ struct TileChoice { int bn, bm, nw; };
 // The 8-wave 256 x 192 tile (waves 2 x 4, 128 x 48 each) exists for the tail: 9280- and 16448-row token
 // GEMMs whose 256 x 256 tile count lands just past a multiple of 256 CUs (enc qkv 333 tiles = 1.3
 // rounds, dec fc1 520 = 2.03, dec proj/fc2 130 = 0.5).
-static constexpr int kNumTiles = 9;
+static constexpr int kNumTiles = 10;
 static constexpr int kTileCand[kNumTiles][3] = {{256, 256, 8}, {128, 128, 4}, {64, 128, 4}, {32, 128, 4}, {64, 64, 4},
-                                                {32, 64, 4},   {256, 192, 8}, {128, 160, 4}, {128, 192, 4}};
+                                                {32, 64, 4},   {256, 192, 8}, {128, 160, 4}, {128, 192, 4},
+                                                {256, 160, 8}};
 // candidates only the bf16 LDS-DMA path instantiates
 static inline bool tile_bf16_only(int i) { return kTileCand[i][2] == 8 || i >= 7; }
 // eff = per-CU throughput relative to two 128 x 128 workgroups.  Forced-tile runs of the bench's token
@@ -597,7 +604,11 @@ static inline bool tile_bf16_only(int i) { return kTileCand[i][2] == 8 || i >= 7
 #endif
 static inline TileChoice choose_tile(int M, int N, int K, int batch, bool allow_big) {
   const double kf = 1.0 + 0.12 * std::log2(std::max(K, 768) / 768.0);
-  const double eff[kNumTiles] = {1.10 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, 1.08 * kf, 1.22, 1.25};
+#ifndef TMAE_GEMM_E256x160
+#define TMAE_GEMM_E256x160 0  // percent; 0 = never chosen (variant builds measure it)
+#endif
+  const double eff[kNumTiles] = {1.10 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, 1.08 * kf, 1.22, 1.25,
+                                 TMAE_GEMM_E256x160 / 100.0 * kf};
   constexpr int forced = TMAE_GEMM_TILE;
   if (forced >= 0 && forced < kNumTiles && (allow_big || !tile_bf16_only(forced)))
     return TileChoice{kTileCand[forced][0], kTileCand[forced][1], kTileCand[forced][2]};
@@ -651,6 +662,7 @@ static int launch_gemm(const char* name, const T* w, long long ws1, long long ws
   const TileChoice tc = choose_tile(M, N, K, n1 * n2, GLDS && sizeof(T) == 2);
   if constexpr (GLDS && sizeof(T) == 2) {
     if (tc.nw == 8 && tc.bm == 192) return launch_one<GLDS, T, 256, 192, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
+    if (tc.nw == 8 && tc.bm == 160) return launch_one<GLDS, T, 256, 160, 4, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 4 && tc.bm == 160) return launch_one<GLDS, T, 128, 160, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 4 && tc.bm == 192) return launch_one<GLDS, T, 128, 192, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 8) return launch_one<GLDS, T, 256, 256, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
