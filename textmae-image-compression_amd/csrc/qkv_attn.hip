@@ -190,10 +190,13 @@ qkv_attn_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, const fl
   }
 }
 
+// ViT-B encoder (T 145): BK 32, two workgroups per CU -- 49.0 vs 51.6 us per launch, forward +2 % same box
+// (profiles/r04/c8_*).  K = 64 (T 65): BK 64 (the BK-32 rows padded to whole 128-row rounds add a third: 31.3 vs
+// 29.2 us).  A/B builds: tools/build_variant.sh qkv_attn.hip -DTMAE_QA_ENC_BK=64
 #ifndef TMAE_QA_ENC_BK
-#define TMAE_QA_ENC_BK 32  // A/B builds (tools/build_variant.sh qkv_attn.hip -DTMAE_QA_ENC_BK=64)
+#define TMAE_QA_ENC_BK 32
 #endif
-template <int DH, int HG, int TPAD, int BK = (DH == 64 ? TMAE_QA_ENC_BK : 64)>
+template <int DH, int HG, int TPAD, int BK = (DH == 64 && TPAD == 160 ? TMAE_QA_ENC_BK : 64)>
 static int qkv_attn_launch(const bf16* x, const bf16* w, const float* b, bf16* out, int B, int T, int H, float scale,
                            hipStream_t st) {
   hipLaunchKernelGGL((qkv_attn_kernel<DH, HG, TPAD, BK>), dim3(B * (H / HG)), dim3(qa::NW * 64), 0, st, x, w, b, out, T,
