@@ -575,10 +575,9 @@ struct TileChoice { int bn, bm, nw; };
 // The 8-wave 256 x 192 tile (waves 2 x 4, 128 x 48 each) exists for the tail: 9280- and 16448-row token
 // GEMMs whose 256 x 256 tile count lands just past a multiple of 256 CUs (enc qkv 333 tiles = 1.3
 // rounds, dec fc1 520 = 2.03, dec proj/fc2 130 = 0.5).
-static constexpr int kNumTiles = 10;
+static constexpr int kNumTiles = 9;
 static constexpr int kTileCand[kNumTiles][3] = {{256, 256, 8}, {128, 128, 4}, {64, 128, 4}, {32, 128, 4}, {64, 64, 4},
-                                                {32, 64, 4},   {256, 192, 8}, {128, 160, 4}, {128, 192, 4},
-                                                {256, 160, 8}};
+                                                {32, 64, 4},   {256, 192, 8}, {128, 160, 4}, {128, 192, 4}};
 // candidates only the bf16 LDS-DMA path instantiates
 static inline bool tile_bf16_only(int i) { return kTileCand[i][2] == 8 || i >= 7; }
 // eff = per-CU throughput relative to two 128 x 128 workgroups.  Forced-tile runs of the bench's token
@@ -598,17 +597,16 @@ static inline bool tile_bf16_only(int i) { return kTileCand[i][2] == 8 || i >= 7
 // leave (whole forward 8108 img/s vs 8041 without it).  Round 3 re-check at HEAD (profiles/r03/
 // s2_gemm_tiles_c13.log, s2_knob_c13_*): the pick within 3 % of the best forced tile on every token GEMM;
 // the efficiencies moved by +-20 % changed the forward by -2 % .. +0.3 %.  (192 x 128 never won: dropped.)
+// Round 4: an 8-wave 256 x 160 tile (half the L2 -> LDS bytes per MFMA of 2 x 128 x 160) measured slower when
+// forced (enc fc1 65.0 vs 63.5 us, dec fc1 66.2 vs 57.3) and -6.5 % on the forward when offered to the chooser
+// (profiles/r04/c9_*): dropped; the partial token-side DMA round it needed stays in the kernel.
 // Tuning experiments override these with a variant build (tools/build_variant.sh -DTMAE_GEMM_TILE=<i>).
 #ifndef TMAE_GEMM_TILE
 #define TMAE_GEMM_TILE -1
 #endif
 static inline TileChoice choose_tile(int M, int N, int K, int batch, bool allow_big) {
   const double kf = 1.0 + 0.12 * std::log2(std::max(K, 768) / 768.0);
-#ifndef TMAE_GEMM_E256x160
-#define TMAE_GEMM_E256x160 0  // percent; 0 = never chosen (variant builds measure it)
-#endif
-  const double eff[kNumTiles] = {1.10 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, 1.08 * kf, 1.22, 1.25,
-                                 TMAE_GEMM_E256x160 / 100.0 * kf};
+  const double eff[kNumTiles] = {1.10 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, 1.08 * kf, 1.22, 1.25};
   constexpr int forced = TMAE_GEMM_TILE;
   if (forced >= 0 && forced < kNumTiles && (allow_big || !tile_bf16_only(forced)))
     return TileChoice{kTileCand[forced][0], kTileCand[forced][1], kTileCand[forced][2]};
@@ -662,7 +660,6 @@ static int launch_gemm(const char* name, const T* w, long long ws1, long long ws
   const TileChoice tc = choose_tile(M, N, K, n1 * n2, GLDS && sizeof(T) == 2);
   if constexpr (GLDS && sizeof(T) == 2) {
     if (tc.nw == 8 && tc.bm == 192) return launch_one<GLDS, T, 256, 192, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
-    if (tc.nw == 8 && tc.bm == 160) return launch_one<GLDS, T, 256, 160, 4, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 4 && tc.bm == 160) return launch_one<GLDS, T, 128, 160, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 4 && tc.bm == 192) return launch_one<GLDS, T, 128, 192, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 8) return launch_one<GLDS, T, 256, 256, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
