@@ -31,7 +31,7 @@ def family(name):
     if "conv_halo_kernel" in name or ("gemm" in name and "ConvSrc" in name):
         return "lic_conv3x3"
     if "qkv_attn_kernel" in name:  # fused qkv GEMM + attention (bf16 inference): dh 64 encoder, dh 32 decoder
-        return "enc_qkv_attn" if "ILi64E" in name else "dec_qkv_attn"
+        return "enc_qkv_attn" if "qkv_attn_kernel<64," in name or "qkv_attn_kernelILi64E" in name else "dec_qkv_attn"
     if "mha_fwd" in name:
         return "enc_attn_core" if "<64>" in name or "ILi64E" in name else "dec_attn_core"
     if "layernorm_kernel" in name:
