@@ -41,7 +41,12 @@ def ev_time(fn, reps):
 def main():
     dt = torch.bfloat16
     out = {}
-    names = sys.argv[1:] or list(SHAPES)
+    torch.manual_seed(0)
+    args = sys.argv[1:]
+    eager = 0  # --eager N: N plain launches of each GEMM, no graphs or timing (PMC passes: tools/gemm_pmc.sh)
+    if args and args[0] == "--eager":
+        eager, args = int(args[1]), args[2:]
+    names = args or list(SHAPES)
     for name in names:
         M, N, K, act = SHAPES[name]
         x = torch.randn(M, K, device="cuda").to(dt)
@@ -50,6 +55,13 @@ def main():
         y = torch.empty(M, N, device="cuda", dtype=dt)
         mine = lambda: ops.linear(x, w, b, dt, act=act, out=y)
         ref = lambda: torch.nn.functional.linear(x, w, b.to(dt))
+        if eager:
+            for _ in range(eager):
+                mine()
+                ref()
+            torch.cuda.synchronize()
+            print(name, "eager", eager, flush=True)
+            continue
         reps = 20 if name != "big" else 5
         fl = 2.0 * M * N * K
         res = {}
@@ -58,6 +70,9 @@ def main():
         res["tf"] = round(fl / min(tm) / 1e12, 1)
         tr = [ev_time(ref, reps) for _ in range(5)]
         res["torch_tf"] = round(fl / min(tr) / 1e12, 1)
+        mine()
+        # bit pattern checksum: equal across variant libraries that keep the MFMA k-order
+        res["bits"] = int(y.view(torch.int16).to(torch.int64).mul_(torch.arange(1, N + 1, device="cuda")).sum().item())
         out[name] = res
         print(name, out[name], flush=True)
     print(json.dumps(out))
