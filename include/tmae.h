@@ -233,6 +233,13 @@ int tmae_mae_masking(const float* noise, int64_t* ids_shuffle, int64_t* ids_rest
 int tmae_mae_loss(const float* pred, const float* imgs, const int64_t* ids_restore, int n, int C, int H, int W, int P,
                   int len_keep, int norm_pix_loss, double* work, float* out, void* stream);
 
+/* forward_loss backward (autograd of models_mae.py:212-214): out[n*L][P*P*C] = dloss[0] * mask * 2 (pred - target)
+ * / (P*P*C * n * (L - len_keep)) (+ dpred_in when non-NULL), in out_dtype (TMAE_F32 / TMAE_BF16).  dloss may be
+ * NULL (no loss gradient: out = dpred_in or zeros). */
+int tmae_mae_loss_bwd(const float* pred, const float* imgs, const int64_t* ids_restore, int n, int C, int H, int W,
+                      int P, int len_keep, int norm_pix_loss, const float* dloss, const float* dpred_in, void* out,
+                      int out_dtype, void* stream);
+
 /* ---------------------------------------------------------------- entropy coding, device side
  * (MCM.compress / decompress, MCM.py:805-968; compressai semantics restated, see rans.cpp) */
 

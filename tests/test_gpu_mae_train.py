@@ -1,0 +1,110 @@
+"""MaskedAutoencoderViT training path (mae_train.py) against autograd through the pinned f32 oracle
+(oracle/mae_oracle.py, the reference models_mae.py forward restated; pinned to the reference's own outputs by
+tests/golden/mae_forward.npz in test_gpu_mae.py).
+
+loss and pred in f32 meet max|a-b| / max|b| <= 1e-3 (north_star tolerance), every parameter gradient
+max|a-b| / max|b| <= 1e-3 (measured ~1e-6); the bf16 path is bounded by the relative L2 of each gradient."""
+import os
+from functools import partial
+
+import pytest
+import torch
+from parity_log import check  # noqa: E402
+
+from oracle.mae_oracle import mae_forward
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def maxrel(a, b):
+    a, b = torch.as_tensor(a).double().cpu(), torch.as_tensor(b).double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def oracle_grads(m, imgs, noise, ratio, patch, heads, dec_heads, depth, dec_depth, norm_pix):
+    sd = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    loss, pred, mask = mae_forward(sd, imgs, noise, ratio, patch, heads, dec_heads, depth, dec_depth,
+                                   norm_pix=norm_pix)
+    loss.backward()
+    return loss.detach(), pred.detach(), mask, {k: v.grad for k, v in sd.items()}
+
+
+def run_train(m, imgs, noise, ratio):
+    m.zero_grad(set_to_none=True)
+    loss, pred, mask = m(imgs.to(DEV), ratio, noise=noise.to(DEV))
+    loss.backward()
+    for n, p in m.named_parameters():
+        if not p.requires_grad:
+            assert p.grad is None, n  # pos_embed / decoder_pos_embed: fixed sin-cos tables
+    return loss.detach(), pred.detach(), mask, {n: p.grad for n, p in m.named_parameters() if p.requires_grad}
+
+
+def tiny(tmae, norm_pix, dec_dim=32):
+    torch.manual_seed(21)
+    return tmae.MaskedAutoencoderViT(img_size=64, patch_size=16, in_chans=3, embed_dim=64, depth=2, num_heads=2,
+                                     decoder_embed_dim=dec_dim, decoder_depth=2, decoder_num_heads=1, mlp_ratio=4.0,
+                                     norm_layer=partial(torch.nn.LayerNorm, eps=1e-6), norm_pix_loss=norm_pix).to(DEV)
+
+
+@pytest.mark.parametrize("norm_pix", [False, True])
+def test_tiny_grads_f32_vs_oracle(tmae, norm_pix):
+    m = tiny(tmae, norm_pix)
+    imgs = torch.randn(3, 3, 64, 64, generator=torch.Generator().manual_seed(22))
+    noise = torch.rand(3, 16, generator=torch.Generator().manual_seed(23))
+    rl, rp, rm, rg = oracle_grads(m, imgs, noise, 0.75, 16, 2, 1, 2, 2, norm_pix)
+    loss, pred, mask, grads = run_train(m, imgs, noise, 0.75)
+    assert torch.equal(mask.cpu(), rm)
+    check(f"maxrel:mae_train_tiny_pred_np{int(norm_pix)}", maxrel(pred, rp), 1e-3)
+    assert abs(float(loss) - float(rl)) <= 1e-3 * abs(float(rl))
+    worst = 0.0
+    for name, g in grads.items():
+        worst = max(worst, maxrel(g, rg[name]))
+    check(f"maxrel:mae_train_tiny_grads_np{int(norm_pix)}", worst, 1e-3)
+
+
+def test_vitb_grads_f32_vs_oracle(tmae):
+    """mae_vit_base_patch16_dec512d8b (models_mae.py:223-228) at batch 2: every gradient against the oracle"""
+    torch.manual_seed(24)
+    m = tmae.mae_vit_base_patch16_dec512d8b().to(DEV)
+    imgs = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(25))
+    noise = torch.rand(2, 196, generator=torch.Generator().manual_seed(26))
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    rl, rp, rm, rg = oracle_grads(m, imgs, noise, 0.75, 16, 12, 16, 12, 8, False)
+    loss, pred, mask, grads = run_train(m, imgs, noise, 0.75)
+    assert torch.equal(mask.cpu(), rm)
+    check("maxrel:mae_train_vitb_pred", maxrel(pred, rp), 1e-3)
+    assert abs(float(loss) - float(rl)) <= 1e-3 * abs(float(rl))
+    worst, name_w = 0.0, None
+    for name, g in grads.items():
+        r = maxrel(g, rg[name])
+        if r > worst:
+            worst, name_w = r, name
+    check("maxrel:mae_train_vitb_grads", worst, 1e-3, note=name_w)
+
+
+def test_bf16_bounded_and_adam_steps(tmae):
+    """bf16 operands: gradients within a relative L2 bound of the f32 oracle; then FusedAdam steps on one batch
+    drive the loss down (the training loop a user of the reference runs)"""
+    from textmae_amd.optim import FusedAdam
+
+    m = tiny(tmae, True, dec_dim=64)
+    m.compute_dtype = torch.bfloat16
+    imgs = torch.randn(8, 3, 64, 64, generator=torch.Generator().manual_seed(27))
+    noise = torch.rand(8, 16, generator=torch.Generator().manual_seed(28))
+    rl, rp, rm, rg = oracle_grads(m, imgs, noise, 0.75, 16, 2, 1, 2, 2, True)
+    loss, pred, mask, grads = run_train(m, imgs, noise, 0.75)
+    worst = 0.0
+    for name, g in grads.items():
+        ref = rg[name].double()
+        worst = max(worst, float((g.double().cpu() - ref).norm() / ref.norm().clamp_min(1e-30)))
+    check("relL2:mae_train_bf16_grads", worst, 2e-2)  # measured 9.2e-3
+    opt = FusedAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
+    first = None
+    for _ in range(8):
+        opt.zero_grad()
+        loss, _, _ = m(imgs.to(DEV), 0.75, noise=noise.to(DEV))
+        loss.backward()
+        opt.step()
+        first = float(loss) if first is None else first
+    assert float(loss) < 0.9 * first, (first, float(loss))

@@ -124,6 +124,7 @@ SIGNATURES = {
     "tmae_gemm_plan": [I, I, I, I, I, ctypes.c_char_p, I],
     "tmae_mae_masking": [P, P, P, P, I, I, I, P],
     "tmae_mae_loss": [P, P, P, I, I, I, I, I, I, I, P, P, P],
+    "tmae_mae_loss_bwd": [P, P, P, I, I, I, I, I, I, I, P, P, P, I, P],
     "tmae_gc_slices_code": [P, I, I, P, P, LL, I, P, I, P, I, I, P, I, I, I, I, I, P, P, P, I, P],
     "tmae_gc_indexes": [P, LL, I, I, I, I, I, P, I, F, P, P],
     "tmae_gc_dequantize": [P, P, LL, I, I, I, I, I, I, P, I, I, P, I, P],

@@ -60,6 +60,38 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// the target of patch `row` (= b * L + l) in the lane-strided layout t[k] = value lane + 64 k of the patchified row
+__device__ __forceinline__ void mae_target(const float* __restrict__ imgs, int row, int L, int G, int P, int C, int H,
+                                           int W, int norm_pix, int lane, float (&t)[MAE_VPL]) {
+  const int D = P * P * C;
+  const int b = row / L, l = row - b * L;
+  const int hy = l / G, hx = l - hy * G;
+  const float* img = imgs + (size_t)b * C * H * W + (size_t)(hy * P) * W + hx * P;
+  float s = 0.0f;
+#pragma unroll
+  for (int k = 0; k < MAE_VPL; ++k) {
+    const int e = lane + 64 * k;
+    t[k] = 0.0f;
+    if (e < D) {
+      const int q = e / C, c = e - q * C;  // e = (py * P + px) * C + c
+      const int py = q / P, px = q - py * P;
+      t[k] = img[((size_t)c * H + py) * W + px];
+      s += t[k];
+    }
+  }
+  if (norm_pix) {
+    const float mean = wave_sum(s) / (float)D;
+    float v = 0.0f;
+#pragma unroll
+    for (int k = 0; k < MAE_VPL; ++k)
+      if (lane + 64 * k < D) v += (t[k] - mean) * (t[k] - mean);
+    const float var = wave_sum(v) / (float)(D - 1);
+    const float inv = 1.0f / sqrtf(var + 1e-6f);
+#pragma unroll
+    for (int k = 0; k < MAE_VPL; ++k) t[k] = (t[k] - mean) * inv;
+  }
+}
+
 __global__ void __launch_bounds__(256)
 mae_loss_partial_kernel(const float* __restrict__ pred, const float* __restrict__ imgs,
                         const int64_t* __restrict__ ids_restore, int n, int L, int G, int P, int C, int H, int W,
@@ -70,32 +102,8 @@ mae_loss_partial_kernel(const float* __restrict__ pred, const float* __restrict_
   double num = 0.0, den = 0.0;
   for (int row = blockIdx.x * 4 + wave; row < n * L; row += gridDim.x * 4) {
     const int b = row / L, l = row - b * L;
-    const int hy = l / G, hx = l - hy * G;
-    const float* img = imgs + (size_t)b * C * H * W + (size_t)(hy * P) * W + hx * P;
     float t[MAE_VPL];
-    float s = 0.0f;
-#pragma unroll
-    for (int k = 0; k < MAE_VPL; ++k) {
-      const int e = lane + 64 * k;
-      t[k] = 0.0f;
-      if (e < D) {
-        const int q = e / C, c = e - q * C;  // e = (py * P + px) * C + c
-        const int py = q / P, px = q - py * P;
-        t[k] = img[((size_t)c * H + py) * W + px];
-        s += t[k];
-      }
-    }
-    if (norm_pix) {
-      const float mean = wave_sum(s) / (float)D;
-      float v = 0.0f;
-#pragma unroll
-      for (int k = 0; k < MAE_VPL; ++k)
-        if (lane + 64 * k < D) v += (t[k] - mean) * (t[k] - mean);
-      const float var = wave_sum(v) / (float)(D - 1);
-      const float inv = 1.0f / sqrtf(var + 1e-6f);
-#pragma unroll
-      for (int k = 0; k < MAE_VPL; ++k) t[k] = (t[k] - mean) * inv;
-    }
+    mae_target(imgs, row, L, G, P, C, H, W, norm_pix, lane, t);
     const float* pr = pred + (size_t)row * D;
     float se = 0.0f;
 #pragma unroll
@@ -155,4 +163,59 @@ extern "C" int tmae_mae_loss(const float* pred, const float* imgs, const int64_t
                      G, P, C, H, W, keep, norm_pix_loss, work);
   hipLaunchKernelGGL(mae_loss_final_kernel, dim3(1), dim3(256), 0, st, work, MAE_LOSS_BLOCKS, out);
   TMAE_LAUNCH_CHECK("tmae_mae_loss");
+}
+
+// ------------------------------------------------------------------ masked MSE backward
+// d loss / d pred[b][l][e] = g * mask[b][l] * 2 (pred - target) / (D * sum(mask)), sum(mask) = n (L - len_keep)
+// (autograd of models_mae.py:212-214); plus an incoming gradient of pred itself when dpred_in is given.
+// One wave per patch row, written in the operand dtype of the decoder_pred weight / data gradients.
+template <typename OT>
+__global__ void __launch_bounds__(256)
+mae_loss_bwd_kernel(const float* __restrict__ pred, const float* __restrict__ imgs, const int64_t* __restrict__ ids_restore,
+                    int n, int L, int G, int P, int C, int H, int W, int keep, int norm_pix, const float* __restrict__ dloss,
+                    const float* __restrict__ dpred_in, OT* __restrict__ out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int D = P * P * C;
+  const float msum = (float)n * (float)(L - keep);
+  const float g = dloss ? dloss[0] : 0.0f;
+  for (int row = blockIdx.x * 4 + wave; row < n * L; row += gridDim.x * 4) {
+    const float m = ids_restore[row] >= keep ? 1.0f : 0.0f;
+    const float sc = m > 0.0f && msum > 0.0f ? g * m / msum / (float)D : 0.0f;
+    const float* pr = pred + (size_t)row * D;
+    OT* o = out + (size_t)row * D;
+    const float* di = dpred_in ? dpred_in + (size_t)row * D : nullptr;
+    float t[MAE_VPL];
+    if (sc != 0.0f) mae_target(imgs, row, L, G, P, C, H, W, norm_pix, lane, t);
+#pragma unroll
+    for (int k = 0; k < MAE_VPL; ++k) {
+      const int e = lane + 64 * k;
+      if (e < D) {
+        float v = sc != 0.0f ? 2.0f * (pr[e] - t[k]) * sc : 0.0f;
+        if (di) v += di[e];
+        o[e] = (OT)v;
+      }
+    }
+  }
+}
+
+extern "C" int tmae_mae_loss_bwd(const float* pred, const float* imgs, const int64_t* ids_restore, int n, int C, int H,
+                                 int W, int P, int keep, int norm_pix_loss, const float* dloss, const float* dpred_in,
+                                 void* out, int out_dtype, void* stream) {
+  TMAE_REQUIRE(pred && imgs && ids_restore && out && P > 0 && H % P == 0 && W == H,
+               "tmae_mae_loss_bwd: bad arguments (H=%d W=%d P=%d)", H, W, P);
+  TMAE_REQUIRE(P * P * C <= 64 * MAE_VPL && P * P * C > 1, "tmae_mae_loss_bwd: patch of %d values unsupported",
+               P * P * C);
+  TMAE_REQUIRE(out_dtype == TMAE_F32 || out_dtype == TMAE_BF16, "tmae_mae_loss_bwd: out dtype %d", out_dtype);
+  const int G = H / P, L = G * G;
+  if (n == 0) return TMAE_OK;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = ceil_div(n * L, 4);
+  const dim3 grid((unsigned)(nb < 4096 ? nb : 4096));
+  if (out_dtype == TMAE_BF16)
+    hipLaunchKernelGGL(mae_loss_bwd_kernel<bf16>, grid, dim3(256), 0, st, pred, imgs, ids_restore, n, L, G, P, C, H, W,
+                       keep, norm_pix_loss, dloss, dpred_in, (bf16*)out);
+  else
+    hipLaunchKernelGGL(mae_loss_bwd_kernel<float>, grid, dim3(256), 0, st, pred, imgs, ids_restore, n, L, G, P, C, H,
+                       W, keep, norm_pix_loss, dloss, dpred_in, (float*)out);
+  TMAE_LAUNCH_CHECK("tmae_mae_loss_bwd");
 }

@@ -54,6 +54,7 @@ class MaskedAutoencoderViT(nn.Module):
         # MI355X execution settings (not part of the reference surface)
         self.compute_dtype = torch.float32
         self._exec = None
+        self._train_exec = None
 
     # ---------------------------------------------------------------------------------- init
     def initialize_weights(self):
@@ -101,12 +102,15 @@ class MaskedAutoencoderViT(nn.Module):
         return x.reshape(x.shape[0], 3, h * p, h * p)
 
     # ---------------------------------------------------------------------------------- execution
-    def _check(self, imgs):
+    def _check(self, imgs, whole=False):
         if not imgs.is_cuda:
             raise ValueError("MaskedAutoencoderViT runs on the MI355X kernels: move the model and inputs to the GPU")
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError(
-                "training-mode autograd is not available in this build: run forward under torch.no_grad()")
+        if not whole and self._training_call():
+            raise NotImplementedError("autograd through forward_encoder / forward_decoder alone is not available in "
+                                      "this build: train through forward() (mae_train.py), or run under torch.no_grad()")
+
+    def _training_call(self):
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
 
     def _check_supported(self):
         """what the kernels cover: head dims 32 / 64 / 80 (attention)"""
@@ -169,8 +173,14 @@ class MaskedAutoencoderViT(nn.Module):
         return (loss * mask).sum() / mask.sum()
 
     def forward(self, imgs, mask_ratio=0.75, noise=None):
-        """models_mae.py:216-220 -> (loss, pred [N, L, p*p*3], mask [N, L])"""
-        self._check(imgs)
+        """models_mae.py:216-220 -> (loss, pred [N, L, p*p*3], mask [N, L]); under autograd the training path
+        (mae_train.py: HIP backward of the whole model)"""
+        self._check(imgs, whole=True)
+        if self._training_call():
+            self._check_supported()
+            from .mae_train import train_forward
+
+            return train_forward(self, imgs, mask_ratio, noise)
         with torch.no_grad():
             imgs = imgs.float().contiguous()
             keep = self._len_keep(mask_ratio)

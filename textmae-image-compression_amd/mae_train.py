@@ -1,0 +1,191 @@
+"""Training path of MaskedAutoencoderViT (reference models/MAE/models_mae.py:216-220 under autograd:
+``loss, pred, mask = model(imgs, mask_ratio)``, ``loss.backward()``).
+
+As for MCM (mcm_train.py), one ``torch.autograd.Function`` covers the model: its forward runs the inference
+kernels while keeping what the backward needs (per-block LayerNorm outputs, GELU inputs, attention log-sum-exp,
+the gathered kept patches); its backward is the reverse pass on HIP kernels writing every parameter gradient into
+one flat f32 buffer whose views autograd adopts as ``p.grad``:
+
+  forward_loss (198-214)         tmae_mae_loss_bwd: mask * 2 (pred - target) / (p*p*c * sum(mask)), norm_pix targets
+  decoder_pred / decoder_norm    split-K TN weight gradient, transposed-weight data gradient, LayerNorm backward
+  decoder blocks                 the timm Block backward shared with MCM (_VitTrainBase._block_bwd)
+  decoder_embed + mask_token     unshuffle gather of the token gradients (172-190: the cls row stays first), the
+                                 mask-token gradient summed over the masked positions
+  norm, encoder blocks           LayerNorm over every token (cls included), Block backward
+  patch_embed / cls_token        weight gradient over the kept patches (the conv16/s16 as a GEMM), column sums
+pos_embed / decoder_pos_embed are fixed sin-cos tables (requires_grad=False in the reference) and get none.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from . import train_ops as T
+from .mcm_train import _VitTrainBase, _Weights, _block_params
+
+
+class MAETrainExec(_VitTrainBase):
+    """Workspaces + saved activations of one MAE training forward for (batch, len_keep, dtype, device)."""
+
+    def __init__(self, m, batch, keep, dtype, device):
+        self.m, self.batch, self.keep, self.dtype, self.device = m, batch, keep, dtype, device
+        self.w = _Weights(dtype)
+        self.P = m.patch_embed.patch_size[0]
+        self.L = m.patch_embed.num_patches
+        C = m.patch_embed.proj.in_channels
+        if (C * self.P * self.P) % 8:
+            raise ValueError(f"MAE training: patch rows of {C * self.P * self.P} values (a multiple of 8 needed by "
+                             "the weight-gradient GEMM; patch 14 trains nowhere in this build)")
+        self._layout()
+
+    def _grad_order(self):
+        m = self.m
+        out = [m.decoder_pred.weight, m.decoder_pred.bias, m.decoder_norm.weight, m.decoder_norm.bias]
+        for blk in reversed(m.decoder_blocks):
+            out += _block_params(blk)
+        out += [m.decoder_embed.weight, m.decoder_embed.bias, m.mask_token, m.norm.weight, m.norm.bias]
+        for blk in reversed(m.blocks):
+            out += _block_params(blk)
+        out += [m.patch_embed.proj.weight, m.patch_embed.proj.bias, m.cls_token]
+        seen = {id(p) for p in out}
+        missing = [n for n, p in m.named_parameters() if p.requires_grad and id(p) not in seen]
+        if missing:
+            raise RuntimeError(f"MAE training executor does not cover parameters {missing}")
+        return out
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, imgs, noise):
+        """-> (loss 0-d f32, pred f32 [B*L, p*p*c], mask [B, L])"""
+        m, dt, B, keep, W = self.m, self.dtype, self.batch, self.keep, self.w
+        E, Dd = m.pos_embed.shape[-1], m.decoder_pos_embed.shape[-1]
+        L, P, Te = self.L, self.P, keep + 1
+        imgs = imgs.float().contiguous()
+        if imgs.shape[2:] != tuple(m.patch_embed.img_size):
+            raise ValueError(f"Input image size {tuple(imgs.shape[2:])} doesn't match model {m.patch_embed.img_size}")
+        self.imgs = imgs
+        self.w.refresh()
+        shuf, rest, mask = ops.mae_masking(noise, keep)
+        self.shuf, self.rest = shuf, rest
+        # patch embed of the kept patches + pos, cls row (models_mae.py:150-170)
+        pw = m.patch_embed.proj.weight
+        pos = m.pos_embed.detach()
+        tok = torch.empty((B * Te, E), dtype=torch.float32, device=self.device)
+        ops.patch_embed(imgs, shuf, W.nt(pw), m.patch_embed.proj.bias.detach(), pos, tok, keep, P, dt)
+        ops.cls_rows(tok, m.cls_token.detach(), pos, B, Te, E)
+        self.patches = T.patch_gather(imgs, shuf, self._e(B * keep, pw[0].numel()), keep, P, dt)
+        self.enc = []
+        for blk in m.blocks:
+            tok = self._block_fwd(blk, tok, B, Te)
+        self.tok_last = tok
+        self.lat = ops.layernorm(tok, m.norm.weight, m.norm.bias, m.norm.eps, dt)
+        # decoder (172-196): embed every latent row, mask tokens, unshuffle, pos; blocks; norm; pred
+        dpos = m.decoder_pos_embed.detach()
+        dec = torch.empty((B * (L + 1), Dd), dtype=torch.float32, device=self.device)
+        ops.decoder_embed(self.lat, W.nt(m.decoder_embed.weight), m.decoder_embed.bias.detach(), dpos, shuf, dec, B,
+                          Te, L, dt)
+        ops.mask_rows(dec, m.mask_token.detach(), dpos, shuf, B, L, Te, Dd)
+        self.dec = []
+        for blk in m.decoder_blocks:
+            dec = self._block_fwd(blk, dec, B, L + 1, store=self.dec)
+        self.dec_last = dec
+        self.dn = ops.layernorm(dec, m.decoder_norm.weight, m.decoder_norm.bias, m.decoder_norm.eps, dt, rows=B * L,
+                                row_group=L, group_stride=L + 1, row_offset=1)
+        self.pred = ops.linear(self.dn, W.nt(m.decoder_pred.weight), m.decoder_pred.bias.detach(), dt,
+                               out_dtype=torch.float32)
+        loss = ops.mae_loss(self.pred, imgs, rest, keep, P, m.norm_pix_loss)
+        return loss, self.pred, mask
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, dloss, dpred, gflat, sync=None):
+        m, dt, W, B, keep = self.m, self.dtype, self.w, self.batch, self.keep
+        E, Dd = m.pos_embed.shape[-1], m.decoder_pos_embed.shape[-1]
+        L, P, Te = self.L, self.P, keep + 1
+        self.gflat, self.sync = gflat, sync
+        if sync is not None:
+            sync.attach(gflat)
+        G = self.grad
+        npred = self.pred.shape[1]
+        # ---- forward_loss + decoder_pred (models_mae.py:193, 198-214)
+        dl = dloss.float().contiguous().reshape(1) if dloss is not None else None
+        dp_in = dpred.float().contiguous() if dpred is not None else None
+        dP = T.mae_loss_bwd(self.pred, self.imgs, self.rest, keep, P, m.norm_pix_loss, dl, dp_in,
+                            self._e(B * L, npred), dt)
+        T.wgrad(dP, self.dn, npred, Dd, B * L, G(m.decoder_pred.weight), dt, bias=G(m.decoder_pred.bias))
+        ddn = torch.empty((B * L, Dd), dtype=torch.float32, device=self.device)
+        T.dgrad_linear(dP, W.t(m.decoder_pred.weight), B * L, npred, Dd, dt, out=ddn)
+        # ---- decoder_norm (the cls row gets no gradient: pred drops it) + blocks
+        ddec = self._z(B * (L + 1), Dd)
+        ddec_op = ddec if dt == torch.float32 else self._z(B * (L + 1), Dd, dtype=dt)
+        T.layernorm_bwd(self.dec_last, m.decoder_norm.weight, ddn, ddec, B * L, Dd, m.decoder_norm.eps,
+                        G(m.decoder_norm.weight), G(m.decoder_norm.bias), dxop=None if dt == torch.float32 else ddec_op,
+                        row_group=L, group_stride=L + 1, row_offset=1)
+        self._ready(m.decoder_norm.bias)
+        for blk, s in zip(reversed(m.decoder_blocks), reversed(self.dec)):
+            ddec, ddec_op = self._block_bwd(blk, s, ddec, ddec_op, B, L + 1)
+            self._ready(_block_params(blk)[-1])
+        # ---- decoder_embed + mask tokens: row 0 of each image is the cls row, rows 1..keep the kept patches
+        dtok = self._e(B * Te, Dd)
+        T.decoder_embed_bwd_gather(ddec, self.shuf, dtok, B, Te, L, Dd, dt, dmask=G(m.mask_token).view(-1))
+        T.wgrad(dtok, self.lat, Dd, E, B * Te, G(m.decoder_embed.weight), dt, bias=G(m.decoder_embed.bias))
+        dlat = torch.empty((B * Te, E), dtype=torch.float32, device=self.device)
+        T.dgrad_linear(dtok, W.t(m.decoder_embed.weight), B * Te, Dd, E, dt, out=dlat)
+        self._ready(m.mask_token)
+        # ---- encoder norm (every row, cls included) + blocks
+        dt_tok = self._z(B * Te, E)
+        dt_op = dt_tok if dt == torch.float32 else self._z(B * Te, E, dtype=dt)
+        T.layernorm_bwd(self.tok_last, m.norm.weight, dlat, dt_tok, B * Te, E, m.norm.eps, G(m.norm.weight),
+                        G(m.norm.bias), dxop=None if dt == torch.float32 else dt_op)
+        self._ready(m.norm.bias)
+        for blk, s in zip(reversed(m.blocks), reversed(self.enc)):
+            dt_tok, dt_op = self._block_bwd(blk, s, dt_tok, dt_op, B, Te)
+            self._ready(_block_params(blk)[-1])
+        # ---- patch embed (kept patches) + cls token
+        pw = m.patch_embed.proj.weight
+        T.wgrad(dt_op, self.patches, E, pw[0].numel(), B * keep, G(pw), dt, lda=E, a_remap=(keep, Te, 1))
+        T.colsum(dt_tok, B * keep, E, G(m.patch_embed.proj.bias), row_group=keep, group_stride=Te, row_offset=1)
+        T.colsum(dt_tok, B, E, G(m.cls_token).view(-1), row_group=1, group_stride=Te, row_offset=0)
+        self._ready(m.cls_token)
+
+
+class _MAETrainFn(torch.autograd.Function):
+    """MaskedAutoencoderViT.forward as one autograd node: (imgs, *params) -> (loss, pred, mask)"""
+
+    @staticmethod
+    def forward(ctx, ex, noise, imgs, *params):
+        loss, pred, mask = ex.forward(imgs, noise)
+        ctx.ex, ctx.params = ex, params
+        ctx.mark_non_differentiable(mask)
+        return loss, pred, mask
+
+    @staticmethod
+    def backward(ctx, dloss, dpred, dmask):
+        ex, params = ctx.ex, ctx.params
+        fresh = any(p.grad is not None for p in params if p.requires_grad)
+        gflat = ex.grads_buffer(fresh)
+        sync = getattr(ex.m, "grad_sync", None)
+        ex.backward(dloss, dpred, gflat, sync=sync)
+        if sync is not None:
+            sync.finish()
+        out = []
+        for p in params:
+            if not p.requires_grad:
+                out.append(None)
+            else:
+                off = ex.offsets[id(p)]
+                out.append(gflat[off:off + p.numel()].view(p.shape))
+        return (None, None, None, *out)
+
+
+def train_forward(m, imgs, mask_ratio, noise):
+    """MaskedAutoencoderViT.forward with autograd: (loss, pred [N, L, p*p*c], mask [N, L])"""
+    imgs = imgs.float().contiguous()
+    B = imgs.shape[0]
+    keep = m._len_keep(mask_ratio)
+    ex = getattr(m, "_train_exec", None)
+    if ex is None or (ex.batch, ex.keep, ex.dtype, ex.device) != (B, keep, m.compute_dtype, imgs.device):
+        ex = m._train_exec = MAETrainExec(m, B, keep, m.compute_dtype, imgs.device)
+    if noise is None:
+        noise = torch.rand(B, ex.L, device=imgs.device)
+    params = [p for p in m.parameters()]
+    loss, pred, mask = _MAETrainFn.apply(ex, noise.to(imgs.device).float().contiguous(), imgs, *params)
+    return loss, pred.view(B, ex.L, -1), mask

@@ -173,27 +173,13 @@ class _BlockSaved:
     __slots__ = ("x", "a1", "qkv", "att", "lse", "xmid", "a2", "hpre", "h")
 
 
-class TrainExec:
-    """Workspaces + saved activations of one training forward for (batch, dtype, device)."""
+class _VitTrainBase:
+    """What the MCM and MAE training executors share: workspaces, the flat gradient buffer laid out in the order
+    the backward finishes the parameters (DP buckets), and the timm Block forward (keeping what its backward
+    needs) / backward."""
 
-    def __init__(self, m, batch, dtype, device):
-        self.m, self.batch, self.dtype, self.device = m, batch, dtype, device
-        self.w = _Weights(dtype)
-        K = m.num_keep_patches
-        self.P = m.encoder_embed.patch_size[0]
-        self.img = m.encoder_embed.img_size[0]
-        self.L = m.encoder_embed.num_patches
-        self.g = int(round(K ** 0.5))
-        if self.g * self.g != K:
-            raise ValueError(f"num_keep_patches={K} must be a perfect square (MCM.py:729-732)")
-        self.hz = ((self.g + 1) // 2 + 1) // 2
-        if self.hz * 4 != self.g:
-            raise ValueError(f"sqrt(num_keep_patches)={self.g} must be a multiple of 4 so h_s returns to the y grid")
-        self.Mp = batch * K
-        self.sw = m.latent_depth // m.num_slices
-        self.ms = m.num_slices // 2
-        self.mid = [l.out_channels for l in _convs(m.cc_transform_mean[0])]
-        # parameter gradient layout: the order in which the backward finishes them (DP buckets)
+    def _layout(self):
+        """parameter gradient layout: the order in which the backward finishes them (DP buckets)"""
         self.params = [p for p in self._grad_order() if p.requires_grad]
         self.offsets = {}
         off = 0
@@ -215,6 +201,107 @@ class TrainExec:
         if self.dtype == torch.float32:
             return src
         return T.relayout(src, torch.empty(src.shape, dtype=self.dtype, device=self.device), (src.numel(),), (1,))
+
+    def grads_buffer(self, fresh):
+        if fresh or self._gflat is None:
+            buf = torch.empty(self.numel, dtype=torch.float32, device=self.device)
+            if fresh:
+                return buf
+            self._gflat = buf
+        return self._gflat
+
+    def grad(self, p):
+        off = self.offsets[id(p)]
+        return self.gflat[off:off + p.numel()].view(p.shape)
+
+    def _ready(self, p):
+        """every gradient up to and including p's is final (DP bucket hand-off)"""
+        if self.sync is not None:
+            self.sync.ready(self.offsets[id(p)] + p.numel())
+
+    def _block_fwd(self, blk, x, B, Tn, store=None):
+        dt, W = self.dtype, self.w
+        rows, D = x.shape
+        s = _BlockSaved()
+        s.x = x
+        s.a1 = ops.layernorm(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, dt)
+        s.qkv = ops.linear(s.a1, W.nt(blk.attn.qkv.weight), _bias(blk.attn.qkv.bias), dt)
+        H = blk.attn.num_heads
+        s.att = self._e(rows, D)
+        s.lse = torch.empty((B * H * Tn,), dtype=torch.float32, device=self.device)
+        T.mha_lse(s.qkv, B, Tn, H, D // H, blk.attn.scale, dt, s.att, s.lse)
+        s.xmid = torch.empty_like(x)
+        T.linear_residual_out(s.att, W.nt(blk.attn.proj.weight), _bias(blk.attn.proj.bias), x, s.xmid, dt)
+        s.a2 = ops.layernorm(s.xmid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, dt)
+        hid = blk.mlp.fc1.out_features
+        s.h, s.hpre = self._e(rows, hid), self._e(rows, hid)
+        T.linear_pre(s.a2, W.nt(blk.mlp.fc1.weight), _bias(blk.mlp.fc1.bias), dt, ACT_GELU, s.h, s.hpre)
+        out = torch.empty_like(x)
+        T.linear_residual_out(s.h, W.nt(blk.mlp.fc2.weight), _bias(blk.mlp.fc2.bias), s.xmid, out, dt)
+        (self.enc if store is None else store).append(s)
+        return out
+
+    def _block_bwd(self, blk, s, dres, dres_op, B, Tn):
+        """timm Block backward: (dres f32, dres in the operand dtype) -> the same for the block input"""
+        dt, W, G = self.dtype, self.w, self.grad
+        rows, D = dres.shape
+        hid = blk.mlp.fc1.out_features
+        H = blk.attn.num_heads
+        f32 = dt == torch.float32
+        # fc2 (+ GELU of fc1 in the data-gradient epilogue)
+        T.wgrad(dres_op, s.h, D, hid, rows, G(blk.mlp.fc2.weight), dt)  # fc2.bias: folded into norm2's backward
+        dh = self._e(rows, hid)
+        T.dgrad_linear(dres_op, W.t(blk.mlp.fc2.weight), rows, D, hid, dt, out=dh, pre=s.hpre)
+        # fc1
+        T.wgrad(dh, s.a2, hid, D, rows, G(blk.mlp.fc1.weight), dt, bias=G(blk.mlp.fc1.bias))
+        da2 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
+        T.dgrad_linear(dh, W.t(blk.mlp.fc1.weight), rows, hid, D, dt, out=da2)
+        # norm2 + residual
+        dmid = torch.empty((rows, D), dtype=torch.float32, device=self.device)
+        dmid_op = dmid if f32 else self._e(rows, D)
+        T.layernorm_bwd(s.xmid, blk.norm2.weight, da2, dmid, rows, D, blk.norm2.eps, G(blk.norm2.weight),
+                        G(blk.norm2.bias), dres=dres, dxop=None if f32 else dmid_op, dres_colsum=G(blk.mlp.fc2.bias))
+        # proj
+        T.wgrad(dmid_op, s.att, D, D, rows, G(blk.attn.proj.weight), dt)  # proj.bias: folded into norm1's backward
+        datt = self._e(rows, D)
+        T.dgrad_linear(dmid_op, W.t(blk.attn.proj.weight), rows, D, D, dt, out=datt)
+        # attention core
+        dqkv = self._e(rows, 3 * D)
+        T.mha_bwd(s.qkv, s.att, datt, s.lse, dqkv, B, Tn, H, D // H, blk.attn.scale, dt)
+        # qkv
+        T.wgrad(dqkv, s.a1, 3 * D, D, rows, G(blk.attn.qkv.weight), dt,
+                bias=G(blk.attn.qkv.bias) if blk.attn.qkv.bias is not None else None)
+        da1 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
+        T.dgrad_linear(dqkv, W.t(blk.attn.qkv.weight), rows, 3 * D, D, dt, out=da1)
+        # norm1 + residual
+        dx = torch.empty((rows, D), dtype=torch.float32, device=self.device)
+        dx_op = dx if f32 else self._e(rows, D)
+        T.layernorm_bwd(s.x, blk.norm1.weight, da1, dx, rows, D, blk.norm1.eps, G(blk.norm1.weight),
+                        G(blk.norm1.bias), dres=dmid, dxop=None if f32 else dx_op, dres_colsum=G(blk.attn.proj.bias))
+        return dx, dx_op
+
+
+class TrainExec(_VitTrainBase):
+    """Workspaces + saved activations of one training forward for (batch, dtype, device)."""
+
+    def __init__(self, m, batch, dtype, device):
+        self.m, self.batch, self.dtype, self.device = m, batch, dtype, device
+        self.w = _Weights(dtype)
+        K = m.num_keep_patches
+        self.P = m.encoder_embed.patch_size[0]
+        self.img = m.encoder_embed.img_size[0]
+        self.L = m.encoder_embed.num_patches
+        self.g = int(round(K ** 0.5))
+        if self.g * self.g != K:
+            raise ValueError(f"num_keep_patches={K} must be a perfect square (MCM.py:729-732)")
+        self.hz = ((self.g + 1) // 2 + 1) // 2
+        if self.hz * 4 != self.g:
+            raise ValueError(f"sqrt(num_keep_patches)={self.g} must be a multiple of 4 so h_s returns to the y grid")
+        self.Mp = batch * K
+        self.sw = m.latent_depth // m.num_slices
+        self.ms = m.num_slices // 2
+        self.mid = [l.out_channels for l in _convs(m.cc_transform_mean[0])]
+        self._layout()
 
     def _grad_order(self):
         m = self.m
@@ -379,28 +466,6 @@ class TrainExec:
         x_hat = torch.empty((B, imgs.shape[1], self.img, self.img), dtype=torch.float32, device=self.device)
         ops.decoder_pred(self.dn, W.nt(m.decoder_pred.weight), m.decoder_pred.bias.detach(), x_hat, B, L, P, dt)
         return x_hat, self.YLIK, self.ZLIK
-
-    def _block_fwd(self, blk, x, B, Tn, store=None):
-        dt, W = self.dtype, self.w
-        rows, D = x.shape
-        s = _BlockSaved()
-        s.x = x
-        s.a1 = ops.layernorm(x, blk.norm1.weight, blk.norm1.bias, blk.norm1.eps, dt)
-        s.qkv = ops.linear(s.a1, W.nt(blk.attn.qkv.weight), _bias(blk.attn.qkv.bias), dt)
-        H = blk.attn.num_heads
-        s.att = self._e(rows, D)
-        s.lse = torch.empty((B * H * Tn,), dtype=torch.float32, device=self.device)
-        T.mha_lse(s.qkv, B, Tn, H, D // H, blk.attn.scale, dt, s.att, s.lse)
-        s.xmid = torch.empty_like(x)
-        T.linear_residual_out(s.att, W.nt(blk.attn.proj.weight), _bias(blk.attn.proj.bias), x, s.xmid, dt)
-        s.a2 = ops.layernorm(s.xmid, blk.norm2.weight, blk.norm2.bias, blk.norm2.eps, dt)
-        hid = blk.mlp.fc1.out_features
-        s.h, s.hpre = self._e(rows, hid), self._e(rows, hid)
-        T.linear_pre(s.a2, W.nt(blk.mlp.fc1.weight), _bias(blk.mlp.fc1.bias), dt, ACT_GELU, s.h, s.hpre)
-        out = torch.empty_like(x)
-        T.linear_residual_out(s.h, W.nt(blk.mlp.fc2.weight), _bias(blk.mlp.fc2.bias), s.xmid, out, dt)
-        (self.enc if store is None else store).append(s)
-        return out
 
     def _h_s_fwd(self, seq, out_final, ld_final):
         dt, W, B = self.dtype, self.w, self.batch
@@ -594,14 +659,6 @@ class TrainExec:
         return saved
 
     # ------------------------------------------------------------------ backward
-    def grads_buffer(self, fresh):
-        if fresh or self._gflat is None:
-            buf = torch.empty(self.numel, dtype=torch.float32, device=self.device)
-            if fresh:
-                return buf
-            self._gflat = buf
-        return self._gflat
-
     def backward(self, dxhat, dylik, dzlik, gflat, sync=None):
         """full reverse pass; every parameter's gradient lands in gflat (views per self.offsets)"""
         m, dt, W, B = self.m, self.dtype, self.w, self.batch
@@ -729,15 +786,6 @@ class TrainExec:
         T.colsum(dt_tok, B, E, G(m.cls_token).view(-1), row_group=1, group_stride=Te, row_offset=0)
         self._ready(m.cls_token)
 
-    def grad(self, p):
-        off = self.offsets[id(p)]
-        return self.gflat[off:off + p.numel()].view(p.shape)
-
-    def _ready(self, p):
-        """every gradient up to and including p's is final (DP bucket hand-off)"""
-        if self.sync is not None:
-            self.sync.ready(self.offsets[id(p)] + p.numel())
-
     def _eb_grads(self, eb):
         from ._lib import EBParams
 
@@ -749,45 +797,6 @@ class TrainExec:
                 g.factor[i] = self.grad(getattr(eb, f"_factor{i}")).data_ptr()
         g.quantiles = self.grad(eb.quantiles).data_ptr()
         return g
-
-    def _block_bwd(self, blk, s, dres, dres_op, B, Tn):
-        """timm Block backward: (dres f32, dres in the operand dtype) -> the same for the block input"""
-        dt, W, G = self.dtype, self.w, self.grad
-        rows, D = dres.shape
-        hid = blk.mlp.fc1.out_features
-        H = blk.attn.num_heads
-        f32 = dt == torch.float32
-        # fc2 (+ GELU of fc1 in the data-gradient epilogue)
-        T.wgrad(dres_op, s.h, D, hid, rows, G(blk.mlp.fc2.weight), dt)  # fc2.bias: folded into norm2's backward
-        dh = self._e(rows, hid)
-        T.dgrad_linear(dres_op, W.t(blk.mlp.fc2.weight), rows, D, hid, dt, out=dh, pre=s.hpre)
-        # fc1
-        T.wgrad(dh, s.a2, hid, D, rows, G(blk.mlp.fc1.weight), dt, bias=G(blk.mlp.fc1.bias))
-        da2 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
-        T.dgrad_linear(dh, W.t(blk.mlp.fc1.weight), rows, hid, D, dt, out=da2)
-        # norm2 + residual
-        dmid = torch.empty((rows, D), dtype=torch.float32, device=self.device)
-        dmid_op = dmid if f32 else self._e(rows, D)
-        T.layernorm_bwd(s.xmid, blk.norm2.weight, da2, dmid, rows, D, blk.norm2.eps, G(blk.norm2.weight),
-                        G(blk.norm2.bias), dres=dres, dxop=None if f32 else dmid_op, dres_colsum=G(blk.mlp.fc2.bias))
-        # proj
-        T.wgrad(dmid_op, s.att, D, D, rows, G(blk.attn.proj.weight), dt)  # proj.bias: folded into norm1's backward
-        datt = self._e(rows, D)
-        T.dgrad_linear(dmid_op, W.t(blk.attn.proj.weight), rows, D, D, dt, out=datt)
-        # attention core
-        dqkv = self._e(rows, 3 * D)
-        T.mha_bwd(s.qkv, s.att, datt, s.lse, dqkv, B, Tn, H, D // H, blk.attn.scale, dt)
-        # qkv
-        T.wgrad(dqkv, s.a1, 3 * D, D, rows, G(blk.attn.qkv.weight), dt,
-                bias=G(blk.attn.qkv.bias) if blk.attn.qkv.bias is not None else None)
-        da1 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
-        T.dgrad_linear(dqkv, W.t(blk.attn.qkv.weight), rows, 3 * D, D, dt, out=da1)
-        # norm1 + residual
-        dx = torch.empty((rows, D), dtype=torch.float32, device=self.device)
-        dx_op = dx if f32 else self._e(rows, D)
-        T.layernorm_bwd(s.x, blk.norm1.weight, da1, dx, rows, D, blk.norm1.eps, G(blk.norm1.weight),
-                        G(blk.norm1.bias), dres=dmid, dxop=None if f32 else dx_op, dres_colsum=G(blk.attn.proj.bias))
-        return dx, dx_op
 
     def _h_s_bwd(self, seq, saved, dout32, dZH):
         dt, W, G, B = self.dtype, self.w, self.grad, self.batch

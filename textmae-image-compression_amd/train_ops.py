@@ -213,6 +213,15 @@ def bpp_bwd(lik, gout, dlik, num_pixels):
     return dlik
 
 
+def mae_loss_bwd(pred, imgs, ids_restore, keep, patch, norm_pix, dloss, dpred, out, dtype):
+    """models_mae.forward_loss backward -> out [n*L, p*p*C] in `dtype` (dloss 1-element f32 or None; dpred the
+    incoming gradient of pred itself, f32, or None)"""
+    n, C, H, W = imgs.shape
+    _lib.call("tmae_mae_loss_bwd", pred.data_ptr(), imgs.data_ptr(), ids_restore.data_ptr(), n, C, H, W, patch, keep,
+              int(bool(norm_pix)), _p(dloss), _p(dpred), out.data_ptr(), dtype_code(dtype), _stream())
+    return out
+
+
 def patchify(imgs, out, patch, dtype):
     n, C, H, W = imgs.shape
     _lib.call("tmae_patchify", imgs.data_ptr(), out.data_ptr(), n, C, H, W, patch, dtype_code(dtype), _stream())
