@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--no-distortion", dest="distortion_line", action="store_false",
                     help="skip the forward_loss (SSIM + L1 + VGG) line")
     ap.add_argument("--no-k64", dest="k64_line", action="store_false", help="skip the K=64 (config 2') line")
+    ap.add_argument("--no-mae-train", dest="mae_train_line", action="store_false",
+                    help="skip the MaskedAutoencoderViT training line")
     ap.add_argument("--kernel-reps", type=int, default=0, help="unused (kept for older command lines)")
     ap.add_argument("--backend", default="nccl", help="process-group backend (nccl = RCCL; gloo for a one-GPU rehearsal)")
     return ap.parse_args()
@@ -218,6 +220,10 @@ class LaunchTimer:
             return "lic_stack", fl
         if name == "tmae_patch_embed_fwd":
             return "patch_embed", 2.0 * a[6] * a[13] * a[11] * a[7] * a[10] * a[10]
+        if name == "tmae_patch_embed_gathered":  # (patches, ids, w, b, pos, tok, n, Kw, D, L, keep, ...)
+            return "patch_embed", 2.0 * a[6] * a[10] * a[8] * a[7]
+        if name == "tmae_patch_gather":  # the kept-patch gather in front of it (time only)
+            return "patch_embed", 0.0
         if name == "tmae_decoder_embed_fwd":
             return "dec_embed", 2.0 * a[7] * a[8] * a[10] * a[11]
         if name in ("tmae_decoder_pred_fwd", "tmae_decoder_pred_cp_fwd"):
@@ -797,6 +803,49 @@ def mae_large_line(args, dev, world, rank, barrier, dtype):
             "step_mfma_frac": round(v * gf * 1e9 / (world * PEAK_BF16), 4)}
 
 
+def mae_train_line(args, dev, world, rank, barrier, dtype):
+    """MaskedAutoencoderViT training step (models_mae.py:216-220 under autograd; mae_train.py): forward with the
+    activations kept, masked-MSE loss, HIP backward of the whole model, FusedAdam; mae_vit_base_patch16_dec512d8b,
+    batch 64, 224^2, mask_ratio 0.75, the step replayed as one HIP graph (engine.GraphedMAEStep); seeded
+    random-init weights and images"""
+    import textmae_amd
+    from textmae_amd import engine
+    from textmae_amd.optim import FusedAdam
+
+    torch.manual_seed(0)
+    m = textmae_amd.mae_vit_base_patch16_dec512d8b().to(dev).train()
+    m.compute_dtype = dtype
+    B, steps = 64, 10
+    imgs = torch.randn(B, 3, 224, 224, generator=torch.Generator().manual_seed(3000 + rank)).to(dev)
+    opt = FusedAdam([p for p in m.parameters() if p.requires_grad], lr=1.5e-4)
+    step = engine.GraphedMAEStep(m, opt, imgs, 0.75, warmup=2)  # fresh masking noise per replay
+    step(imgs)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss = step(imgs)
+    torch.cuda.synchronize()
+    barrier()
+    el = max_over_ranks(time.perf_counter() - t0, world, dev, args.backend)
+    L, keep, E, Dd = 196, 49, 768, 512
+    fl = 2 * keep * E * 768
+    fl += 12 * (2 * (keep + 1) * E * 12 * E + 4 * (keep + 1) ** 2 * E)
+    fl += 2 * (keep + 1) * E * Dd
+    fl += 8 * (2 * (L + 1) * Dd * 12 * Dd + 4 * (L + 1) ** 2 * Dd)
+    fl += 2 * L * Dd * 768
+    gf = 3 * fl / 1e9  # forward + the two backward GEMM passes
+    v = world * B * steps / el
+    out = {"workload": "MAE ViT-Base/16 dec512d8b training step (forward + masked MSE + HIP backward + FusedAdam), "
+                       "224^2, mask 0.75, HIP graph", "value": round(v, 2), "unit": "images/s", "batch": B,
+           "ms_per_step": round(el / steps * 1e3, 3), "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
+           "gflop_per_image": round(gf, 3), "step_mfma_frac": round(v * gf * 1e9 / (world * PEAK_BF16), 4),
+           "loss_last": round(float(loss), 6), "hip_graph": True}
+    del step, m, opt
+    torch.cuda.empty_cache()
+    return out
+
+
 def max_over_ranks(el, world, dev, backend):
     if world <= 1:
         return el
@@ -891,6 +940,11 @@ def main():
         progress("config 4 (MAE ViT-L, batch 128) line")
         mae_l = mae_large_line(args, dev, world, rank, barrier, dtype)
 
+    mae_t = None
+    if args.mae_train_line and vitb_default(args) and world == 1:
+        progress("MAE ViT-B training line")
+        mae_t = mae_train_line(args, dev, world, rank, barrier, dtype)
+
     dist_line = None
     if args.distortion_line and vitb_default(args):
         progress("forward_loss line")
@@ -927,6 +981,8 @@ def main():
         rec["forward_loss"] = dist_line
     if mae_l is not None:
         rec["config4_mae_large"] = mae_l
+    if mae_t is not None:
+        rec["mae_train"] = mae_t
     if train is not None:
         rec["train"] = train
     if rank == 0:

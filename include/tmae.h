@@ -70,6 +70,13 @@ int tmae_patch_embed_fwd(const float* imgs, const int64_t* ids_shuffle, const vo
                          const float* pos, float* tokens, int n, int C, int H, int W, int patch, int D, int L,
                          int keep, int dtype, void* stream);
 
+/* the same projection over kept patches gathered beforehand by tmae_patch_gather (patches [n*keep][Kw] in the
+ * operand dtype, Kw = C*P*P when P % 8 == 0): the LDS-DMA GEMM instead of the converting register path, same
+ * MFMA k-order (same tokens). */
+int tmae_patch_embed_gathered(const void* patches, const int64_t* ids_shuffle, const void* w, const float* bias,
+                              const float* pos, float* tokens, int n, int Kw, int D, int L, int keep, int dtype,
+                              void* stream);
+
 /* tokens[b][0] = cls_token + pos[0]  (MCM.py:624-626) */
 int tmae_cls_rows(float* tokens, const float* cls, const float* pos, int n, int rows_per_img, int D, void* stream);
 

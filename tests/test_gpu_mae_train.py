@@ -108,3 +108,31 @@ def test_bf16_bounded_and_adam_steps(tmae):
         opt.step()
         first = float(loss) if first is None else first
     assert float(loss) < 0.9 * first, (first, float(loss))
+
+
+def test_graphed_mae_step_bitwise(tmae):
+    """engine.GraphedMAEStep: replays equal eager steps (loss and weights, bitwise) with injected noise"""
+    from textmae_amd.engine import GraphedMAEStep
+    from textmae_amd.optim import FusedAdam
+
+    def make():
+        m = tiny(tmae, True, dec_dim=64)
+        m.compute_dtype = torch.bfloat16
+        return m, FusedAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
+
+    imgs = [torch.randn(4, 3, 64, 64, generator=torch.Generator().manual_seed(40 + i)).to(DEV) for i in range(4)]
+    noise = [torch.rand(4, 16, generator=torch.Generator().manual_seed(50 + i)).to(DEV) for i in range(4)]
+    m1, o1 = make()
+    eager = []
+    for x, nz in zip(imgs, noise):
+        o1.zero_grad()
+        loss, _, _ = m1(x, 0.75, noise=nz)
+        loss.backward()
+        o1.step()
+        eager.append(float(loss))
+    m2, o2 = make()
+    step = GraphedMAEStep(m2, o2, imgs[0], 0.75, warmup=1, noise=noise[0])  # the warm-up step is step 0
+    graphed = [eager[0]] + [float(step(x, noise=nz)) for x, nz in zip(imgs[1:], noise[1:])]
+    assert graphed == eager, (graphed, eager)
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(a, b), n

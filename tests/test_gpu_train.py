@@ -282,12 +282,15 @@ def test_mha_bwd(T, T_, H, dh, dt):
 
 
 # ------------------------------------------------------------------------------ distortion
-def test_distortion_fwd_bwd_vs_oracle():
+@pytest.mark.parametrize("hw", [(40, 37), (100, 150), (256, 256)])
+def test_distortion_fwd_bwd_vs_oracle(hw):
+    """one tile, several 32 x 64 tiles with ragged edges, the bench's 256^2 (tiled kernels, distortion.hip)"""
     from oracle.thirdparty import ssim as ssim_ref
     from textmae_amd.distortion import ssim_l1_loss
 
-    x = torch.rand(2, 3, 40, 37, generator=torch.Generator().manual_seed(30))
-    y = (x + 0.1 * _rnd(2, 3, 40, 37, seed=31)).clamp(0, 1)
+    H, W = hw
+    x = torch.rand(2, 3, H, W, generator=torch.Generator().manual_seed(30))
+    y = (x + 0.1 * _rnd(2, 3, H, W, seed=31)).clamp(0, 1)
     xr = x.double().requires_grad_(True)
     s_ref = 1 - ssim_ref(xr, y.double(), data_range=1)
     l_ref = F.l1_loss(xr, y.double())

@@ -105,6 +105,7 @@ SIGNATURES = {
     "tmae_linear_fwd": [P, I, I, I, I, I, P, P, P, I, I, P, I, I, I, I, I, I, P],
     "tmae_linear_residual_fwd": [P, I, P, P, P, I, I, I, I, I, P],
     "tmae_patch_embed_fwd": [P, P, P, P, P, P, I, I, I, I, I, I, I, I, I, P],
+    "tmae_patch_embed_gathered": [P, P, P, P, P, P, I, I, I, I, I, I, P],
     "tmae_cls_rows": [P, P, P, I, I, I, P],
     "tmae_mha_fwd": [P, P, I, I, I, I, F, I, P],
     "tmae_qkv_attn_fwd": [P, P, P, P, I, I, I, I, F, I, P],

@@ -2,10 +2,11 @@
 // 11-tap gaussian window, sigma 1.5, "valid" separable filtering, K = (0.01, 0.03), data range 1,
 // mean over every channel map) and L1, forward and backward, over NCHW f32 planes.
 //
-// forward:  hpass  (x, y, x^2, y^2, xy filtered along W)           -> 5 maps [P][H][Wo]
-//           vpass  (filtered along H; per output pixel S and dS/d{mu_x, E[x^2], E[xy]}) -> 3 maps [P][Ho][Wo]
-//                  + fixed-grid f64 partial sums of S and |x - y|
-// backward: the transposed filters of the 3 derivative maps (H then W), combined with x and y:
+// forward:  per 32 x 64 output tile, x and y through LDS: filtered along W (x, y, x^2, y^2, xy), then along H;
+//           per output pixel S and dS/d{mu_x, E[x^2], E[xy]} -> 3 maps [P][Ho][Wo]; f64 partial sums of S per
+//           tile and of |x - y| over a fixed grid
+// backward: per 32 x 64 input tile, the transposed filters of the 3 derivative maps (H then W) through LDS,
+//           combined with x and y:
 //           dL/dx = -g_ssim / N_out * (G^T D1 + 2 x G^T D2 + y G^T D3) + g_l1 * sign(x - y) / N_in
 #include "common.h"
 
@@ -26,59 +27,72 @@ static SsimWin ssim_window(float sigma) {
   return w;
 }
 
-__global__ void __launch_bounds__(256)
-ssim_hpass_kernel(const float* __restrict__ x, const float* __restrict__ y, float* __restrict__ h, int P, int H, int W,
-                  SsimWin win) {
-  const int Wo = W - (SS_WIN - 1);
-  const long long plane = (long long)H * Wo;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)P * plane) return;
-  const int p = (int)(i / plane);
-  const int rem = (int)(i - (long long)p * plane);
-  const int r = rem / Wo, c = rem - r * Wo;
-  const float* xr = x + ((size_t)p * H + r) * W + c;
-  const float* yr = y + ((size_t)p * H + r) * W + c;
-  float a = 0.f, b = 0.f, aa = 0.f, bb = 0.f, ab = 0.f;
-#pragma unroll
-  for (int t = 0; t < SS_WIN; ++t) {
-    const float xv = xr[t], yv = yr[t], g = win.g[t];
-    a += g * xv;
-    b += g * yv;
-    aa += g * xv * xv;
-    bb += g * yv * yv;
-    ab += g * xv * yv;
-  }
-  const long long n = (long long)P * plane;
-  h[i] = a;
-  h[n + i] = b;
-  h[2 * n + i] = aa;
-  h[3 * n + i] = bb;
-  h[4 * n + i] = ab;
-}
+// ---- forward, one workgroup per (plane, 32 x 64 output tile): the (32 + 10) x (64 + 10) x / y patch goes to LDS,
+// the horizontal pass writes the 5 filtered maps of its 42 rows to LDS, the vertical pass forms S and the three
+// derivative maps per output pixel.  Per-pixel arithmetic is the separable filter in tap order (h then v);
+// S is summed per workgroup in f64 into one partial per tile (fixed grid, folded in index order).
+#define SS_TH 32
+#define SS_TW 64
+#define SS_IH (SS_TH + SS_WIN - 1)
+#define SS_IW (SS_TW + SS_WIN - 1)
 
 __global__ void __launch_bounds__(256)
-ssim_vpass_kernel(const float* __restrict__ h, float* __restrict__ d, int P, int H, int W, SsimWin win, float c1,
-                  float c2, double* __restrict__ part, long long total) {
-  __shared__ double red[256];
+ssim_fwd_tile_kernel(const float* __restrict__ x, const float* __restrict__ y, float* __restrict__ d, int P, int H,
+                     int W, SsimWin win, float c1, float c2, double* __restrict__ part) {
+  __shared__ float xs[SS_IH][SS_IW], ys[SS_IH][SS_IW];
+  __shared__ float hm[5][SS_IH][SS_TW];
+  __shared__ double red[4];
   const int Wo = W - (SS_WIN - 1), Ho = H - (SS_WIN - 1);
-  const long long hplane = (long long)H * Wo, oplane = (long long)Ho * Wo;
-  const long long nh = (long long)P * hplane, no = (long long)P * oplane;
+  const int tx = (Wo + SS_TW - 1) / SS_TW, ty = (Ho + SS_TH - 1) / SS_TH;
+  const int t = threadIdx.x;
+  int b = blockIdx.x;
+  const int p = b / (tx * ty);
+  b -= p * tx * ty;
+  const int r0 = (b / tx) * SS_TH, c0 = (b % tx) * SS_TW;
+  const float* xp = x + (size_t)p * H * W;
+  const float* yp = y + (size_t)p * H * W;
+  for (int e = t; e < SS_IH * SS_IW; e += 256) {
+    const int rr = e / SS_IW, cc = e - rr * SS_IW;
+    const int r = r0 + rr, c = c0 + cc;
+    const bool in = r < H && c < W;
+    xs[rr][cc] = in ? xp[(size_t)r * W + c] : 0.0f;
+    ys[rr][cc] = in ? yp[(size_t)r * W + c] : 0.0f;
+  }
+  __syncthreads();
+  for (int e = t; e < SS_IH * SS_TW; e += 256) {
+    const int rr = e / SS_TW, cc = e - rr * SS_TW;
+    float a = 0.f, bb_ = 0.f, aa = 0.f, bb = 0.f, ab = 0.f;
+#pragma unroll
+    for (int k = 0; k < SS_WIN; ++k) {
+      const float xv = xs[rr][cc + k], yv = ys[rr][cc + k], g = win.g[k];
+      a += g * xv;
+      bb_ += g * yv;
+      aa += g * xv * xv;
+      bb += g * yv * yv;
+      ab += g * xv * yv;
+    }
+    hm[0][rr][cc] = a;
+    hm[1][rr][cc] = bb_;
+    hm[2][rr][cc] = aa;
+    hm[3][rr][cc] = bb;
+    hm[4][rr][cc] = ab;
+  }
+  __syncthreads();
+  const long long no = (long long)P * Ho * Wo;
   double acc = 0.0;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const int p = (int)(i / oplane);
-    const int rem = (int)(i - (long long)p * oplane);
-    const int r = rem / Wo, c = rem - r * Wo;
-    const float* hb = h + (size_t)p * hplane + (size_t)r * Wo + c;
+  for (int e = t; e < SS_TH * SS_TW; e += 256) {
+    const int rr = e / SS_TW, cc = e - rr * SS_TW;
+    const int r = r0 + rr, c = c0 + cc;
+    if (r >= Ho || c >= Wo) continue;
     float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
 #pragma unroll
-    for (int t = 0; t < SS_WIN; ++t) {
-      const float g = win.g[t];
-      const size_t o = (size_t)t * Wo;
-      m1 += g * hb[o];
-      m2 += g * hb[nh + o];
-      e11 += g * hb[2 * nh + o];
-      e22 += g * hb[3 * nh + o];
-      e12 += g * hb[4 * nh + o];
+    for (int k = 0; k < SS_WIN; ++k) {
+      const float g = win.g[k];
+      m1 += g * hm[0][rr + k][cc];
+      m2 += g * hm[1][rr + k][cc];
+      e11 += g * hm[2][rr + k][cc];
+      e22 += g * hm[3][rr + k][cc];
+      e12 += g * hm[4][rr + k][cc];
     }
     const float s11 = e11 - m1 * m1, s22 = e22 - m2 * m2, s12 = e12 - m1 * m2;
     const float A1 = 2.f * m1 * m2 + c1, B1 = m1 * m1 + m2 * m2 + c1;
@@ -86,6 +100,7 @@ ssim_vpass_kernel(const float* __restrict__ h, float* __restrict__ d, int P, int
     const float l = A1 / B1, cs = A2 / B2;
     acc += (double)(l * cs);
     if (d) {
+      const long long i = ((long long)p * Ho + r) * Wo + c;
       const float dl = (2.f * m2 * B1 - A1 * 2.f * m1) / (B1 * B1);
       const float dcs = (-2.f * m2 * B2 + A2 * 2.f * m1) / (B2 * B2);
       d[i] = dl * cs + l * dcs;             // dS / d mu_x
@@ -93,20 +108,23 @@ ssim_vpass_kernel(const float* __restrict__ h, float* __restrict__ d, int P, int
       d[2 * no + i] = l * 2.f / B2;         // dS / d E[xy]
     }
   }
-  red[threadIdx.x] = acc;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((t & 63) == 0) red[t >> 6] = acc;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+  if (t == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 __global__ void __launch_bounds__(256)
 l1_partial_kernel(const float* __restrict__ x, const float* __restrict__ y, long long n, double* __restrict__ part) {
   __shared__ double red[256];
   double s = 0.0;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+  const long long n4 = ((((size_t)x | (size_t)y) & 15) == 0) ? n / 4 : 0;  // 16-B loads over the aligned body
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const f32x4 a = *reinterpret_cast<const f32x4*>(x + 4 * i), b = *reinterpret_cast<const f32x4*>(y + 4 * i);
+    s += (double)(fabsf(a[0] - b[0]) + fabsf(a[1] - b[1])) + (double)(fabsf(a[2] - b[2]) + fabsf(a[3] - b[3]));
+  }
+  for (long long i = 4 * n4 + (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
     s += (double)fabsf(x[i] - y[i]);
   red[threadIdx.x] = s;
   __syncthreads();
@@ -119,14 +137,12 @@ l1_partial_kernel(const float* __restrict__ x, const float* __restrict__ y, long
 
 // out[0] = 1 - mean S, out[1] = mean |x - y|
 __global__ void __launch_bounds__(256)
-distortion_final_kernel(const double* __restrict__ ps, const double* __restrict__ pl, int np, double n_out, double n_in,
-                        float* __restrict__ out) {
+distortion_final_kernel(const double* __restrict__ ps, int nps, const double* __restrict__ pl, int npl, double n_out,
+                        double n_in, float* __restrict__ out) {
   __shared__ double r1[256], r2[256];
   double a = 0.0, b = 0.0;
-  for (int i = threadIdx.x; i < np; i += 256) {
-    a += ps[i];
-    b += pl[i];
-  }
+  for (int i = threadIdx.x; i < nps; i += 256) a += ps[i];
+  for (int i = threadIdx.x; i < npl; i += 256) b += pl[i];
   r1[threadIdx.x] = a;
   r2[threadIdx.x] = b;
   __syncthreads();
@@ -143,91 +159,109 @@ distortion_final_kernel(const double* __restrict__ ps, const double* __restrict_
   }
 }
 
+static inline int ssim_tiles(int P, int Ho, int Wo) {
+  return P * ((Ho + SS_TH - 1) / SS_TH) * ((Wo + SS_TW - 1) / SS_TW);
+}
+
 extern "C" int tmae_distortion_fwd(const float* x, const float* y, int P, int H, int W, float* hwork, float* dmaps,
                                    double* part, float* out, void* stream) {
   TMAE_REQUIRE(x && y && hwork && part && out && H >= SS_WIN && W >= SS_WIN, "tmae_distortion_fwd: bad arguments");
   hipStream_t st = (hipStream_t)stream;
   const SsimWin win = ssim_window(1.5f);
   const int Wo = W - (SS_WIN - 1), Ho = H - (SS_WIN - 1);
-  const long long nh = (long long)P * H * Wo, no = (long long)P * Ho * Wo, ni = (long long)P * H * W;
-  hipLaunchKernelGGL(ssim_hpass_kernel, dim3((unsigned)((nh + 255) / 256)), dim3(256), 0, st, x, y, hwork, P, H, W, win);
-  hipLaunchKernelGGL(ssim_vpass_kernel, dim3(SS_BLOCKS), dim3(256), 0, st, hwork, dmaps, P, H, W, win, 0.01f * 0.01f,
-                     0.03f * 0.03f, part, no);
+  const long long no = (long long)P * Ho * Wo, ni = (long long)P * H * W;
+  TMAE_REQUIRE(no < (1ll << 31) && ni < (1ll << 31), "tmae_distortion_fwd: %lld pixels exceed the 32-bit index range",
+               ni);
+  // one f64 partial per tile, kept in the caller's hwork (>= 5 P H (W - 10) floats, far more than the tiles)
+  const int nt = ssim_tiles(P, Ho, Wo);
+  TMAE_REQUIRE(2ll * nt <= 5ll * P * H * Wo, "tmae_distortion_fwd: workspace");
+  double* tpart = reinterpret_cast<double*>(hwork);
+  hipLaunchKernelGGL(ssim_fwd_tile_kernel, dim3((unsigned)nt), dim3(256), 0, st, x, y, dmaps, P, H, W, win,
+                     0.01f * 0.01f, 0.03f * 0.03f, tpart);
   hipLaunchKernelGGL(l1_partial_kernel, dim3(SS_BLOCKS), dim3(256), 0, st, x, y, ni, part + SS_BLOCKS);
-  hipLaunchKernelGGL(distortion_final_kernel, dim3(1), dim3(256), 0, st, part, part + SS_BLOCKS, SS_BLOCKS, (double)no,
-                     (double)ni, out);
+  hipLaunchKernelGGL(distortion_final_kernel, dim3(1), dim3(256), 0, st, tpart, nt, part + SS_BLOCKS, SS_BLOCKS,
+                     (double)no, (double)ni, out);
   TMAE_LAUNCH_CHECK("tmae_distortion_fwd");
 }
 
-// transposed vertical filter of the 3 derivative maps: v[k][p][r][c] = sum_t g[t] d[k][p][r - t][c], r in [0, H)
+// ---- backward, one workgroup per (plane, 32 x 64 INPUT tile): the three derivative maps over the rows and
+// columns the tile's transposed filters reach ((32 + 10) x (64 + 10), zero outside the valid output) go to LDS;
+// the transposed vertical filter v[k][r][c'] = sum_t g[t] d[k][r - t][c'] for the tile's rows and columns
+// c0 - 10 .. c0 + 63 to LDS; then gx[r][c] = -g_ssim / N_out (G^T D1 + 2 x G^T D2 + y G^T D3) + g_l1 sign(x - y) / N_in
+// with the transposed horizontal filter.  Taps outside the valid output add g * 0.
 __global__ void __launch_bounds__(256)
-ssim_bwd_vpass_kernel(const float* __restrict__ d, float* __restrict__ v, int P, int H, int W, SsimWin win) {
+ssim_bwd_tile_kernel(const float* __restrict__ d, const float* __restrict__ x, const float* __restrict__ y,
+                     float* __restrict__ gx, int P, int H, int W, SsimWin win, const float* __restrict__ gout,
+                     float inv_out, float inv_in) {
+  __shared__ float ds[3][SS_IH][SS_IW];
+  __shared__ float vs[3][SS_TH][SS_IW];
   const int Wo = W - (SS_WIN - 1), Ho = H - (SS_WIN - 1);
-  const long long vplane = (long long)H * Wo, oplane = (long long)Ho * Wo;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)P * vplane) return;
-  const int p = (int)(i / vplane);
-  const int rem = (int)(i - (long long)p * vplane);
-  const int r = rem / Wo, c = rem - r * Wo;
-  const long long no = (long long)P * oplane, nv = (long long)P * vplane;
-  float a = 0.f, b = 0.f, e = 0.f;
+  const int tx = (W + SS_TW - 1) / SS_TW, ty = (H + SS_TH - 1) / SS_TH;
+  const int t = threadIdx.x;
+  int b = blockIdx.x;
+  const int p = b / (tx * ty);
+  b -= p * tx * ty;
+  const int r0 = (b / tx) * SS_TH, c0 = (b % tx) * SS_TW;
+  const long long no = (long long)P * Ho * Wo;
+  const float* dp = d + (size_t)p * Ho * Wo;
+  // ds[k][i][j] = d[k][r0 - 10 + i][c0 - 10 + j]
+  for (int e = t; e < SS_IH * SS_IW; e += 256) {
+    const int i = e / SS_IW, j = e - i * SS_IW;
+    const int r = r0 - (SS_WIN - 1) + i, c = c0 - (SS_WIN - 1) + j;
+    const bool in = r >= 0 && r < Ho && c >= 0 && c < Wo;
+    const size_t o = (size_t)r * Wo + c;
 #pragma unroll
-  for (int t = 0; t < SS_WIN; ++t) {
-    const int rr = r - t;
-    if (rr >= 0 && rr < Ho) {
-      const size_t o = (size_t)p * oplane + (size_t)rr * Wo + c;
-      const float g = win.g[t];
-      a += g * d[o];
-      b += g * d[no + o];
-      e += g * d[2 * no + o];
-    }
+    for (int k = 0; k < 3; ++k) ds[k][i][j] = in ? dp[k * no + o] : 0.0f;
   }
-  v[i] = a;
-  v[nv + i] = b;
-  v[2 * nv + i] = e;
-}
-
-__global__ void __launch_bounds__(256)
-ssim_bwd_hpass_kernel(const float* __restrict__ v, const float* __restrict__ x, const float* __restrict__ y,
-                      float* __restrict__ gx, int P, int H, int W, SsimWin win, const float* __restrict__ gout,
-                      float inv_out, float inv_in) {
-  const int Wo = W - (SS_WIN - 1);
-  const long long iplane = (long long)H * W, vplane = (long long)H * Wo;
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)P * iplane) return;
-  const int p = (int)(i / iplane);
-  const int rem = (int)(i - (long long)p * iplane);
-  const int r = rem / W, c = rem - r * W;
-  const long long nv = (long long)P * vplane;
-  float a = 0.f, b = 0.f, e = 0.f;
+  __syncthreads();
+  // vs[k][i][j] = v[k][r0 + i][c0 - 10 + j] = sum_t g[t] d[k][r0 + i - t][...] = sum_t g[t] ds[k][i + 10 - t][j]
+  for (int e = t; e < SS_TH * SS_IW; e += 256) {
+    const int i = e / SS_IW, j = e - i * SS_IW;
+    float a = 0.f, bq = 0.f, q = 0.f;
 #pragma unroll
-  for (int t = 0; t < SS_WIN; ++t) {
-    const int cc = c - t;
-    if (cc >= 0 && cc < Wo) {
-      const size_t o = (size_t)p * vplane + (size_t)r * Wo + cc;
-      const float g = win.g[t];
-      a += g * v[o];
-      b += g * v[nv + o];
-      e += g * v[2 * nv + o];
+    for (int k = 0; k < SS_WIN; ++k) {
+      const float g = win.g[k];
+      a += g * ds[0][i + SS_WIN - 1 - k][j];
+      bq += g * ds[1][i + SS_WIN - 1 - k][j];
+      q += g * ds[2][i + SS_WIN - 1 - k][j];
     }
+    vs[0][i][j] = a;
+    vs[1][i][j] = bq;
+    vs[2][i][j] = q;
   }
-  const float xv = x[i], yv = y[i];
+  __syncthreads();
   const float gs = gout ? gout[0] : 0.0f, gl = gout ? gout[1] : 0.0f;
-  const float diff = xv - yv;
-  const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
-  gx[i] = -gs * inv_out * (a + 2.f * xv * b + yv * e) + gl * inv_in * sg;
+  for (int e = t; e < SS_TH * SS_TW; e += 256) {
+    const int i = e / SS_TW, j = e - i * SS_TW;
+    const int r = r0 + i, c = c0 + j;
+    if (r >= H || c >= W) continue;
+    float a = 0.f, bq = 0.f, q = 0.f;
+#pragma unroll
+    for (int k = 0; k < SS_WIN; ++k) {  // v column c - k = vs column j + 10 - k
+      const float g = win.g[k];
+      a += g * vs[0][i][j + SS_WIN - 1 - k];
+      bq += g * vs[1][i][j + SS_WIN - 1 - k];
+      q += g * vs[2][i][j + SS_WIN - 1 - k];
+    }
+    const size_t o = ((size_t)p * H + r) * W + c;
+    const float xv = x[o], yv = y[o];
+    const float diff = xv - yv;
+    const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+    gx[o] = -gs * inv_out * (a + 2.f * xv * bq + yv * q) + gl * inv_in * sg;
+  }
 }
 
 extern "C" int tmae_distortion_bwd(const float* x, const float* y, int P, int H, int W, const float* dmaps, float* vwork,
                                    const float* gout, float* gx, void* stream) {
-  TMAE_REQUIRE(x && y && dmaps && vwork && gout && gx, "tmae_distortion_bwd: bad arguments");
+  TMAE_REQUIRE(x && y && dmaps && gout && gx && H >= SS_WIN && W >= SS_WIN, "tmae_distortion_bwd: bad arguments");
+  (void)vwork;  // the transposed vertical pass lives in LDS since round 4
   hipStream_t st = (hipStream_t)stream;
   const SsimWin win = ssim_window(1.5f);
   const int Wo = W - (SS_WIN - 1), Ho = H - (SS_WIN - 1);
-  const long long nv = (long long)P * H * Wo, ni = (long long)P * H * W;
-  hipLaunchKernelGGL(ssim_bwd_vpass_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, st, dmaps, vwork, P, H, W,
-                     win);
-  hipLaunchKernelGGL(ssim_bwd_hpass_kernel, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, st, vwork, x, y, gx, P, H,
-                     W, win, gout, (float)(1.0 / ((double)P * Ho * Wo)), (float)(1.0 / (double)ni));
+  const long long ni = (long long)P * H * W;
+  TMAE_REQUIRE(ni < (1ll << 31), "tmae_distortion_bwd: %lld pixels exceed the 32-bit index range", ni);
+  const int nt = P * ((H + SS_TH - 1) / SS_TH) * ((W + SS_TW - 1) / SS_TW);
+  hipLaunchKernelGGL(ssim_bwd_tile_kernel, dim3((unsigned)nt), dim3(256), 0, st, dmaps, x, y, gx, P, H, W, win, gout,
+                     (float)(1.0 / ((double)P * Ho * Wo)), (float)(1.0 / (double)ni));
   TMAE_LAUNCH_CHECK("tmae_distortion_bwd");
 }

@@ -305,6 +305,25 @@ extern "C" int tmae_patch_embed_fwd(const float* imgs, const int64_t* ids_shuffl
   return patch_t<float>(imgs, ids_shuffle, w, bias, pos, tokens, n, C, H, W, patch, D, L, keep, (hipStream_t)stream);
 }
 
+// the same GEMM over patches gathered beforehand (tmae_patch_gather: [n*keep][Kw] in T): the LDS-DMA kernel
+// instead of the register-staged f32 -> T conversion on load; same MFMA k-order, so the same tokens
+template <typename T>
+static int patch_gathered_t(const void* patches, const int64_t* ids, const void* w, const float* bias, const float* pos,
+                            float* tok, int n, int Kw, int D, int L, int keep, hipStream_t st) {
+  TMAE_REQUIRE(check_k<T>(Kw) && D % 4 == 0, "tmae_patch_embed_gathered: K=%d / dim %d unsupported", Kw, D);
+  DenseSrc<T> xs{(const T*)patches, Kw, n * keep, Kw, 1 << 30, 0, 0, BStride{0, 0}};
+  return launch_gemm<true, T>("tmae_patch_embed_gathered", (const T*)w, 0, 0, D, Kw, xs,
+                              EpiPatchEmbed{tok, bias, pos, ids, L, keep, D}, n * keep, 1, 1, st);
+}
+
+extern "C" int tmae_patch_embed_gathered(const void* patches, const int64_t* ids_shuffle, const void* w,
+                                         const float* bias, const float* pos, float* tokens, int n, int Kw, int D,
+                                         int L, int keep, int dtype, void* stream) {
+  if (dtype == TMAE_BF16)
+    return patch_gathered_t<bf16>(patches, ids_shuffle, w, bias, pos, tokens, n, Kw, D, L, keep, (hipStream_t)stream);
+  return patch_gathered_t<float>(patches, ids_shuffle, w, bias, pos, tokens, n, Kw, D, L, keep, (hipStream_t)stream);
+}
+
 // ------------------------------------------------------------------ decoder embed / pred
 template <typename T>
 static int dec_embed_t(const void* x, int x_f32, const void* w, const float* bias, const float* pos,

@@ -1300,10 +1300,41 @@ patch_gather_kernel(const float* __restrict__ img, const int64_t* __restrict__ i
   out[i] = to_out<T>(img[(((size_t)b * C + c) * H + hy * P + py) * W + hx * P + px]);
 }
 
+// the same with 8 consecutive pixels of one patch row per thread (P % 8 == 0): two 16-B loads, one 16-B (bf16) or
+// two (f32) stores; one thread per (row, channel, patch row, 8-pixel group)
+template <typename T>
+__global__ void __launch_bounds__(256)
+patch_gather8_kernel(const float* __restrict__ img, const int64_t* __restrict__ ids, T* __restrict__ out, int n, int C,
+                     int H, int W, int P, int L, int keep) {
+  const int per_row = C * P * (P / 8);
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n * keep * per_row) return;
+  const int row = i / per_row, q = i - row * per_row;
+  const int b = row / keep, k = row - b * keep;
+  const int c = q / (P * (P / 8)), r2 = q - c * P * (P / 8);
+  const int py = r2 / (P / 8), px = (r2 - py * (P / 8)) * 8;
+  const int p = (int)ids[(size_t)b * L + k];
+  const int G = W / P;
+  const int hy = p / G, hx = p - hy * G;
+  const float* src = img + (((size_t)b * C + c) * H + hy * P + py) * W + hx * P + px;
+  const f32x4 lo = *reinterpret_cast<const f32x4*>(src), hi = *reinterpret_cast<const f32x4*>(src + 4);
+  store8(out + (size_t)row * C * P * P + (c * P + py) * P + px, lo, hi);
+}
+
 extern "C" int tmae_patch_gather(const float* imgs, const int64_t* ids_shuffle, void* out, int n, int C, int H, int W,
                                  int patch, int L, int keep, int dtype, void* stream) {
   const long long total = (long long)n * keep * C * patch * patch;
   if (total == 0) return TMAE_OK;
+  if (patch % 8 == 0 && W % 4 == 0 && ((size_t)imgs & 15) == 0 && total / 8 < (1ll << 31)) {
+    const dim3 g8((unsigned)((total / 8 + 255) / 256));
+    if (dtype == TMAE_BF16)
+      hipLaunchKernelGGL(patch_gather8_kernel<bf16>, g8, dim3(256), 0, (hipStream_t)stream, imgs, ids_shuffle,
+                         (bf16*)out, n, C, H, W, patch, L, keep);
+    else
+      hipLaunchKernelGGL(patch_gather8_kernel<float>, g8, dim3(256), 0, (hipStream_t)stream, imgs, ids_shuffle,
+                         (float*)out, n, C, H, W, patch, L, keep);
+    TMAE_LAUNCH_CHECK("tmae_patch_gather");
+  }
   const dim3 grid((unsigned)((total + 255) / 256));
   if (dtype == TMAE_BF16)
     hipLaunchKernelGGL(patch_gather_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, imgs, ids_shuffle, (bf16*)out,

@@ -15,7 +15,16 @@ from __future__ import annotations
 import torch
 
 from . import distributed
-from .optim import clip_grad_norm_
+from .optim import FusedAdam, clip_grad_norm_, clip_norm_deferred
+
+
+def _clip_buffer(optimizer):
+    """the persistent [norm, factor] f32 pair of this optimizer's deferred clip (allocated outside any capture)"""
+    buf = getattr(optimizer, "_clip_buf", None)
+    if buf is None:
+        dev = next(p.device for g in optimizer.param_groups for p in g["params"])
+        buf = optimizer._clip_buf = torch.empty(2, dtype=torch.float32, device=dev)
+    return buf
 
 METRICS = ("loss", "L1_loss", "ssim_loss", "vgg_loss", "bpp_loss", "aux_loss")
 
@@ -29,9 +38,20 @@ def train_step(model, criterion, samples, total_scores, optimizer, aux_optimizer
     aux_loss = model.aux_loss() / accum_iter
     if step_now:
         out_criterion["loss"].backward()
+        scale = None
         if clip_max_norm > 0:
-            clip_grad_norm_(model.parameters(), clip_max_norm)
-        optimizer.step()
+            if isinstance(optimizer, FusedAdam):
+                # the clip factor goes into the Adam update (g * s, the product the in-place scale would store):
+                # one pass over the 805 MB gradient buffer less; the gradients are zeroed below either way
+                buf = _clip_buffer(optimizer)
+                if clip_norm_deferred(model.parameters(), clip_max_norm, buf):
+                    scale = buf[1:]
+            else:
+                clip_grad_norm_(model.parameters(), clip_max_norm)
+        if scale is not None:
+            optimizer.step(grad_scale=scale)
+        else:
+            optimizer.step()
         aux_loss.backward()
         aux_optimizer.step()
         optimizer.zero_grad()
@@ -124,6 +144,68 @@ class GraphedTrainStep:
 
         bump_versions(self.params)
         return self.out
+
+
+class GraphedMAEStep:
+    """MaskedAutoencoderViT pre-training step (models_mae.py:216-220 under autograd + an optimizer step) captured
+    once into a HIP graph, replayed per batch: zero_grad, forward (masking noise from torch's graph-safe generator,
+    or a static noise tensor refreshed per call), masked-MSE loss, the HIP backward (mae_train.py) and the FusedAdam
+    update.  Same capture rules as GraphedTrainStep (device step counts, pinned launch tables, persistent gradient
+    buffer); a changed learning rate re-captures.  Returns the step's loss (a static device tensor)."""
+
+    def __init__(self, model, optimizer, imgs, mask_ratio=0.75, warmup=1, noise=None):
+        if not imgs.is_cuda:
+            raise ValueError("GraphedMAEStep needs device inputs")
+        self.model, self.optimizer, self.mask_ratio = model, optimizer, mask_ratio
+        self.imgs = imgs.detach().float().clone()
+        self.noise = noise.detach().float().clone() if noise is not None else None
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.graph, self.loss = None, None
+        self._capture(warmup)
+
+    def _hyper(self):
+        return tuple((g["lr"], tuple(g["betas"]), g["eps"], g["weight_decay"]) for g in self.optimizer.param_groups)
+
+    def _step(self):
+        self.optimizer.zero_grad()
+        loss, _, _ = self.model(self.imgs, self.mask_ratio, noise=self.noise)
+        loss.backward()
+        self.optimizer.step()
+        return loss.detach()
+
+    def _capture(self, warmup):
+        from .optim import bump_versions, reserve_capture_staging
+
+        self.graph, self.loss = None, None
+        cur = torch.cuda.current_stream(self.imgs.device)
+        side = torch.cuda.Stream(device=self.imgs.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self._step()
+        cur.wait_stream(side)
+        self.optimizer.zero_grad()
+        bump_versions(self.params)
+        reserve_capture_staging()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            loss = self._step()
+        self.graph, self.loss = g, loss
+        self._hyper_at_capture = self._hyper()
+
+    def __call__(self, imgs, noise=None):
+        if (noise is None) != (self.noise is None):
+            raise ValueError("GraphedMAEStep: noise must be given at every call iff it was given at capture")
+        if self._hyper() != self._hyper_at_capture:
+            self._capture(0)
+        self.imgs.copy_(imgs, non_blocking=True)
+        if noise is not None:
+            self.noise.copy_(noise, non_blocking=True)
+        self.graph.replay()
+        from .optim import bump_versions
+
+        bump_versions(self.params)
+        return self.loss
 
 
 def train_one_epoch(model, criterion, train_dataloader, optimizer, aux_optimizer, epoch, clip_max_norm=1.0,

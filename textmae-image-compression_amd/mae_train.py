@@ -70,9 +70,10 @@ class MAETrainExec(_VitTrainBase):
         pw = m.patch_embed.proj.weight
         pos = m.pos_embed.detach()
         tok = torch.empty((B * Te, E), dtype=torch.float32, device=self.device)
-        ops.patch_embed(imgs, shuf, W.nt(pw), m.patch_embed.proj.bias.detach(), pos, tok, keep, P, dt)
-        ops.cls_rows(tok, m.cls_token.detach(), pos, B, Te, E)
         self.patches = T.patch_gather(imgs, shuf, self._e(B * keep, pw[0].numel()), keep, P, dt)
+        ops.patch_embed(imgs, shuf, W.nt(pw), m.patch_embed.proj.bias.detach(), pos, tok, keep, P, dt,
+                        patches=self.patches)
+        ops.cls_rows(tok, m.cls_token.detach(), pos, B, Te, E)
         self.enc = []
         for blk in m.blocks:
             tok = self._block_fwd(blk, tok, B, Te)

@@ -364,10 +364,10 @@ class TrainExec(_VitTrainBase):
         self.shuf, self.rest = shuf, rest
         pos_e = m.encoder_pos_embed.detach()
         tok = torch.empty((B * Te, E), dtype=torch.float32, device=self.device)
-        ops.patch_embed(imgs, shuf, W.nt(m.encoder_embed.proj.weight), m.encoder_embed.proj.bias.detach(), pos_e, tok,
-                        K, P, dt)
-        ops.cls_rows(tok, m.cls_token.detach(), pos_e, B, Te, E)
         self.patches = T.patch_gather(imgs, shuf, self._e(B * K, m.encoder_embed.proj.weight[0].numel()), K, P, dt)
+        ops.patch_embed(imgs, shuf, W.nt(m.encoder_embed.proj.weight), m.encoder_embed.proj.bias.detach(), pos_e, tok,
+                        K, P, dt, patches=self.patches)
+        ops.cls_rows(tok, m.cls_token.detach(), pos_e, B, Te, E)
         self.enc = []
         for blk in m.encoder_blocks:
             tok = self._block_fwd(blk, tok, B, Te)

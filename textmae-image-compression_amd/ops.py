@@ -112,12 +112,31 @@ def linear_residual(x, w, b, resid, dtype):
     return resid
 
 
-def patch_embed(imgs, ids_shuffle, w, b, pos, tokens, keep, patch, dtype):
+_PATCH_WORK: dict = {}
+
+
+def patch_embed(imgs, ids_shuffle, w, b, pos, tokens, keep, patch, dtype, patches=None):
+    """kept-patch embedding (+ pos) into tokens rows 1..keep of every image.  Patches whose rows are whole 16-B
+    chunks (P % 8 == 0) are gathered first (into `patches` [n*keep][C*P*P] of dtype when given -- the training
+    forward keeps them for the weight gradient -- else a cached workspace) and projected by the LDS-DMA GEMM;
+    others (ViT-H's patch 14) are gathered value by value inside the GEMM."""
     n, C, H, W = imgs.shape
     D = w.shape[0]
     L = ids_shuffle.shape[1]
     if w.dim() != 2 or w.shape[1] != -(-C * patch * patch // 8) * 8 or not w.is_contiguous():
         raise ValueError(f"patch_embed: weight {tuple(w.shape)} must be contiguous [D][C*P*P rounded up to 8]")
+    KP = C * patch * patch
+    if patch % 8 == 0:
+        if patches is None:
+            key = (imgs.device, dtype, n * keep * KP)
+            patches = _PATCH_WORK.get(key)
+            if patches is None:
+                patches = _PATCH_WORK[key] = torch.empty((n * keep, KP), dtype=dtype, device=imgs.device)
+            _lib.call("tmae_patch_gather", _need(imgs, torch.float32, "imgs").data_ptr(), ids_shuffle.data_ptr(),
+                      patches.data_ptr(), n, C, H, W, patch, L, keep, dtype_code(dtype), _stream())
+        _lib.call("tmae_patch_embed_gathered", patches.data_ptr(), ids_shuffle.data_ptr(), w.data_ptr(), b.data_ptr(),
+                  pos.data_ptr(), tokens.data_ptr(), n, KP, D, L, keep, dtype_code(dtype), _stream())
+        return tokens
     _lib.call("tmae_patch_embed_fwd", _need(imgs, torch.float32, "imgs").data_ptr(), ids_shuffle.data_ptr(),
               w.data_ptr(), b.data_ptr(), pos.data_ptr(), tokens.data_ptr(), n, C, H, W, patch, D, L, keep,
               dtype_code(dtype), _stream())

@@ -131,7 +131,9 @@ class FusedAdam(torch.optim.Optimizer):
         return tab, chunk
 
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, grad_scale=None):
+        """grad_scale: optional 1-element f32 device tensor every gradient is multiplied by inside the update
+        (clip_grad_norm_'s factor left unapplied by clip_norm_deferred; the same f32 product scale_ would store)"""
         loss = None
         if closure is not None:
             with torch.enable_grad():
@@ -146,7 +148,8 @@ class FusedAdam(torch.optim.Optimizer):
             tab, nchunks = self._table(gi, live)
             b1, b2 = group["betas"]
             _lib.call("tmae_adam_multi", tab.data_ptr(), len(live), nchunks, float(group["lr"]), float(b1), float(b2),
-                      float(group["eps"]), float(group["weight_decay"]), None, torch.cuda.current_stream().cuda_stream)
+                      float(group["eps"]), float(group["weight_decay"]),
+                      None if grad_scale is None else grad_scale.data_ptr(), torch.cuda.current_stream().cuda_stream)
             bump_versions(live)
         return loss
 
@@ -223,6 +226,22 @@ def clip_grad_norm_(parameters, max_norm, out=None):
     T.grad_norm(flat, max_norm, res)
     T.scale_(flat, res[1:])
     return res[0]
+
+
+def clip_norm_deferred(parameters, max_norm, out):
+    """clip_grad_norm_ with the scaling left to the optimizer: when every gradient lives in one flat buffer, writes
+    out[0] = total norm, out[1] = min(1, max_norm / (norm + 1e-6)) and returns True without touching the gradients
+    (pass out[1:] to FusedAdam.step(grad_scale=...)); otherwise clips in place like clip_grad_norm_ and returns
+    False."""
+    params = [p for p in parameters if p.grad is not None]
+    if not params:
+        return False
+    flat = _flat_owner(params)
+    if flat is None:
+        torch.nn.utils.clip_grad_norm_(params, max_norm)
+        return False
+    T.grad_norm(flat, max_norm, out)
+    return True
 
 
 def configure_optimizers(model, lr=1e-4, aux_lr=1e-4, fused=True):

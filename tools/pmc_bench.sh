@@ -10,7 +10,7 @@ tag=$1; fam=$2
 for c in FETCH_SIZE WRITE_SIZE; do
   rm -rf "gpurun_out/pmc_${tag}_$c"
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $c -f csv -d "gpurun_out/pmc_${tag}_$c" -o p -- \
-    python3 bench.py --no-graph --no-roofline --no-distortion --steps 2 --warmup 1 --no-cpu-baseline --no-train --no-k64 > /dev/null
+    python3 bench.py --no-graph --no-roofline --no-distortion --steps 2 --warmup 1 --no-cpu-baseline --no-train --no-k64 --no-mae-train > /dev/null
 done
 python3 tools/pmc_family.py "$(find gpurun_out/pmc_${tag}_FETCH_SIZE -name '*counter_collection.csv' | head -1)" \
   "$(find gpurun_out/pmc_${tag}_WRITE_SIZE -name '*counter_collection.csv' | head -1)" "$fam" \

@@ -14,8 +14,8 @@ tools/gpu_session.sh \
   "${tag}_trace:400:tools/trace_bench.sh $tag" \
   "${tag}_pmc:600:tools/pmc_bench.sh $tag lic_stack" \
   "${tag}_cfg4:400:python bench.py --enc-dim 1024 --enc-depth 24 --enc-heads 16 --batch 128 --no-cpu-baseline --no-train --no-k64 --no-distortion" \
-  "${tag}_maelarge:300:python bench.py --mae-large --no-cpu-baseline --no-train --no-k64 --no-distortion --no-roofline" \
-  "${tag}_proftrain:400:rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/${tag}_ptrain -o t -- python3 bench.py --no-cpu-baseline --no-k64 --no-roofline --no-distortion --no-dp-rehearsal --steps 3 --warmup 1" || exit $?
+  "${tag}_maelarge:300:python bench.py --mae-large --no-cpu-baseline --no-train --no-k64 --no-distortion --no-roofline --no-mae-train" \
+  "${tag}_proftrain:400:rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/${tag}_ptrain -o t -- python3 bench.py --no-cpu-baseline --no-k64 --no-roofline --no-distortion --no-dp-rehearsal --no-mae-train --steps 3 --warmup 1" || exit $?
 cp "$(find gpurun_out/${tag}_ptrain -name '*kernel_stats.csv' | head -1)" "gpurun_out/${tag}_train_kernel_stats.csv"
 kt=$(find "gpurun_out/trace_${tag}" -name '*kernel_trace.csv' | head -1)
 python3 tools/fwd_trace.py "$kt" > "gpurun_out/${tag}_fwd_timeline.txt"

@@ -9,7 +9,7 @@ tag=$1; shift
 out=gpurun_out/trace_$tag
 rm -rf "$out"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$out" -o bench -- \
-  python3 bench.py --no-cpu-baseline --no-train --no-k64 --no-distortion "$@" > "gpurun_out/trace_${tag}_bench.json"
+  python3 bench.py --no-cpu-baseline --no-train --no-k64 --no-distortion --no-mae-train "$@" > "gpurun_out/trace_${tag}_bench.json"
 kt=$(find "$out" -name '*kernel_trace.csv' | head -1)
 ks=$(find "$out" -name '*kernel_stats.csv' | head -1)
 python3 tools/family_summary.py "$kt" --both --json "gpurun_out/trace_families_${tag}.json" > /dev/null
