@@ -33,15 +33,20 @@ static SsimWin ssim_window(float sigma) {
 // S is summed per workgroup in f64 into one partial per tile (fixed grid, folded in index order).
 #define SS_TH 32
 #define SS_TW 64
+#ifndef SS_NT
+#define SS_NT 512  // threads per tile workgroup: 8 waves, two workgroups (78.6 / 65.7 KB of LDS) per CU
+#endif
 #define SS_IH (SS_TH + SS_WIN - 1)
 #define SS_IW (SS_TW + SS_WIN - 1)
+#define SS_VR 4  // output rows per vertical-pass item (register blocking of the filtered rows)
+#define SS_IWP 76  // x / y patch row pitch: 74 columns padded to whole 16-B chunks (the h pass reads 4 at a time)
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(SS_NT)
 ssim_fwd_tile_kernel(const float* __restrict__ x, const float* __restrict__ y, float* __restrict__ d, int P, int H,
                      int W, SsimWin win, float c1, float c2, double* __restrict__ part) {
-  __shared__ float xs[SS_IH][SS_IW], ys[SS_IH][SS_IW];
-  __shared__ float hm[5][SS_IH][SS_TW];
-  __shared__ double red[4];
+  __shared__ __attribute__((aligned(16))) float xs[SS_IH][SS_IWP], ys[SS_IH][SS_IWP];
+  __shared__ __attribute__((aligned(16))) float hm[5][SS_IH][SS_TW];
+  __shared__ double red[SS_NT / 64];
   const int Wo = W - (SS_WIN - 1), Ho = H - (SS_WIN - 1);
   const int tx = (Wo + SS_TW - 1) / SS_TW, ty = (Ho + SS_TH - 1) / SS_TH;
   const int t = threadIdx.x;
@@ -51,68 +56,98 @@ ssim_fwd_tile_kernel(const float* __restrict__ x, const float* __restrict__ y, f
   const int r0 = (b / tx) * SS_TH, c0 = (b % tx) * SS_TW;
   const float* xp = x + (size_t)p * H * W;
   const float* yp = y + (size_t)p * H * W;
-  for (int e = t; e < SS_IH * SS_IW; e += 256) {
-    const int rr = e / SS_IW, cc = e - rr * SS_IW;
+  for (int e = t; e < SS_IH * SS_IWP; e += SS_NT) {
+    const int rr = e / SS_IWP, cc = e - rr * SS_IWP;
     const int r = r0 + rr, c = c0 + cc;
-    const bool in = r < H && c < W;
+    const bool in = cc < SS_IW && r < H && c < W;
     xs[rr][cc] = in ? xp[(size_t)r * W + c] : 0.0f;
     ys[rr][cc] = in ? yp[(size_t)r * W + c] : 0.0f;
   }
   __syncthreads();
-  for (int e = t; e < SS_IH * SS_TW; e += 256) {
-    const int rr = e / SS_TW, cc = e - rr * SS_TW;
-    float a = 0.f, bb_ = 0.f, aa = 0.f, bb = 0.f, ab = 0.f;
+  // horizontal pass: one item = one row x 4 consecutive columns, its 14 x and y values read as 16-B LDS loads
+  for (int e = t; e < SS_IH * (SS_TW / 4); e += SS_NT) {
+    const int rr = e / (SS_TW / 4), cc = 4 * (e - rr * (SS_TW / 4));
+    float xv[16], yv[16];
 #pragma unroll
-    for (int k = 0; k < SS_WIN; ++k) {
-      const float xv = xs[rr][cc + k], yv = ys[rr][cc + k], g = win.g[k];
-      a += g * xv;
-      bb_ += g * yv;
-      aa += g * xv * xv;
-      bb += g * yv * yv;
-      ab += g * xv * yv;
+    for (int q = 0; q < 4; ++q) {
+      const f32x4 a4 = *reinterpret_cast<const f32x4*>(&xs[rr][cc + 4 * q]);
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(&ys[rr][cc + 4 * q]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { xv[4 * q + j] = a4[j]; yv[4 * q + j] = b4[j]; }
     }
-    hm[0][rr][cc] = a;
-    hm[1][rr][cc] = bb_;
-    hm[2][rr][cc] = aa;
-    hm[3][rr][cc] = bb;
-    hm[4][rr][cc] = ab;
+    f32x4 o0, o1, o2, o3, o4;
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      float a = 0.f, bb_ = 0.f, aa = 0.f, bb = 0.f, ab = 0.f;
+#pragma unroll
+      for (int k = 0; k < SS_WIN; ++k) {
+        const float xk = xv[o + k], yk = yv[o + k], g = win.g[k];
+        a += g * xk;
+        bb_ += g * yk;
+        aa += g * xk * xk;
+        bb += g * yk * yk;
+        ab += g * xk * yk;
+      }
+      o0[o] = a; o1[o] = bb_; o2[o] = aa; o3[o] = bb; o4[o] = ab;
+    }
+    *reinterpret_cast<f32x4*>(&hm[0][rr][cc]) = o0;
+    *reinterpret_cast<f32x4*>(&hm[1][rr][cc]) = o1;
+    *reinterpret_cast<f32x4*>(&hm[2][rr][cc]) = o2;
+    *reinterpret_cast<f32x4*>(&hm[3][rr][cc]) = o3;
+    *reinterpret_cast<f32x4*>(&hm[4][rr][cc]) = o4;
   }
   __syncthreads();
   const long long no = (long long)P * Ho * Wo;
   double acc = 0.0;
-  for (int e = t; e < SS_TH * SS_TW; e += 256) {
-    const int rr = e / SS_TW, cc = e - rr * SS_TW;
-    const int r = r0 + rr, c = c0 + cc;
-    if (r >= Ho || c >= Wo) continue;
-    float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+  // each item: one column, SS_VR consecutive output rows; the SS_VR + 10 filtered rows it needs are read from LDS
+  // once (per output the taps still accumulate in order 0..10, as one output per item would)
+  for (int e = t; e < (SS_TH / SS_VR) * SS_TW; e += SS_NT) {
+    const int rs = e / SS_TW, cc = e - rs * SS_TW;
+    const int rr0 = rs * SS_VR;
+    float hv[5][SS_VR + SS_WIN - 1];
 #pragma unroll
-    for (int k = 0; k < SS_WIN; ++k) {
-      const float g = win.g[k];
-      m1 += g * hm[0][rr + k][cc];
-      m2 += g * hm[1][rr + k][cc];
-      e11 += g * hm[2][rr + k][cc];
-      e22 += g * hm[3][rr + k][cc];
-      e12 += g * hm[4][rr + k][cc];
-    }
-    const float s11 = e11 - m1 * m1, s22 = e22 - m2 * m2, s12 = e12 - m1 * m2;
-    const float A1 = 2.f * m1 * m2 + c1, B1 = m1 * m1 + m2 * m2 + c1;
-    const float A2 = 2.f * s12 + c2, B2 = s11 + s22 + c2;
-    const float l = A1 / B1, cs = A2 / B2;
-    acc += (double)(l * cs);
-    if (d) {
-      const long long i = ((long long)p * Ho + r) * Wo + c;
-      const float dl = (2.f * m2 * B1 - A1 * 2.f * m1) / (B1 * B1);
-      const float dcs = (-2.f * m2 * B2 + A2 * 2.f * m1) / (B2 * B2);
-      d[i] = dl * cs + l * dcs;             // dS / d mu_x
-      d[no + i] = -l * A2 / (B2 * B2);      // dS / d E[x^2]
-      d[2 * no + i] = l * 2.f / B2;         // dS / d E[xy]
+    for (int m = 0; m < 5; ++m)
+#pragma unroll
+      for (int k = 0; k < SS_VR + SS_WIN - 1; ++k) hv[m][k] = hm[m][rr0 + k][cc];
+#pragma unroll
+    for (int o = 0; o < SS_VR; ++o) {
+      const int r = r0 + rr0 + o, c = c0 + cc;
+      if (r >= Ho || c >= Wo) continue;
+      float m1 = 0.f, m2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+#pragma unroll
+      for (int k = 0; k < SS_WIN; ++k) {
+        const float g = win.g[k];
+        m1 += g * hv[0][o + k];
+        m2 += g * hv[1][o + k];
+        e11 += g * hv[2][o + k];
+        e22 += g * hv[3][o + k];
+        e12 += g * hv[4][o + k];
+      }
+      const float s11 = e11 - m1 * m1, s22 = e22 - m2 * m2, s12 = e12 - m1 * m2;
+      const float A1 = 2.f * m1 * m2 + c1, B1 = m1 * m1 + m2 * m2 + c1;
+      const float A2 = 2.f * s12 + c2, B2 = s11 + s22 + c2;
+      const float l = A1 / B1, cs = A2 / B2;
+      acc += (double)(l * cs);
+      if (d) {
+        const long long i = ((long long)p * Ho + r) * Wo + c;
+        const float dl = (2.f * m2 * B1 - A1 * 2.f * m1) / (B1 * B1);
+        const float dcs = (-2.f * m2 * B2 + A2 * 2.f * m1) / (B2 * B2);
+        d[i] = dl * cs + l * dcs;             // dS / d mu_x
+        d[no + i] = -l * A2 / (B2 * B2);      // dS / d E[x^2]
+        d[2 * no + i] = l * 2.f / B2;         // dS / d E[xy]
+      }
     }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if ((t & 63) == 0) red[t >> 6] = acc;
   __syncthreads();
-  if (t == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (t == 0) {
+    double sum = 0.0;
+#pragma unroll
+    for (int w = 0; w < SS_NT / 64; ++w) sum += red[w];
+    part[blockIdx.x] = sum;
+  }
 }
 
 __global__ void __launch_bounds__(256)
@@ -176,7 +211,7 @@ extern "C" int tmae_distortion_fwd(const float* x, const float* y, int P, int H,
   const int nt = ssim_tiles(P, Ho, Wo);
   TMAE_REQUIRE(2ll * nt <= 5ll * P * H * Wo, "tmae_distortion_fwd: workspace");
   double* tpart = reinterpret_cast<double*>(hwork);
-  hipLaunchKernelGGL(ssim_fwd_tile_kernel, dim3((unsigned)nt), dim3(256), 0, st, x, y, dmaps, P, H, W, win,
+  hipLaunchKernelGGL(ssim_fwd_tile_kernel, dim3((unsigned)nt), dim3(SS_NT), 0, st, x, y, dmaps, P, H, W, win,
                      0.01f * 0.01f, 0.03f * 0.03f, tpart);
   hipLaunchKernelGGL(l1_partial_kernel, dim3(SS_BLOCKS), dim3(256), 0, st, x, y, ni, part + SS_BLOCKS);
   hipLaunchKernelGGL(distortion_final_kernel, dim3(1), dim3(256), 0, st, tpart, nt, part + SS_BLOCKS, SS_BLOCKS,
@@ -189,12 +224,12 @@ extern "C" int tmae_distortion_fwd(const float* x, const float* y, int P, int H,
 // the transposed vertical filter v[k][r][c'] = sum_t g[t] d[k][r - t][c'] for the tile's rows and columns
 // c0 - 10 .. c0 + 63 to LDS; then gx[r][c] = -g_ssim / N_out (G^T D1 + 2 x G^T D2 + y G^T D3) + g_l1 sign(x - y) / N_in
 // with the transposed horizontal filter.  Taps outside the valid output add g * 0.
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(SS_NT)
 ssim_bwd_tile_kernel(const float* __restrict__ d, const float* __restrict__ x, const float* __restrict__ y,
                      float* __restrict__ gx, int P, int H, int W, SsimWin win, const float* __restrict__ gout,
                      float inv_out, float inv_in) {
   __shared__ float ds[3][SS_IH][SS_IW];
-  __shared__ float vs[3][SS_TH][SS_IW];
+  __shared__ __attribute__((aligned(16))) float vs[3][SS_TH][SS_IWP];
   const int Wo = W - (SS_WIN - 1), Ho = H - (SS_WIN - 1);
   const int tx = (W + SS_TW - 1) / SS_TW, ty = (H + SS_TH - 1) / SS_TH;
   const int t = threadIdx.x;
@@ -205,7 +240,7 @@ ssim_bwd_tile_kernel(const float* __restrict__ d, const float* __restrict__ x, c
   const long long no = (long long)P * Ho * Wo;
   const float* dp = d + (size_t)p * Ho * Wo;
   // ds[k][i][j] = d[k][r0 - 10 + i][c0 - 10 + j]
-  for (int e = t; e < SS_IH * SS_IW; e += 256) {
+  for (int e = t; e < SS_IH * SS_IW; e += SS_NT) {
     const int i = e / SS_IW, j = e - i * SS_IW;
     const int r = r0 - (SS_WIN - 1) + i, c = c0 - (SS_WIN - 1) + j;
     const bool in = r >= 0 && r < Ho && c >= 0 && c < Wo;
@@ -215,39 +250,81 @@ ssim_bwd_tile_kernel(const float* __restrict__ d, const float* __restrict__ x, c
   }
   __syncthreads();
   // vs[k][i][j] = v[k][r0 + i][c0 - 10 + j] = sum_t g[t] d[k][r0 + i - t][...] = sum_t g[t] ds[k][i + 10 - t][j]
-  for (int e = t; e < SS_TH * SS_IW; e += 256) {
-    const int i = e / SS_IW, j = e - i * SS_IW;
-    float a = 0.f, bq = 0.f, q = 0.f;
+  for (int e = t; e < (SS_TH / SS_VR) * SS_IW; e += SS_NT) {  // SS_VR rows per item, as in the forward
+    const int is = e / SS_IW, j = e - is * SS_IW;
+    const int i0 = is * SS_VR;
+    float dv[3][SS_VR + SS_WIN - 1];
 #pragma unroll
-    for (int k = 0; k < SS_WIN; ++k) {
-      const float g = win.g[k];
-      a += g * ds[0][i + SS_WIN - 1 - k][j];
-      bq += g * ds[1][i + SS_WIN - 1 - k][j];
-      q += g * ds[2][i + SS_WIN - 1 - k][j];
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int k = 0; k < SS_VR + SS_WIN - 1; ++k) dv[m][k] = ds[m][i0 + k][j];
+#pragma unroll
+    for (int o = 0; o < SS_VR; ++o) {
+      float a = 0.f, bq = 0.f, q = 0.f;
+#pragma unroll
+      for (int k = 0; k < SS_WIN; ++k) {
+        const float g = win.g[k];
+        a += g * dv[0][o + SS_WIN - 1 - k];
+        bq += g * dv[1][o + SS_WIN - 1 - k];
+        q += g * dv[2][o + SS_WIN - 1 - k];
+      }
+      vs[0][i0 + o][j] = a;
+      vs[1][i0 + o][j] = bq;
+      vs[2][i0 + o][j] = q;
     }
-    vs[0][i][j] = a;
-    vs[1][i][j] = bq;
-    vs[2][i][j] = q;
   }
   __syncthreads();
   const float gs = gout ? gout[0] : 0.0f, gl = gout ? gout[1] : 0.0f;
-  for (int e = t; e < SS_TH * SS_TW; e += 256) {
-    const int i = e / SS_TW, j = e - i * SS_TW;
+  // transposed horizontal pass + the combination with x and y: one item = one row x 4 consecutive columns, the
+  // 14 v values of each map read as 16-B LDS loads, x / y / dx as 16-B global accesses
+  for (int e = t; e < SS_TH * (SS_TW / 4); e += SS_NT) {
+    const int i = e / (SS_TW / 4), j = 4 * (e - i * (SS_TW / 4));
     const int r = r0 + i, c = c0 + j;
     if (r >= H || c >= W) continue;
-    float a = 0.f, bq = 0.f, q = 0.f;
+    float vv[3][16];
 #pragma unroll
-    for (int k = 0; k < SS_WIN; ++k) {  // v column c - k = vs column j + 10 - k
-      const float g = win.g[k];
-      a += g * vs[0][i][j + SS_WIN - 1 - k];
-      bq += g * vs[1][i][j + SS_WIN - 1 - k];
-      q += g * vs[2][i][j + SS_WIN - 1 - k];
-    }
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const f32x4 v4 = *reinterpret_cast<const f32x4*>(&vs[m][i][j + 4 * q4]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) vv[m][4 * q4 + u] = v4[u];
+      }
     const size_t o = ((size_t)p * H + r) * W + c;
-    const float xv = x[o], yv = y[o];
-    const float diff = xv - yv;
-    const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
-    gx[o] = -gs * inv_out * (a + 2.f * xv * bq + yv * q) + gl * inv_in * sg;
+    const bool full = c + 4 <= W && (W & 3) == 0;
+    f32x4 xv4, yv4, gv4;
+    if (full) {
+      xv4 = *reinterpret_cast<const f32x4*>(x + o);
+      yv4 = *reinterpret_cast<const f32x4*>(y + o);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        xv4[u] = c + u < W ? x[o + u] : 0.f;
+        yv4[u] = c + u < W ? y[o + u] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float a = 0.f, bq = 0.f, q = 0.f;
+#pragma unroll
+      for (int k = 0; k < SS_WIN; ++k) {  // v column c + u - k = vs column j + u + 10 - k
+        const float g = win.g[k];
+        a += g * vv[0][u + SS_WIN - 1 - k];
+        bq += g * vv[1][u + SS_WIN - 1 - k];
+        q += g * vv[2][u + SS_WIN - 1 - k];
+      }
+      const float xv = xv4[u], yv = yv4[u];
+      const float diff = xv - yv;
+      const float sg = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+      gv4[u] = -gs * inv_out * (a + 2.f * xv * bq + yv * q) + gl * inv_in * sg;
+    }
+    if (full) {
+      *reinterpret_cast<f32x4*>(gx + o) = gv4;
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (c + u < W) gx[o + u] = gv4[u];
+    }
   }
 }
 
@@ -261,7 +338,7 @@ extern "C" int tmae_distortion_bwd(const float* x, const float* y, int P, int H,
   const long long ni = (long long)P * H * W;
   TMAE_REQUIRE(ni < (1ll << 31), "tmae_distortion_bwd: %lld pixels exceed the 32-bit index range", ni);
   const int nt = P * ((H + SS_TH - 1) / SS_TH) * ((W + SS_TW - 1) / SS_TW);
-  hipLaunchKernelGGL(ssim_bwd_tile_kernel, dim3((unsigned)nt), dim3(256), 0, st, dmaps, x, y, gx, P, H, W, win, gout,
+  hipLaunchKernelGGL(ssim_bwd_tile_kernel, dim3((unsigned)nt), dim3(SS_NT), 0, st, dmaps, x, y, gx, P, H, W, win, gout,
                      (float)(1.0 / ((double)P * Ho * Wo)), (float)(1.0 / (double)ni));
   TMAE_LAUNCH_CHECK("tmae_distortion_bwd");
 }

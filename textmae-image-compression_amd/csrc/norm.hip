@@ -7,7 +7,7 @@
 
 // RPW rows per wave: gamma / beta loaded once per wave, all RPW rows' loads in flight together.  Measured
 // slower at the bench shapes (42 launches: 390 us at 4 or 2 rows per wave, 348 us at 1 -- fewer waves hide
-// less latency), so one row per wave is the default; TMAE_LN_RPW=2/4 selects the others.
+// less latency), so the launcher instantiates one row per wave only.
 template <typename OT, int VPL, int RPW>
 __global__ void __launch_bounds__(256)
 layernorm_kernel(const float* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,

@@ -201,8 +201,7 @@ class MCM(CompressionModel):
             ex = self._executor(imgs.shape[0], imgs.device)
             out = ex.run(imgs, total_scores, self.training, noise)
             x_hat = out["x_hat"]
-            loss = self.forward_loss(imgs, x_hat) if self.distortion != "none" else (
-                torch.zeros((), device=imgs.device),) * 3
+            loss = self.forward_loss(imgs, x_hat) if self.distortion != "none" else (ex.zero_loss,) * 3
         return {"loss": loss, "likelihoods": {"y": out["y"], "z": out["z"]}, "x_hat": x_hat}
 
     def _forward_train(self, imgs, total_scores, noise):
@@ -369,6 +368,7 @@ class _Executor:
         self.ZLIK = z(B, N, self.hz, self.hz)
         self.ZHAT = z(B * self.hz * self.hz, N, dtype=dt)
         self.eb_table = z(N, 59)
+        self.zero_loss = torch.zeros((), device=device)  # the loss terms of distortion="none" (never written)
         hs_out = [m.h_s_mean[0].out_channels, m.h_s_mean[2][0].out_channels // 4, m.h_s_mean[4].out_channels,
                   m.h_s_mean[6][0].out_channels // 4]
         hs_res = [self.hz, 2 * self.hz, 2 * self.hz, g]
@@ -531,6 +531,9 @@ class _Executor:
         else:
             z_noise = y_noise = None
 
+        # the likelihoods are returned to the caller: fresh tensors per forward (no copy of the executor's)
+        self.ZLIK = torch.empty_like(self.ZLIK)
+        self.YLIK = torch.empty_like(self.YLIK)
         shuf, rest = self._front(imgs, scores)
 
         # ---- entropy bottleneck + z_hat (MCM.py:741-744)
@@ -544,7 +547,7 @@ class _Executor:
         self._slices(self._gc_forward(y_noise), chain_ok=True)
 
         x_hat = self._back(shuf, imgs.shape[1])
-        return {"x_hat": x_hat, "y": self.YLIK.clone(), "z": self.ZLIK.clone(), "ids_restore": rest,
+        return {"x_hat": x_hat, "y": self.YLIK, "z": self.ZLIK, "ids_restore": rest,
                 "ids_shuffle": shuf}
 
     # ------------------------------------------------------------------ compress / decompress
