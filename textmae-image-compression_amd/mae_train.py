@@ -104,6 +104,7 @@ class MAETrainExec(_VitTrainBase):
         self.gflat, self.sync = gflat, sync
         if sync is not None:
             sync.attach(gflat)
+        self._side_begin()
         G = self.grad
         npred = self.pred.shape[1]
         # ---- forward_loss + decoder_pred (models_mae.py:193, 198-214)
@@ -111,7 +112,7 @@ class MAETrainExec(_VitTrainBase):
         dp_in = dpred.float().contiguous() if dpred is not None else None
         dP = T.mae_loss_bwd(self.pred, self.imgs, self.rest, keep, P, m.norm_pix_loss, dl, dp_in,
                             self._e(B * L, npred), dt)
-        T.wgrad(dP, self.dn, npred, Dd, B * L, G(m.decoder_pred.weight), dt, bias=G(m.decoder_pred.bias))
+        self._wg(dP, self.dn, npred, Dd, B * L, G(m.decoder_pred.weight), dt, bias=G(m.decoder_pred.bias))
         ddn = torch.empty((B * L, Dd), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dP, W.t(m.decoder_pred.weight), B * L, npred, Dd, dt, out=ddn)
         # ---- decoder_norm (the cls row gets no gradient: pred drops it) + blocks
@@ -127,7 +128,7 @@ class MAETrainExec(_VitTrainBase):
         # ---- decoder_embed + mask tokens: row 0 of each image is the cls row, rows 1..keep the kept patches
         dtok = self._e(B * Te, Dd)
         T.decoder_embed_bwd_gather(ddec, self.shuf, dtok, B, Te, L, Dd, dt, dmask=G(m.mask_token).view(-1))
-        T.wgrad(dtok, self.lat, Dd, E, B * Te, G(m.decoder_embed.weight), dt, bias=G(m.decoder_embed.bias))
+        self._wg(dtok, self.lat, Dd, E, B * Te, G(m.decoder_embed.weight), dt, bias=G(m.decoder_embed.bias))
         dlat = torch.empty((B * Te, E), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dtok, W.t(m.decoder_embed.weight), B * Te, Dd, E, dt, out=dlat)
         self._ready(m.mask_token)
@@ -142,10 +143,11 @@ class MAETrainExec(_VitTrainBase):
             self._ready(_block_params(blk)[-1])
         # ---- patch embed (kept patches) + cls token
         pw = m.patch_embed.proj.weight
-        T.wgrad(dt_op, self.patches, E, pw[0].numel(), B * keep, G(pw), dt, lda=E, a_remap=(keep, Te, 1))
+        self._wg(dt_op, self.patches, E, pw[0].numel(), B * keep, G(pw), dt, lda=E, a_remap=(keep, Te, 1))
         T.colsum(dt_tok, B * keep, E, G(m.patch_embed.proj.bias), row_group=keep, group_stride=Te, row_offset=1)
         T.colsum(dt_tok, B, E, G(m.cls_token).view(-1), row_group=1, group_stride=Te, row_offset=0)
         self._ready(m.cls_token)
+        self._side_join()
 
 
 class _MAETrainFn(torch.autograd.Function):

@@ -178,6 +178,12 @@ class _VitTrainBase:
     the backward finishes the parameters (DP buckets), and the timm Block forward (keeping what its backward
     needs) / backward."""
 
+    _side = None          # side stream of the weight gradients (_wg), made by _side_begin
+    _side_used = False
+    _pending = ()
+    _queued = ()
+    _groups = ()
+
     def _layout(self):
         """parameter gradient layout: the order in which the backward finishes them (DP buckets)"""
         self.params = [p for p in self._grad_order() if p.requires_grad]
@@ -215,9 +221,72 @@ class _VitTrainBase:
         return self.gflat[off:off + p.numel()].view(p.shape)
 
     def _ready(self, p):
-        """every gradient up to and including p's is final (DP bucket hand-off)"""
-        if self.sync is not None:
-            self.sync.ready(self.offsets[id(p)] + p.numel())
+        """every gradient up to and including p's is final (DP bucket hand-off).  With weight gradients on the
+        side stream the hand-off lags one call: the compute stream waits for the side stream's work up to the
+        PREVIOUS hand-off point (long done by then), so the collective never stalls the data-gradient chain."""
+        if self.sync is None:
+            self._wg_flush()
+            return
+        if self._side is not None:
+            self._wg_flush(last=True)  # the event below must follow every group up to p
+        upto = self.offsets[id(p)] + p.numel()
+        if not self._side_used:
+            self.sync.ready(upto)
+            return
+        ev = torch.cuda.Event()
+        ev.record(self._side)
+        self._pending.append((ev, upto))
+        main = torch.cuda.current_stream(self.device)
+        while len(self._pending) > 1:
+            e, u = self._pending.pop(0)
+            main.wait_event(e)
+            self.sync.ready(u)
+
+    # ------------------------------------------------------------------ side-stream weight gradients
+    def _side_begin(self):
+        """called at the top of a backward: a side stream for the weight gradients when on a GPU"""
+        if "_side" not in self.__dict__:  # the class default is None
+            self._side = torch.cuda.Stream(device=self.device) if torch.device(self.device).type == "cuda" else None
+        self._side_used = False
+        self._pending, self._keep, self._queued, self._groups = [], [], [], []
+
+    def _wg(self, a, *args, **kw):
+        """T.wgrad for the side stream: a weight gradient has no consumer inside the backward, so it runs under
+        the serial data-gradient chain.  Queued here and enqueued by _wg_flush behind ONE fork per group (a stack,
+        a block): a captured graph pays a cross-queue dependency per fork.  `a` (this layer's output gradient, a
+        fresh tensor of the chain) is kept alive until the join; every other operand is a saved activation."""
+        if self._side is None:
+            return T.wgrad(a, *args, **kw)
+        self._queued.append((a, args, kw))
+
+    def _wg_flush(self, last=False):
+        """close the queued group: record its fork point on the compute stream now, but enqueue the group on the
+        side stream only at the NEXT flush (or the join), after the compute stream's next kernels -- in a captured
+        graph the fork node's first child is then the compute chain's next kernel, which keeps the compute
+        chain on its own queue (the side branch takes the cross-queue dependency instead)"""
+        if self._queued:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._groups.append((ev, self._queued))
+            self._queued = []
+        while len(self._groups) > (0 if last else 1):
+            ev, group = self._groups.pop(0)
+            self._side.wait_event(ev)
+            with torch.cuda.stream(self._side):
+                for a, args, kw in group:
+                    T.wgrad(a, *args, ws_slot=4, **kw)
+                    self._keep.append(a)
+            self._side_used = True
+
+    def _side_join(self):
+        """order the compute stream after every side-stream weight gradient and hand off what is left"""
+        if self._side is not None:
+            self._wg_flush(last=True)
+        if self._side is not None and self._side_used:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+            for _, u in self._pending:
+                self.sync.ready(u)
+        self._pending, self._keep, self._side_used = [], [], False
 
     def _block_fwd(self, blk, x, B, Tn, store=None):
         dt, W = self.dtype, self.w
@@ -249,11 +318,11 @@ class _VitTrainBase:
         H = blk.attn.num_heads
         f32 = dt == torch.float32
         # fc2 (+ GELU of fc1 in the data-gradient epilogue)
-        T.wgrad(dres_op, s.h, D, hid, rows, G(blk.mlp.fc2.weight), dt)  # fc2.bias: folded into norm2's backward
+        self._wg(dres_op, s.h, D, hid, rows, G(blk.mlp.fc2.weight), dt)  # fc2.bias: folded into norm2's backward
         dh = self._e(rows, hid)
         T.dgrad_linear(dres_op, W.t(blk.mlp.fc2.weight), rows, D, hid, dt, out=dh, pre=s.hpre)
         # fc1
-        T.wgrad(dh, s.a2, hid, D, rows, G(blk.mlp.fc1.weight), dt, bias=G(blk.mlp.fc1.bias))
+        self._wg(dh, s.a2, hid, D, rows, G(blk.mlp.fc1.weight), dt, bias=G(blk.mlp.fc1.bias))
         da2 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dh, W.t(blk.mlp.fc1.weight), rows, hid, D, dt, out=da2)
         # norm2 + residual
@@ -262,14 +331,14 @@ class _VitTrainBase:
         T.layernorm_bwd(s.xmid, blk.norm2.weight, da2, dmid, rows, D, blk.norm2.eps, G(blk.norm2.weight),
                         G(blk.norm2.bias), dres=dres, dxop=None if f32 else dmid_op, dres_colsum=G(blk.mlp.fc2.bias))
         # proj
-        T.wgrad(dmid_op, s.att, D, D, rows, G(blk.attn.proj.weight), dt)  # proj.bias: folded into norm1's backward
+        self._wg(dmid_op, s.att, D, D, rows, G(blk.attn.proj.weight), dt)  # proj.bias: folded into norm1's backward
         datt = self._e(rows, D)
         T.dgrad_linear(dmid_op, W.t(blk.attn.proj.weight), rows, D, D, dt, out=datt)
         # attention core
         dqkv = self._e(rows, 3 * D)
         T.mha_bwd(s.qkv, s.att, datt, s.lse, dqkv, B, Tn, H, D // H, blk.attn.scale, dt)
         # qkv
-        T.wgrad(dqkv, s.a1, 3 * D, D, rows, G(blk.attn.qkv.weight), dt,
+        self._wg(dqkv, s.a1, 3 * D, D, rows, G(blk.attn.qkv.weight), dt,
                 bias=G(blk.attn.qkv.bias) if blk.attn.qkv.bias is not None else None)
         da1 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dqkv, W.t(blk.attn.qkv.weight), rows, 3 * D, D, dt, out=da1)
@@ -671,6 +740,7 @@ class TrainExec(_VitTrainBase):
         self.sync = sync
         if sync is not None:
             sync.attach(gflat)
+        self._side_begin()
         G = self.grad
         dxhat = dxhat.float().contiguous() if dxhat is not None else torch.zeros_like(self.imgs)
         dylik = dylik.float().contiguous() if dylik is not None else None
@@ -679,7 +749,7 @@ class TrainExec(_VitTrainBase):
         # ---- decoder_pred + unpatchify (MCM.py:683-686, 797)
         dP = T.patchify(dxhat, self._e(B * L, dxhat.shape[1] * P * P), P, dt)
         npred = dP.shape[1]
-        T.wgrad(dP, self.dn, npred, Dd, B * L, G(m.decoder_pred.weight), dt, bias=G(m.decoder_pred.bias))
+        self._wg(dP, self.dn, npred, Dd, B * L, G(m.decoder_pred.weight), dt, bias=G(m.decoder_pred.bias))
         ddn = torch.empty((B * L, Dd), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dP, W.t(m.decoder_pred.weight), B * L, npred, Dd, dt, out=ddn)
         ddec = self._z(B * Td, Dd)
@@ -695,7 +765,7 @@ class TrainExec(_VitTrainBase):
         # ---- decoder_embed + mask tokens (MCM.py:657-675)
         dtok = self._e(Mp, Dd)
         T.decoder_embed_bwd_gather(ddec, self.shuf, dtok, B, K, L, Dd, dt, dmask=G(m.mask_token).view(-1))
-        T.wgrad(dtok, self.gs_out, Dd, E, Mp, G(m.decoder_embed.weight), dt, bias=G(m.decoder_embed.bias))
+        self._wg(dtok, self.gs_out, Dd, E, Mp, G(m.decoder_embed.weight), dt, bias=G(m.decoder_embed.bias))
         d = self._e(Mp, E)
         T.dgrad_linear(dtok, W.t(m.decoder_embed.weight), Mp, Dd, E, dt, out=d)
         self._ready(m.mask_token)
@@ -707,7 +777,7 @@ class TrainExec(_VitTrainBase):
             x, _ = self.gs[j]
             pre_prev = self.gs[j - 1][1] if j > 0 else None
             cin, cout = l.in_channels, l.out_channels
-            T.wgrad(d, x, cout, cin, Mp, G(l.weight), dt, layout="dense_t", bias=G(l.bias))
+            self._wg(d, x, cout, cin, Mp, G(l.weight), dt, layout="dense_t", bias=G(l.bias))
             dx = self._e(Mp, cin)
             T.dgrad_linear(d, W.raw(l.weight), Mp, cout, cin, dt, out=dx, pre=pre_prev)
             d = dx
@@ -739,7 +809,7 @@ class TrainExec(_VitTrainBase):
             pre_prev = self.ha[j - 1][4] if j > 0 else None
             cout = c.out_channels
             Ho = (H + 2 - 3) // s + 1
-            T.wgrad(d, x, cout, 9 * cin, B * Ho * Ho, G(c.weight), dt,
+            self._wg(d, x, cout, 9 * cin, B * Ho * Ho, G(c.weight), dt,
                     conv=dict(c1=cin, H=H, W=H, stride=s, cin=cin), layout="conv", bias=G(c.bias))
             if j > 0:
                 dx = self._e(B * H * H, cin)
@@ -757,7 +827,7 @@ class TrainExec(_VitTrainBase):
             x, _ = self.ga[j]
             pre_prev = self.ga[j - 1][1] if j > 0 else None
             cin, cout = l.in_channels, l.out_channels
-            T.wgrad(d, x, cout, cin, Mp, G(l.weight), dt, bias=G(l.bias))
+            self._wg(d, x, cout, cin, Mp, G(l.weight), dt, bias=G(l.bias))
             if j > 0:
                 dx = self._e(Mp, cin)
                 T.dgrad_linear(d, W.t(l.weight), Mp, cout, cin, dt, out=dx, pre=pre_prev)
@@ -781,10 +851,11 @@ class TrainExec(_VitTrainBase):
 
         # ---- patch embed + cls token (MCM.py:615-626)
         pw = m.encoder_embed.proj.weight
-        T.wgrad(dt_op, self.patches, E, pw[0].numel(), B * K, G(pw), dt, lda=E, a_remap=(K, Te, 1))
+        self._wg(dt_op, self.patches, E, pw[0].numel(), B * K, G(pw), dt, lda=E, a_remap=(K, Te, 1))
         T.colsum(dt_tok, B * K, E, G(m.encoder_embed.proj.bias), row_group=K, group_stride=Te, row_offset=1)
         T.colsum(dt_tok, B, E, G(m.cls_token).view(-1), row_group=1, group_stride=Te, row_offset=0)
         self._ready(m.cls_token)
+        self._side_join()
 
     def _eb_grads(self, eb):
         from ._lib import EBParams
@@ -806,7 +877,7 @@ class TrainExec(_VitTrainBase):
             c, pshuf = layers[j]
             x, cin, H, _, _ = saved[j]
             cout = c.out_channels
-            T.wgrad(d, x, cout, 9 * cin, B * H * H, G(c.weight), dt, conv=dict(c1=cin, H=H, W=H, cin=cin),
+            self._wg(d, x, cout, 9 * cin, B * H * H, G(c.weight), dt, conv=dict(c1=cin, H=H, W=H, cin=cin),
                     layout="conv", bias=G(c.bias))
             if j == 0:
                 T.conv_dgrad(d, W.conv_dg(c.weight), B, H, H, 1, cout, cin, dt, routes=[(dZH, cin, cin)])
@@ -834,9 +905,10 @@ class TrainExec(_VitTrainBase):
         dLS = self._z(Mp, M)
         dSUP = self._z(Mp, M)
         GS = torch.empty((Mp, M), dtype=torch.float32, device=self.device)
-        dT = self._e(Mp, sw)
-        dMU, dSG = self._e(Mp, sw), self._e(Mp, sw)
         for i in reversed(range(S)):
+            # fresh per slice: the side stream's weight gradients of slice i + 1 may still read the last ones
+            dT = self._e(Mp, sw)
+            dMU, dSG = self._e(Mp, sw), self._e(Mp, sw)
             k = min(i, ms)
             cin_m = M + sw * k
             rec = self.sl[i]
@@ -865,7 +937,7 @@ class TrainExec(_VitTrainBase):
             c = convs[l]
             cin, cout = c.in_channels, c.out_channels
             act_prev, pre_prev = saved[l - 1]
-            T.wgrad(d, act_prev, cout, 9 * cin, Mp, G(c.weight), dt, conv=dict(c1=cin, H=g, W=g, cin=cin),
+            self._wg(d, act_prev, cout, 9 * cin, Mp, G(c.weight), dt, conv=dict(c1=cin, H=g, W=g, cin=cin),
                     layout="conv", bias=G(c.bias))
             dx = self._e(Mp, cin)
             T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, out=dx, pre=pre_prev)
@@ -873,10 +945,11 @@ class TrainExec(_VitTrainBase):
         c = convs[0]
         x1, c1, ld1, x2, c2, ld2 = first
         cin, cout = c1 + c2, c.out_channels
-        T.wgrad(d, x1, cout, 9 * cin, Mp, G(c.weight), dt, ldb=ld1,
+        self._wg(d, x1, cout, 9 * cin, Mp, G(c.weight), dt, ldb=ld1,
                 conv=dict(x2=x2, c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
         # zero-width routes (no support slices yet) stay in place: their limits still partition the channels
         T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
+        self._wg_flush()
 
 
 def _bias(b):

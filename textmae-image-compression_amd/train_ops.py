@@ -73,7 +73,7 @@ def patch_gather(imgs, ids, out, keep, patch, dtype):
 
 # ------------------------------------------------------------------------------------- gradients
 def wgrad(a, b, M, N, K, out, dtype, lda=None, ldb=None, a_remap=(None, 0, 0), b_remap=(None, 0, 0), conv=None,
-          layout="dense", cin_total=None, ci_off=0, accumulate=False, bias=None, bias_accumulate=False):
+          layout="dense", cin_total=None, ci_off=0, accumulate=False, bias=None, bias_accumulate=False, ws_slot=1):
     """out <- sum_k A(k, m) B(k, n) in the parameter's layout; bias (optional) <- sum_k A(k, m), the bias
     gradient of the layer whose output gradient A is, formed by the same GEMM.
     layout: "dense" (out [M][N]), "dense_t" (out [N][M]: ConvTranspose2d 1x1 weights), "conv"
@@ -82,7 +82,7 @@ def wgrad(a, b, M, N, K, out, dtype, lda=None, ldb=None, a_remap=(None, 0, 0), b
     dev = out.device
     code = dtype_code(dtype)
     need = _lib.value("tmae_wgrad_workspace", M, N, K, code)
-    ws = scratch(dev, need, slot=1)
+    ws = scratch(dev, need, slot=ws_slot)  # slot 4: the side stream's weight gradients (mcm_train._wg)
     args = WgradArgs()
     args.a, args.lda = _p(a), (lda if lda is not None else M)
     G, Gs, off = a_remap
