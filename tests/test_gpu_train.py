@@ -430,6 +430,21 @@ def test_mcm_train_bf16_close_to_f32():
     check("_rel2:flat16", _rel2(flat16, flat32), 3e-3)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_side_stream_wgrads_bitwise(dt):
+    """weight gradients on the side stream (mcm_train._wg, deferred one-per-group forks) == the same backward
+    with every weight gradient on the compute stream, bit for bit; and the side stream really ran them"""
+    m, cfg, sd, imgs, scores, zn, yn, R = _model_and_oracle(SMALL, 5, 3, dt)
+    g_side, *_ = _hip_grads(m, imgs, scores, zn, yn, R)
+    ex = m._train_exec
+    assert ex.__dict__.get("_side") is not None and ex._side_calls > 0
+    ex._side = None  # _side_begin keeps an instance attribute: None = every weight gradient on the compute stream
+    g_one, *_ = _hip_grads(m, imgs, scores, zn, yn, R)
+    assert ex._side_calls == 0
+    bad = [k for k in g_side if not torch.equal(g_side[k], g_one[k])]
+    assert not bad, bad[:10]
+
+
 def _partial_loss_grads(m, imgs, scores, zn, yn, R, nsel):
     """HIP backward of a loss over the first `nsel` images only (rate of those images + sum(x_hat * R)), run
     at the batch of `imgs`: images never mix, so the gradient equals that of the same loss on a batch of

@@ -248,6 +248,7 @@ class _VitTrainBase:
         if "_side" not in self.__dict__:  # the class default is None
             self._side = torch.cuda.Stream(device=self.device) if torch.device(self.device).type == "cuda" else None
         self._side_used = False
+        self._side_calls = 0  # weight gradients the side stream ran in this backward (tests)
         self._pending, self._keep, self._queued, self._groups = [], [], [], []
 
     def _wg(self, a, *args, **kw):
@@ -276,6 +277,7 @@ class _VitTrainBase:
                 for a, args, kw in group:
                     T.wgrad(a, *args, ws_slot=4, **kw)
                     self._keep.append(a)
+                    self._side_calls += 1
             self._side_used = True
 
     def _side_join(self):
