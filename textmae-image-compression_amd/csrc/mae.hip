@@ -60,9 +60,24 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// offset of value lane + 64 k of a patchified row (e = (py * P + px) * C + c) from the patch's top-left pixel in
+// plane 0 of its image (NCHW), -1 past the row: the same for every row, so worked out once per thread (the two
+// integer divisions per value were most of the loss kernels' time)
+__device__ __forceinline__ void mae_offsets(int P, int C, int H, int W, int lane, int (&off)[MAE_VPL]) {
+  const int D = P * P * C;
+#pragma unroll
+  for (int k = 0; k < MAE_VPL; ++k) {
+    const int e = lane + 64 * k;
+    const int q = e / C, c = e - q * C;
+    const int py = q / P, px = q - py * P;
+    off[k] = e < D ? (c * H + py) * W + px : -1;
+  }
+}
+
 // the target of patch `row` (= b * L + l) in the lane-strided layout t[k] = value lane + 64 k of the patchified row
+// (models_mae.py:198-214 patchify + norm_pix_loss), offsets from mae_offsets
 __device__ __forceinline__ void mae_target(const float* __restrict__ imgs, int row, int L, int G, int P, int C, int H,
-                                           int W, int norm_pix, int lane, float (&t)[MAE_VPL]) {
+                                           int W, int norm_pix, int lane, const int (&off)[MAE_VPL], float (&t)[MAE_VPL]) {
   const int D = P * P * C;
   const int b = row / L, l = row - b * L;
   const int hy = l / G, hx = l - hy * G;
@@ -70,21 +85,15 @@ __device__ __forceinline__ void mae_target(const float* __restrict__ imgs, int r
   float s = 0.0f;
 #pragma unroll
   for (int k = 0; k < MAE_VPL; ++k) {
-    const int e = lane + 64 * k;
-    t[k] = 0.0f;
-    if (e < D) {
-      const int q = e / C, c = e - q * C;  // e = (py * P + px) * C + c
-      const int py = q / P, px = q - py * P;
-      t[k] = img[((size_t)c * H + py) * W + px];
-      s += t[k];
-    }
+    t[k] = off[k] >= 0 ? img[off[k]] : 0.0f;
+    s += t[k];
   }
   if (norm_pix) {
     const float mean = wave_sum(s) / (float)D;
     float v = 0.0f;
 #pragma unroll
     for (int k = 0; k < MAE_VPL; ++k)
-      if (lane + 64 * k < D) v += (t[k] - mean) * (t[k] - mean);
+      if (off[k] >= 0) v += (t[k] - mean) * (t[k] - mean);
     const float var = wave_sum(v) / (float)(D - 1);
     const float inv = 1.0f / sqrtf(var + 1e-6f);
 #pragma unroll
@@ -92,18 +101,24 @@ __device__ __forceinline__ void mae_target(const float* __restrict__ imgs, int r
   }
 }
 
+// PC / CC: the patch size / channel count as compile-time constants (16 / 3: every bench and reference config),
+// 0 = the run-time values; the constants turn mae_offsets' divisions into multiplies
+template <int PC, int CC>
 __global__ void __launch_bounds__(256)
 mae_loss_partial_kernel(const float* __restrict__ pred, const float* __restrict__ imgs,
-                        const int64_t* __restrict__ ids_restore, int n, int L, int G, int P, int C, int H, int W,
+                        const int64_t* __restrict__ ids_restore, int n, int L, int G, int P_, int C_, int H, int W,
                         int keep, int norm_pix, double* __restrict__ part) {
+  const int P = PC ? PC : P_, C = CC ? CC : C_;
   __shared__ double red[2][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int D = P * P * C;
   double num = 0.0, den = 0.0;
+  int off[MAE_VPL];
+  mae_offsets(P, C, H, W, lane, off);
   for (int row = blockIdx.x * 4 + wave; row < n * L; row += gridDim.x * 4) {
     const int b = row / L, l = row - b * L;
     float t[MAE_VPL];
-    mae_target(imgs, row, L, G, P, C, H, W, norm_pix, lane, t);
+    mae_target(imgs, row, L, G, P, C, H, W, norm_pix, lane, off, t);
     const float* pr = pred + (size_t)row * D;
     float se = 0.0f;
 #pragma unroll
@@ -159,8 +174,12 @@ extern "C" int tmae_mae_loss(const float* pred, const float* imgs, const int64_t
   TMAE_REQUIRE(P * P * C <= 64 * MAE_VPL && P * P * C > 1, "tmae_mae_loss: patch of %d values unsupported", P * P * C);
   const int G = H / P, L = G * G;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(mae_loss_partial_kernel, dim3(MAE_LOSS_BLOCKS), dim3(256), 0, st, pred, imgs, ids_restore, n, L,
-                     G, P, C, H, W, keep, norm_pix_loss, work);
+  if (P == 16 && C == 3)
+    hipLaunchKernelGGL((mae_loss_partial_kernel<16, 3>), dim3(MAE_LOSS_BLOCKS), dim3(256), 0, st, pred, imgs,
+                       ids_restore, n, L, G, P, C, H, W, keep, norm_pix_loss, work);
+  else
+    hipLaunchKernelGGL((mae_loss_partial_kernel<0, 0>), dim3(MAE_LOSS_BLOCKS), dim3(256), 0, st, pred, imgs,
+                       ids_restore, n, L, G, P, C, H, W, keep, norm_pix_loss, work);
   hipLaunchKernelGGL(mae_loss_final_kernel, dim3(1), dim3(256), 0, st, work, MAE_LOSS_BLOCKS, out);
   TMAE_LAUNCH_CHECK("tmae_mae_loss");
 }
@@ -169,15 +188,18 @@ extern "C" int tmae_mae_loss(const float* pred, const float* imgs, const int64_t
 // d loss / d pred[b][l][e] = g * mask[b][l] * 2 (pred - target) / (D * sum(mask)), sum(mask) = n (L - len_keep)
 // (autograd of models_mae.py:212-214); plus an incoming gradient of pred itself when dpred_in is given.
 // One wave per patch row, written in the operand dtype of the decoder_pred weight / data gradients.
-template <typename OT>
+template <typename OT, int PC, int CC>
 __global__ void __launch_bounds__(256)
 mae_loss_bwd_kernel(const float* __restrict__ pred, const float* __restrict__ imgs, const int64_t* __restrict__ ids_restore,
-                    int n, int L, int G, int P, int C, int H, int W, int keep, int norm_pix, const float* __restrict__ dloss,
+                    int n, int L, int G, int P_, int C_, int H, int W, int keep, int norm_pix, const float* __restrict__ dloss,
                     const float* __restrict__ dpred_in, OT* __restrict__ out) {
+  const int P = PC ? PC : P_, C = CC ? CC : C_;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int D = P * P * C;
   const float msum = (float)n * (float)(L - keep);
   const float g = dloss ? dloss[0] : 0.0f;
+  int off[MAE_VPL];
+  mae_offsets(P, C, H, W, lane, off);
   for (int row = blockIdx.x * 4 + wave; row < n * L; row += gridDim.x * 4) {
     const float m = ids_restore[row] >= keep ? 1.0f : 0.0f;
     const float sc = m > 0.0f && msum > 0.0f ? g * m / msum / (float)D : 0.0f;
@@ -185,7 +207,7 @@ mae_loss_bwd_kernel(const float* __restrict__ pred, const float* __restrict__ im
     OT* o = out + (size_t)row * D;
     const float* di = dpred_in ? dpred_in + (size_t)row * D : nullptr;
     float t[MAE_VPL];
-    if (sc != 0.0f) mae_target(imgs, row, L, G, P, C, H, W, norm_pix, lane, t);
+    if (sc != 0.0f) mae_target(imgs, row, L, G, P, C, H, W, norm_pix, lane, off, t);
 #pragma unroll
     for (int k = 0; k < MAE_VPL; ++k) {
       const int e = lane + 64 * k;
@@ -209,13 +231,20 @@ extern "C" int tmae_mae_loss_bwd(const float* pred, const float* imgs, const int
   const int G = H / P, L = G * G;
   if (n == 0) return TMAE_OK;
   hipStream_t st = (hipStream_t)stream;
-  const int nb = ceil_div(n * L, 4);
-  const dim3 grid((unsigned)(nb < 4096 ? nb : 4096));
-  if (out_dtype == TMAE_BF16)
-    hipLaunchKernelGGL(mae_loss_bwd_kernel<bf16>, grid, dim3(256), 0, st, pred, imgs, ids_restore, n, L, G, P, C, H, W,
-                       keep, norm_pix_loss, dloss, dpred_in, (bf16*)out);
-  else
-    hipLaunchKernelGGL(mae_loss_bwd_kernel<float>, grid, dim3(256), 0, st, pred, imgs, ids_restore, n, L, G, P, C, H,
-                       W, keep, norm_pix_loss, dloss, dpred_in, (float*)out);
+  // about three rows per wave: the per-thread offset table is worked out once per wave
+  const int nb = ceil_div(n * L, 12);
+  const dim3 grid((unsigned)(nb < 2048 ? nb : 2048));
+#define MAE_BWD_LAUNCH(OT, PC, CC)                                                                                   \
+  hipLaunchKernelGGL((mae_loss_bwd_kernel<OT, PC, CC>), grid, dim3(256), 0, st, pred, imgs, ids_restore, n, L, G, P, C, \
+                     H, W, keep, norm_pix_loss, dloss, dpred_in, (OT*)out)
+  const bool std_patch = P == 16 && C == 3;
+  if (out_dtype == TMAE_BF16) {
+    if (std_patch) MAE_BWD_LAUNCH(bf16, 16, 3);
+    else MAE_BWD_LAUNCH(bf16, 0, 0);
+  } else {
+    if (std_patch) MAE_BWD_LAUNCH(float, 16, 3);
+    else MAE_BWD_LAUNCH(float, 0, 0);
+  }
+#undef MAE_BWD_LAUNCH
   TMAE_LAUNCH_CHECK("tmae_mae_loss_bwd");
 }

@@ -1392,18 +1392,31 @@ dec_gather_kernel(const float* __restrict__ g, const int64_t* __restrict__ ids, 
 }
 
 // mask_token gradient: sum over every decoder row the mask token filled (MCM.py:660-664)
+// per image b, column d: the sum over the masked positions mi in [ntok - 1, L) of the decoder-input gradient row
+// 1 + ids[b][mi] (the mask token's gradient, before the fold over images).  Four waves per block split the
+// positions round-robin (their loads in flight together) and add their partials in wave order: one serial walk
+// over the ~150 positions of an image was a chain of dependent index + row loads (46 us per call).
 __global__ void __launch_bounds__(256)
 mask_token_bwd_kernel(const float* __restrict__ g, const int64_t* __restrict__ ids, float* __restrict__ part, int n,
                       int ntok, int L, int D) {
+  __shared__ float red[4][64];
+  __shared__ int rows[256];
   const int b = blockIdx.y;
-  const int d = blockIdx.x * 256 + threadIdx.x;
-  if (d >= D) return;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int d = blockIdx.x * 64 + tx;
   float s = 0.0f;
-  for (int mi = ntok - 1; mi < L; ++mi) {
-    const int row = 1 + (int)ids[(size_t)b * L + mi];
-    s += g[((size_t)b * (L + 1) + row) * D + d];
+  // the masked positions' row indexes go through LDS first, so the row loads below are all independent
+  for (int c0 = ntok - 1; c0 < L; c0 += 256) {
+    const int nc = min(256, L - c0);
+    __syncthreads();
+    if ((int)threadIdx.x < nc) rows[threadIdx.x] = 1 + (int)ids[(size_t)b * L + c0 + threadIdx.x];
+    __syncthreads();
+    if (d < D)
+      for (int i = ty; i < nc; i += 4) s += g[((size_t)b * (L + 1) + rows[i]) * D + d];
   }
-  part[(size_t)b * D + d] = s;
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && d < D) part[(size_t)b * D + d] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
 }
 
 extern "C" int tmae_decoder_embed_bwd_gather(const float* dec_grad, const int64_t* ids_shuffle, void* tok_grad, int n,
@@ -1423,7 +1436,7 @@ extern "C" int tmae_decoder_embed_bwd_gather(const float* dec_grad, const int64_
   }
   if (dmask) {
     TMAE_REQUIRE(mask_part != nullptr, "tmae_decoder_embed_bwd_gather: mask_part workspace required");
-    hipLaunchKernelGGL(mask_token_bwd_kernel, dim3(ceil_div(D, 256), n), dim3(256), 0, st, dec_grad, ids_shuffle,
+    hipLaunchKernelGGL(mask_token_bwd_kernel, dim3(ceil_div(D, 64), n), dim3(256), 0, st, dec_grad, ids_shuffle,
                        mask_part, n, ntok, L, D);
     fold_rows(mask_part, n, D, dmask, dmask, D, accumulate, st);
   }
