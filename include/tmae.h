@@ -441,10 +441,10 @@ int tmae_unshuffle_bwd(const void* dy, int dy_f32, int ldy, const void* pre, int
                        int C4, int dtype, void* stream);
 /* out = dy * gelu'(pre), elementwise */
 int tmae_gelu_bwd(const void* dy, int dy_f32, const void* pre, void* out, long long total, int dtype, void* stream);
-/* y_hat = y_hat_pre + 0.5 tanh(t) (MCM.py:782-783): g = g32 (f32) + g16 (dtype), either optional;
+/* y_hat = y_hat_pre + 0.5 tanh(t) (MCM.py:782-783): g = (g32 + g32b) (f32) + g16 (dtype), each optional;
  * dt = g * 0.5 (1 - tanh^2 t) (dtype), gsum = g (f32, optional) */
-int tmae_lrp_bwd(const float* g32, int ld32, const void* g16, int ld16, const float* t, int ldt, void* dt, int lddt,
-                 float* gsum, int ldgs, int rows, int C, int dtype, void* stream);
+int tmae_lrp_bwd(const float* g32, int ld32, const float* g32b, int ld32b, const void* g16, int ld16, const float* t,
+                 int ldt, void* dt, int lddt, float* gsum, int ldgs, int rows, int C, int dtype, void* stream);
 /* strided 2-D copy, element size esz (2 or 4 bytes) */
 int tmae_copy2d(const void* src, int lds, void* dst, int ldd, int rows, int cols, int esz, void* stream);
 /* GaussianConditional likelihood + quantize_ste backward for one slice (MCM.py:767-776) */

@@ -172,7 +172,7 @@ SIGNATURES = {
     "tmae_layernorm_bwd": [P, P, P, P, P, P, I, I, I, I, I, I, F, P, LL, P, P, P, I, P],
     "tmae_unshuffle_bwd": [P, I, I, P, I, P, I, I, I, I, I, P],
     "tmae_gelu_bwd": [P, I, P, P, LL, I, P],
-    "tmae_lrp_bwd": [P, I, P, I, P, I, P, I, P, I, I, I, I, P],
+    "tmae_lrp_bwd": [P, I, P, I, P, I, P, I, P, I, P, I, I, I, I, P],
     "tmae_copy2d": [P, I, P, I, I, I, I, P],
     "tmae_gc_bwd": [P, I, I, P, P, I, P, I, P, P, I, P, I, P, P, I, I, I, I, I, P],
     "tmae_eb_bwd": [ctypes.POINTER(EBParams), P, P, P, P, P, I, I, I, ctypes.POINTER(EBParams), I, P],

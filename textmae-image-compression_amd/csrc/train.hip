@@ -939,28 +939,31 @@ extern "C" int tmae_gelu_bwd(const void* dy, int dy_f32, const void* pre, void* 
 // gsum = g (f32, optional: the y_hat_pre gradient the GaussianConditional backward continues with)
 template <typename T>
 __global__ void __launch_bounds__(256)
-lrp_bwd_kernel(const float* __restrict__ g32, int ld32, const T* __restrict__ g16, int ld16, const float* __restrict__ t,
-               int ldt, T* __restrict__ dt, int lddt, float* __restrict__ gsum, int ldgs, int rows, int C) {
+lrp_bwd_kernel(const float* __restrict__ g32, int ld32, const float* __restrict__ g32b, int ld32b,
+               const T* __restrict__ g16, int ld16, const float* __restrict__ t, int ldt, T* __restrict__ dt, int lddt,
+               float* __restrict__ gsum, int ldgs, int rows, int C) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= rows * C) return;
   const int m = i / C, c = i - m * C;
   float g = g32 ? g32[(size_t)m * ld32 + c] : 0.0f;
+  if (g32b) g += g32b[(size_t)m * ld32b + c];
   if (g16) g += (float)g16[(size_t)m * ld16 + c];
   const float th = tanhf(t[(size_t)m * ldt + c]);
   dt[(size_t)m * lddt + c] = to_out<T>(g * 0.5f * (1.0f - th * th));
   if (gsum) gsum[(size_t)m * ldgs + c] = g;
 }
 
-extern "C" int tmae_lrp_bwd(const float* g32, int ld32, const void* g16, int ld16, const float* t, int ldt, void* dt,
-                            int lddt, float* gsum, int ldgs, int rows, int C, int dtype, void* stream) {
+extern "C" int tmae_lrp_bwd(const float* g32, int ld32, const float* g32b, int ld32b, const void* g16, int ld16,
+                            const float* t, int ldt, void* dt, int lddt, float* gsum, int ldgs, int rows, int C,
+                            int dtype, void* stream) {
   if (rows * C == 0) return TMAE_OK;
   const dim3 grid(ceil_div(rows * C, 256));
   if (dtype == TMAE_BF16)
-    hipLaunchKernelGGL(lrp_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, g32, ld32, (const bf16*)g16, ld16,
-                       t, ldt, (bf16*)dt, lddt, gsum, ldgs, rows, C);
+    hipLaunchKernelGGL(lrp_bwd_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, g32, ld32, g32b, ld32b,
+                       (const bf16*)g16, ld16, t, ldt, (bf16*)dt, lddt, gsum, ldgs, rows, C);
   else
-    hipLaunchKernelGGL(lrp_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, g32, ld32, (const float*)g16,
-                       ld16, t, ldt, (float*)dt, lddt, gsum, ldgs, rows, C);
+    hipLaunchKernelGGL(lrp_bwd_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, g32, ld32, g32b, ld32b,
+                       (const float*)g16, ld16, t, ldt, (float*)dt, lddt, gsum, ldgs, rows, C);
   TMAE_LAUNCH_CHECK("tmae_lrp_bwd");
 }
 

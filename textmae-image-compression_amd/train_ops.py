@@ -189,9 +189,10 @@ def unshuffle_bwd(dy, ldy, pre, ldp, out, n, H, W, C4, dtype, dy_f32):
               _stream())
 
 
-def lrp_bwd(t, ldt, dt, lddt, rows, C, dtype, g32=None, ld32=0, g16=None, ld16=0, gsum=None, ldgs=0):
-    _lib.call("tmae_lrp_bwd", _p(g32), ld32, _p(g16), ld16, _p(t), ldt, _p(dt), lddt, _p(gsum), ldgs, rows, C,
-              dtype_code(dtype), _stream())
+def lrp_bwd(t, ldt, dt, lddt, rows, C, dtype, g32=None, ld32=0, g16=None, ld16=0, gsum=None, ldgs=0, g32b=None,
+            ld32b=0):
+    _lib.call("tmae_lrp_bwd", _p(g32), ld32, _p(g32b), ld32b, _p(g16), ld16, _p(t), ldt, _p(dt), lddt, _p(gsum), ldgs,
+              rows, C, dtype_code(dtype), _stream())
 
 
 def gc_bwd(y, ldy, yoff, mu, sigma, ld_ms, noise, Mtot, glik, gyp, ldg, dy, lddy, dmu, dsigma, ldd, n, HW, sw, dtype):
