@@ -155,6 +155,26 @@ __device__ __forceinline__ uint4 pack8_bf16(f32x4 a, f32x4 b) {
 
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
 // blocks b and b+8 land on one XCD; give each XCD a contiguous run of logical tiles.
+// Sum over the 64 lanes of a wave, every lane getting the total, without the LDS crossbar: DPP quad permutes
+// (xor 1, xor 2) and row mirrors (8, 16 lanes) leave each 16-lane row's sum in all its lanes, then the four row
+// sums are read lane-uniformly (v_readlane) and added as (r0 + r1) + (r2 + r3).  Every lane ends with the same
+// bits.  (A __shfl_xor butterfly is six ds_bpermute round trips through the LDS unit.)  Whole wave active.
+#define TMAE_DPP_ADD(v, ctrl)                                                                                      \
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), ctrl, 0xF, 0xF, true))
+__device__ __forceinline__ float wave_allsum(float v) {
+  TMAE_DPP_ADD(v, 0xB1);   // quad_perm [1,0,3,2]: xor 1
+  TMAE_DPP_ADD(v, 0x4E);   // quad_perm [2,3,0,1]: xor 2
+  TMAE_DPP_ADD(v, 0x141);  // row_half_mirror: the other quad of each 8
+  TMAE_DPP_ADD(v, 0x140);  // row_mirror: the other 8 of each 16
+  const int b = __builtin_bit_cast(int, v);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48));
+  return (r0 + r1) + (r2 + r3);
+}
+#undef TMAE_DPP_ADD
+
 __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   const int q = nwg >> 3, r = nwg & 7, x = b & 7;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);

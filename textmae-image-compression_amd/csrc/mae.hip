@@ -54,11 +54,7 @@ extern "C" int tmae_mae_masking(const float* noise, int64_t* ids_shuffle, int64_
 #define MAE_LOSS_BLOCKS 512
 #define MAE_VPL 32  // values per lane held in registers: p*p*c <= 64 * 32 = 2048
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+__device__ __forceinline__ float wave_sum(float v) { return wave_allsum(v); }
 
 // offset of value lane + 64 k of a patchified row (e = (py * P + px) * C + c) from the patch's top-left pixel in
 // plane 0 of its image (NCHW), -1 past the row: the same for every row, so worked out once per thread (the two

@@ -40,10 +40,15 @@ layernorm_kernel(const float* __restrict__ x, const float* __restrict__ gamma, c
 #pragma unroll
     for (int i = 0; i < VPL; ++i) s[k] += (v[k][i][0] + v[k][i][1]) + (v[k][i][2] + v[k][i][3]);
   }
+#ifdef TMAE_LN_SHFL  // A/B builds: the ds_bpermute butterfly
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
     for (int k = 0; k < RPW; ++k) s[k] += __shfl_xor(s[k], o);
+#else
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) s[k] = wave_allsum(s[k]);
+#endif
 #pragma unroll
   for (int k = 0; k < RPW; ++k) {
     const float mean = s[k] / (float)D;
@@ -61,10 +66,15 @@ layernorm_kernel(const float* __restrict__ x, const float* __restrict__ gamma, c
       }
     }
   }
+#ifdef TMAE_LN_SHFL
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
     for (int k = 0; k < RPW; ++k) q[k] += __shfl_xor(q[k], o);
+#else
+#pragma unroll
+  for (int k = 0; k < RPW; ++k) q[k] = wave_allsum(q[k]);
+#endif
 #pragma unroll
   for (int k = 0; k < RPW; ++k) {
     const int r = r0 + k;

@@ -730,8 +730,7 @@ layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamm
     float s = 0.0f;
 #pragma unroll
     for (int i = 0; i < VPL; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    s = wave_allsum(s);
     const float mean = s / (float)D;
     float q = 0.0f;
 #pragma unroll
@@ -745,8 +744,7 @@ layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamm
         }
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    q = wave_allsum(q);
     const float rstd = 1.0f / sqrtf(q / (float)D + eps);
     float sa = 0.0f, sb = 0.0f;
 #pragma unroll
@@ -765,11 +763,8 @@ layernorm_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gamm
         }
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      sa += __shfl_xor(sa, o);
-      sb += __shfl_xor(sb, o);
-    }
+    sa = wave_allsum(sa);
+    sb = wave_allsum(sb);
     sa /= (float)D;
     sb /= (float)D;
 #pragma unroll
@@ -1180,9 +1175,7 @@ eb_bwd_kernel(tmae_eb_params p, const float* __restrict__ z, const float* __rest
   __shared__ float red[EB_NG][4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int k = 0; k < EB_NG; ++k) {
-    float v = gf[k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const float v = wave_allsum(gf[k]);
     if (lane == 0) red[k][wv] = v;
   }
   __syncthreads();
