@@ -391,6 +391,8 @@ typedef struct tmae_wgrad_args {
   float* work; long long work_elems;
   float* out; long long o_base, o_sm, o_sc, o_st; int o_cp; int accumulate;
   float* bias_out; int bias_accumulate;
+  int slot_div;  /* split-K sized for 1 / slot_div of the CU slots (0 or 1: the whole chip); a weight gradient on
+                    a side stream shares the chip, and fewer splits write and reduce fewer partial slabs */
 } tmae_wgrad_args;
 int tmae_wgrad(const tmae_wgrad_args* args, int dtype, void* stream);
 long long tmae_wgrad_workspace(int M, int N, int K, int dtype);

@@ -49,6 +49,7 @@ class WgradArgs(ctypes.Structure):
         ("work", P), ("work_elems", LL),
         ("out", P), ("o_base", LL), ("o_sm", LL), ("o_sc", LL), ("o_st", LL), ("o_cp", I), ("accumulate", I),
         ("bias_out", P), ("bias_accumulate", I),
+        ("slot_div", I),
     ]
 
 

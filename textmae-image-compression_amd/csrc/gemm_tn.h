@@ -302,7 +302,7 @@ gemm_tn_f32_kernel(AS as, BS bs, EpiSplitWs epi, int M, int N, int K, int kchunk
 // ------------------------------------------------------------------ launch
 struct TnPlan { int bn, bm, nw, splits, kchunk; };
 
-static inline TnPlan tn_plan(int M, int N, int K, bool bf) {
+static inline TnPlan tn_plan(int M, int N, int K, bool bf, int slot_div = 1) {
   TnPlan p;
   if (!bf) {
     p.bn = 64; p.bm = 64; p.nw = 4;
@@ -313,7 +313,7 @@ static inline TnPlan tn_plan(int M, int N, int K, bool bf) {
     else { p.bn = 128; p.bm = 128; p.nw = 4; }
   }
   const int tiles = ceil_div(N, p.bn) * ceil_div(M, p.bm);
-  const int slots = p.nw == 8 ? 256 : 512;
+  const int slots = (p.nw == 8 ? 256 : 512) / std::max(1, slot_div);
   const int kmin = bf ? 256 : 128;
   // splits: as many as fit ONE round of the slots (floor): with the ceiling, tiles * splits overshot the
   // 256 slots of the 8-wave tile on every encoder weight gradient (qkv 270, fc1 / fc2 288, proj 261

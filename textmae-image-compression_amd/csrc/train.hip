@@ -55,7 +55,7 @@ static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
                a.M, a.N, e);
   TMAE_REQUIRE(a.a_G > 0 && a.o_cp > 0, "tmae_wgrad: bad row group / column period");
   const bool bf = sizeof(T) == 2;
-  const TnPlan p = tn_plan(a.M, a.N, a.K, bf);
+  const TnPlan p = tn_plan(a.M, a.N, a.K, bf, a.slot_div);
   const long long slabs = (long long)p.splits * a.M * a.N;
   TMAE_REQUIRE(slabs + (long long)p.splits * a.M <= a.work_elems, "tmae_wgrad: workspace too small (%lld < %lld)",
                a.work_elems, slabs + (long long)p.splits * a.M);

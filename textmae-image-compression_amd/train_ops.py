@@ -73,7 +73,8 @@ def patch_gather(imgs, ids, out, keep, patch, dtype):
 
 # ------------------------------------------------------------------------------------- gradients
 def wgrad(a, b, M, N, K, out, dtype, lda=None, ldb=None, a_remap=(None, 0, 0), b_remap=(None, 0, 0), conv=None,
-          layout="dense", cin_total=None, ci_off=0, accumulate=False, bias=None, bias_accumulate=False, ws_slot=1):
+          layout="dense", cin_total=None, ci_off=0, accumulate=False, bias=None, bias_accumulate=False, ws_slot=1,
+          slot_div=1):
     """out <- sum_k A(k, m) B(k, n) in the parameter's layout; bias (optional) <- sum_k A(k, m), the bias
     gradient of the layer whose output gradient A is, formed by the same GEMM.
     layout: "dense" (out [M][N]), "dense_t" (out [N][M]: ConvTranspose2d 1x1 weights), "conv"
@@ -115,6 +116,7 @@ def wgrad(a, b, M, N, K, out, dtype, lda=None, ldb=None, a_remap=(None, 0, 0), b
     args.accumulate = int(accumulate)
     args.bias_out = _p(bias)
     args.bias_accumulate = int(bias_accumulate)
+    args.slot_div = int(slot_div)
     _lib.call("tmae_wgrad", ctypes.byref(args), code, _stream())
     return out
 
