@@ -261,8 +261,8 @@ class _VitTrainBase:
         the serial data-gradient chain.  Queued here and enqueued by _wg_flush behind ONE fork per group (a stack,
         a block): a captured graph pays a cross-queue dependency per fork.  `a` (this layer's output gradient, a
         fresh tensor of the chain) is kept alive until the join; every other operand is a saved activation."""
-        if self._side is None:
-            return T.wgrad(a, *args, **kw)
+        if self._side is None:  # same split plan as the side stream's, so both modes sum in the same order
+            return T.wgrad(a, *args, slot_div=_SIDE_SLOT_DIV, **kw)
         self._queued.append((a, args, kw))
 
     def _wg_flush(self, last=False):
