@@ -915,7 +915,8 @@ class TrainExec(_VitTrainBase):
         # stream beside the mean stack, its support-channel gradients in their own buffer (dSUP2, added where slice
         # j's lrp backward reads column block j), so the two data-gradient chains never touch the same accumulator.
         # Not under graph capture: HIP's graph executor ran that topology 3.4 ms slower per step (31.4 -> 34.8 ms;
-        # eager 31.9 -> 31.4), so a captured step keeps both stacks on the compute stream (same sums either way).
+        # eager 31.9 -> 31.4), and 6.5 ms slower with joins only where slices <= 5 read dSUP2 (31.9 -> 38.4), so a
+        # captured step keeps both stacks on the compute stream (same sums either way).
         conc = self._side is not None and not torch.cuda.is_current_stream_capturing()
         if conc and "_scale_stream" not in self.__dict__:
             self._scale_stream = torch.cuda.Stream(device=self.device)
@@ -931,7 +932,7 @@ class TrainExec(_VitTrainBase):
             cin_m = M + sw * k
             rec = self.sl[i]
             gs_i = GS.data_ptr() + i * sw * 4
-            if joined is not None:  # slice i + 1's scale stack wrote dSUP2's block i
+            if joined is not None and i < ms:  # later slices' scale stacks wrote dSUP2's block i (read below)
                 main.wait_event(joined)
                 joined = None
             # y_hat = y_hat_pre + 0.5 tanh(t)   (MCM.py:782-783)
