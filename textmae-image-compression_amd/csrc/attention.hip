@@ -522,13 +522,17 @@ mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, c
   constexpr int LDR = AttnBwd<DH>::LDR;
   constexpr int NDT = (DH + 31) / 32;
   constexpr int CPR = DH / 8;
+  // dh 32: a wave's 32 keys of K ([32][32] bf16, the size of its dS scratch) are staged through that scratch once
+  // and held in registers as the dQ product's B fragments, so K takes no LDS of its own (88 -> 74 KB at 224
+  // tokens: two workgroups per CU)
+  constexpr bool KREG = DH == 32;
   static_assert(DH % 32 == 0, "one-pass backward: whole 32-wide head-dim tiles");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int nw = Tpad / 32, LDQ = Tpad + 4;
   bf16* Qs = reinterpret_cast<bf16*>(smem);
   bf16* Gs = Qs + (size_t)Tpad * LDR;
-  bf16* Ks = Gs + (size_t)Tpad * LDR;
-  bf16* dSs = Ks + (size_t)Tpad * LDR;                     // nw x [32 keys][32 queries]
+  bf16* Ks = Gs + (size_t)Tpad * LDR;                      // (not allocated when KREG)
+  bf16* dSs = Ks + (KREG ? 0 : (size_t)Tpad * LDR);        // nw x [32 keys][32 queries]
   float* dQs = reinterpret_cast<float*>(dSs + (size_t)nw * 1024);  // [DH][LDQ]
   float* lse_s = dQs + (size_t)DH * LDQ;
   float* dl_s = lse_s + Tpad;
@@ -541,12 +545,13 @@ mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, c
   const int tid = threadIdx.x, nthr = blockDim.x;
 
   attn_stage2<DH, LDR>(Qs, base, ld, Gs, gbase, D, Tn, Tpad, tid, nthr);  // Q, dO
-  for (int i = tid; i < Tpad * CPR; i += nthr) {                          // K
-    const int r = i / CPR, c = i - r * CPR;
-    uint4 x = uint4{0, 0, 0, 0};
-    if (r < Tn) x = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + D + c * 8);
-    *reinterpret_cast<uint4*>(Ks + (size_t)r * LDR + c * 8) = x;
-  }
+  if constexpr (!KREG)
+    for (int i = tid; i < Tpad * CPR; i += nthr) {                          // K
+      const int r = i / CPR, c = i - r * CPR;
+      uint4 x = uint4{0, 0, 0, 0};
+      if (r < Tn) x = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + D + c * 8);
+      *reinterpret_cast<uint4*>(Ks + (size_t)r * LDR + c * 8) = x;
+    }
   for (int i = tid; i < DH * LDQ / 4; i += nthr) reinterpret_cast<f32x4*>(dQs)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int r = tid; r < Tpad; r += nthr) {  // delta = rowsum(dO * O), lse
     float d = 0.0f, l = 0.0f;
@@ -587,6 +592,22 @@ mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, c
   const bool kmask = ragged && wave == nw - 1;  // wave-uniform: this wave holds the keys past Tn
   const bool kok = kb + col < Tn;
   bf16* dsw = dSs + (size_t)wave * 1024;
+  bf16x8 kt[2];  // KREG: this wave's K rows as the dQ product's B fragments (k = key, 16 per fragment)
+  if constexpr (KREG) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {  // 32 rows x 4 chunks of 8, two per lane
+      const int i = lane + 64 * j, r = i >> 2, c = i & 3;
+      uint4 x = uint4{0, 0, 0, 0};
+      if (kb + r < Tn) x = *reinterpret_cast<const uint4*>(base + (size_t)(kb + r) * ld + D + c * 8);
+      *reinterpret_cast<uint4*>(dsw + (size_t)r * LDR + c * 8) = x;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) kt[s2] = attn_tr_frag<LDR>(dsw, 16 * s2, 0, lane);
+    // the first dS store below follows these reads in the wave's in-order LDS queue
+  }
 
   for (int it = 0; it < nw; ++it) {
     int qt = wave + it;
@@ -652,8 +673,8 @@ mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, c
       const bf16x8 a = attn_tr_frag<32>(dsw, 16 * s, 0, lane);
 #pragma unroll
       for (int t = 0; t < NDT; ++t)
-        dQp[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, attn_tr_frag<LDR>(Ks, kb + 16 * s, 32 * t, lane), dQp[t],
-                                                         0, 0, 0);
+        dQp[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+            a, KREG ? kt[s] : attn_tr_frag<LDR>(Ks, kb + 16 * s, 32 * t, lane), dQp[t], 0, 0, 0);
     }
     // lane holds dQ[q = qt*32 + (r&3) + 8(r>>2) + 4hh][d = 32t + col]: four 16-B runs of the [d][q] accumulator
 #pragma unroll
@@ -827,8 +848,9 @@ static int mha_bwd_launch(const void* qkv, const void* o, const void* dout, cons
   if (dtype == TMAE_BF16) {
     TMAE_REQUIRE(DH == 32 || nthr <= 512, "tmae_mha_bwd: sequence length %d too long for head dim %d", Tn, DH);
     constexpr int LDR = AttnBwd<DH>::LDR;
-    const size_t lds1 = (size_t)3 * Tpad * LDR * 2 + (size_t)(Tpad / 32) * 2048 + (size_t)DH * (Tpad + 4) * 4 +
-                        (size_t)2 * Tpad * 4;
+    // Q, dO (and K unless dh 32 holds it in registers), dS scratch, dQ, lse / delta
+    const size_t lds1 = (size_t)(DH == 32 ? 2 : 3) * Tpad * LDR * 2 + (size_t)(Tpad / 32) * 2048 +
+                        (size_t)DH * (Tpad + 4) * 4 + (size_t)2 * Tpad * 4;
     if (AttnBwdOnePass<DH>::value && lds1 <= 160 * 1024) {
       hipLaunchKernelGGL((mha_bwd1_bf16_kernel<AttnBwdOnePass<DH>::value ? DH : 32>), dim3(B * H), dim3(nthr), lds1,
                          st, (const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, (bf16*)dqkv, Tn, H, Tpad, scale);
