@@ -415,6 +415,9 @@ typedef struct tmae_conv_dgrad_args {
   const void* wd;
   void* out; int out_f32, ldo; const void* pre; int ldp;
   float* acc[3]; int ld_acc[3]; int lim[3];
+  /* nb = 2: a second problem of the same shape (no routes) at element offsets s_dy / s_wd / s_out / s_pre from
+     the first's dy / wd / out / pre -- the mean and scale stacks of one slice as one launch (0 or 1: one) */
+  int nb; long long s_dy, s_wd, s_out, s_pre;
 } tmae_conv_dgrad_args;
 int tmae_conv_dgrad(const tmae_conv_dgrad_args* args, int dtype, void* stream);
 

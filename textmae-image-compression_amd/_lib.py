@@ -61,6 +61,7 @@ class ConvDgradArgs(ctypes.Structure):
         ("wd", P),
         ("out", P), ("out_f32", I), ("ldo", I), ("pre", P), ("ldp", I),
         ("acc", P * 3), ("ld_acc", I * 3), ("lim", I * 3),
+        ("nb", I), ("s_dy", LL), ("s_wd", LL), ("s_out", LL), ("s_pre", LL),
     ]
 
 

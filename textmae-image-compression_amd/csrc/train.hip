@@ -209,7 +209,11 @@ template <typename OT, typename PT> struct EpiDgrad {
   int ldp;
   float* acc;
   int lda;
-  __device__ void batch(int, int) {}
+  long long s_out = 0, s_pre = 0;  // element offsets of problem b1's out / pre (batched launches)
+  __device__ void batch(int b1, int) {
+    out += b1 * s_out;
+    if (pre) pre += b1 * s_pre;
+  }
   __device__ void operator()(int m, int n, f32x4 v) const {
     if (pre) {
       const f32x4 p = load4f(pre + (size_t)m * ldp + n);
@@ -297,8 +301,9 @@ template <typename T> struct ConvTSrc {
   const T* dy;
   int ldy, Cout, H, W, Ho, Wo, stride, rows, K;
   float inv_cout;
+  long long s_dy;  // element offset of problem b1's dy (batched launches)
   struct Row { int b; int iy; int ix; bool ok; };
-  __device__ void batch(int, int) {}
+  __device__ void batch(int b1, int) { dy += b1 * s_dy; }
   __device__ Row row(int m) const {
     if (m >= rows) return {0, 0, 0, false};
     const int hw = H * W;
@@ -339,8 +344,11 @@ static int conv_dgrad_t(const tmae_conv_dgrad_args& a, hipStream_t st) {
   xs.dy = (const T*)a.dy; xs.ldy = a.ldy; xs.Cout = a.cout; xs.H = a.H; xs.W = a.W; xs.stride = a.stride;
   xs.Ho = (a.H + 2 - 3) / a.stride + 1; xs.Wo = (a.W + 2 - 3) / a.stride + 1;
   xs.rows = a.n * a.H * a.W; xs.K = 9 * a.cout; xs.inv_cout = 1.0f / (float)a.cout;
+  xs.s_dy = a.s_dy;
   const int M = xs.rows, K = xs.K, N = a.cin;
+  const int nb = a.nb > 1 ? a.nb : 1;
   const char* nm = "tmae_conv_dgrad";
+  TMAE_REQUIRE(nb <= 2 && (nb == 1 || !a.acc[0]), "tmae_conv_dgrad: batched (nb = %d) launches take no routes", nb);
   if (a.acc[0]) {
     TMAE_REQUIRE(a.lim[0] % 8 == 0 && a.lim[1] % 8 == 0 && a.lim[2] == a.cin && a.lim[0] <= a.lim[1] &&
                      a.lim[1] <= a.lim[2],
@@ -352,11 +360,11 @@ static int conv_dgrad_t(const tmae_conv_dgrad_args& a, hipStream_t st) {
     return launch_gemm<true, T>(nm, (const T*)a.wd, 0, 0, N, K, xs, r, M, 1, 1, st);
   }
   if (a.out_f32) {
-    EpiDgrad<float, T> g{(float*)a.out, a.ldo, (const T*)a.pre, a.ldp, nullptr, 0};
-    return launch_gemm<true, T>(nm, (const T*)a.wd, 0, 0, N, K, xs, g, M, 1, 1, st);
+    EpiDgrad<float, T> g{(float*)a.out, a.ldo, (const T*)a.pre, a.ldp, nullptr, 0, a.s_out, a.s_pre};
+    return launch_gemm<true, T>(nm, (const T*)a.wd, a.s_wd, 0, N, K, xs, g, M, nb, 1, st);
   }
-  EpiDgrad<T, T> g{(T*)a.out, a.ldo, (const T*)a.pre, a.ldp, nullptr, 0};
-  return launch_gemm<true, T>(nm, (const T*)a.wd, 0, 0, N, K, xs, g, M, 1, 1, st);
+  EpiDgrad<T, T> g{(T*)a.out, a.ldo, (const T*)a.pre, a.ldp, nullptr, 0, a.s_out, a.s_pre};
+  return launch_gemm<true, T>(nm, (const T*)a.wd, a.s_wd, 0, N, K, xs, g, M, nb, 1, st);
 }
 
 extern "C" int tmae_conv_dgrad(const tmae_conv_dgrad_args* a, int dtype, void* stream) {

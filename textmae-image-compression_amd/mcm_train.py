@@ -916,7 +916,8 @@ class TrainExec(_VitTrainBase):
         # j's lrp backward reads column block j), so the two data-gradient chains never touch the same accumulator.
         # Not under graph capture: HIP's graph executor ran that topology 3.4 ms slower per step (31.4 -> 34.8 ms;
         # eager 31.9 -> 31.4), and 6.5 ms slower with joins only where slices <= 5 read dSUP2 (31.9 -> 38.4), so a
-        # captured step keeps both stacks on the compute stream (same sums either way).
+        # captured step keeps both stacks on the compute stream, their layers 4..1 as 2-problem data-gradient
+        # launches (_stack_bwd_pair; same sums either way).
         conc = self._side is not None and not torch.cuda.is_current_stream_capturing()
         if conc and "_scale_stream" not in self.__dict__:
             self._scale_stream = torch.cuda.Stream(device=self.device)
@@ -948,26 +949,53 @@ class TrainExec(_VitTrainBase):
             scale_args = (_convs(m.cc_transform_scale[i]), rec["scale"], dSG,
                           (self.LS, M, 2 * M, lms + M * esz if k else None, sw * k, 2 * M),
                           [(dLS, M, M), (dSUP2, M, sw * k)])
-            if conc:
-                fork = torch.cuda.Event()
-                fork.record(main)
-            # the mean stack first: in a captured graph the fork node's first child stays on the compute queue
-            self._stack_bwd(_convs(m.cc_transform_mean[i]), rec["mean"], dMU, (self.LMS, cin_m, 2 * M, None, 0, 0),
-                            [(dLM, M, M), (dSUP, M, sw * k)])
-            if conc:
-                ss = self._scale_stream
-                ss.wait_event(fork)
-                with torch.cuda.stream(ss):
-                    self._stack_bwd(*scale_args)
-                joined = torch.cuda.Event()
-                joined.record(ss)
-                self._keep.append(dSG)  # read on the scale stream; freed after the backward's join
-            else:
+            mean_args = (_convs(m.cc_transform_mean[i]), rec["mean"], dMU, (self.LMS, cin_m, 2 * M, None, 0, 0),
+                         [(dLM, M, M), (dSUP, M, sw * k)])
+            if not conc:
+                # one stream: layers 4..1 of both stacks as 2-problem data-gradient launches
+                self._stack_bwd_pair(mean_args, scale_args)
+                self._ready(_convs(m.cc_transform_scale[i])[0].bias)
+                continue
+            # eager: the scale stack on its own stream, the mean stack first on the compute stream
+            fork = torch.cuda.Event()
+            fork.record(main)
+            self._stack_bwd(*mean_args)
+            ss = self._scale_stream
+            ss.wait_event(fork)
+            with torch.cuda.stream(ss):
                 self._stack_bwd(*scale_args)
+            joined = torch.cuda.Event()
+            joined.record(ss)
+            self._keep.append(dSG)  # read on the scale stream; freed after the backward's join
             self._ready(_convs(m.cc_transform_scale[i])[0].bias)
         if joined is not None:
             main.wait_event(joined)
         return DY, dLM, dLS
+
+    def _stack_bwd_pair(self, a, b):
+        """_stack_bwd of two stacks with the same layer shapes (a slice's mean and scale stacks): the data gradients
+        of layers 4..1 run as one 2-problem launch each (the same per-problem sums as two launches); the weight
+        gradients and the first layers (their own input splits / routes) one by one, a's before b's"""
+        dt, W, G, B, g, Mp = self.dtype, self.w, self.grad, self.batch, self.g, self.Mp
+        (ca, sa, da, fa, ra), (cb, sb, db, fb, rb) = a, b
+        for l in range(4, 0, -1):
+            for c, saved, d in ((ca[l], sa, da), (cb[l], sb, db)):
+                cin = c.in_channels
+                self._wg(d, saved[l - 1][0], c.out_channels, 9 * cin, Mp, G(c.weight), dt,
+                         conv=dict(c1=cin, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
+            cin, cout = ca[l].in_channels, ca[l].out_channels
+            assert (cb[l].in_channels, cb[l].out_channels) == (cin, cout)
+            dxa, dxb = self._e(Mp, cin), self._e(Mp, cin)
+            T.conv_dgrad(da, W.conv_dg(ca[l].weight), B, g, g, 1, cout, cin, dt, out=dxa, pre=sa[l - 1][1],
+                         second=(db, W.conv_dg(cb[l].weight), dxb, sb[l - 1][1]))
+            da, db = dxa, dxb
+        for c, d, first, routes in ((ca[0], da, fa, ra), (cb[0], db, fb, rb)):
+            x1, c1, ld1, x2, c2, ld2 = first
+            cin, cout = c1 + c2, c.out_channels
+            self._wg(d, x1, cout, 9 * cin, Mp, G(c.weight), dt, ldb=ld1,
+                     conv=dict(x2=x2, c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
+            T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
+        self._wg_flush()
 
     def _stack_bwd(self, convs, saved, dtop, first, routes):
         dt, W, G, B, g, Mp = self.dtype, self.w, self.grad, self.batch, self.g, self.Mp

@@ -131,10 +131,25 @@ def dgrad_linear(dy, wt, M, N, K, dtype, out=None, pre=None, acc32=None, ldy=Non
 
 
 def conv_dgrad(dy, wd, n, H, W, stride, cout, cin, dtype, out=None, pre=None, ldy=None, ldo=None, ldp=None,
-               routes=None, out_f32=None):
+               routes=None, out_f32=None, second=None):
     """dx [n*H*W][cin] of a 3x3 conv from dy [n*Ho*Wo][cout]; wd = weight as [cin][3][3][cout] (dtype).
-    routes: [(acc_f32, ld, ncols), ...] (<= 3, f32 +=, consecutive input-channel ranges)"""
+    routes: [(acc_f32, ld, ncols), ...] (<= 3, f32 +=, consecutive input-channel ranges).
+    second = (dy2, wd2, out2, pre2): a second problem of the same shape and layout in the same launch (no routes)"""
     a = ConvDgradArgs()
+    if second is not None:
+        def off(t2, t1, what):
+            if t2.dtype != t1.dtype:
+                raise ValueError(f"conv_dgrad second problem: {what} dtype {t2.dtype} != {t1.dtype}")
+            d = t2.data_ptr() - t1.data_ptr()
+            if d % t1.element_size():
+                raise ValueError(f"conv_dgrad second problem: {what} offset {d} B is not whole elements")
+            return d // t1.element_size()
+        dy2, wd2, out2, pre2 = second
+        a.nb = 2
+        a.s_dy, a.s_wd, a.s_out = off(dy2, dy, "dy"), off(wd2, wd, "wd"), off(out2, out, "out")
+        if (pre is None) != (pre2 is None):
+            raise ValueError("conv_dgrad second problem: pre given for one problem only")
+        a.s_pre = off(pre2, pre, "pre") if pre is not None else 0
     a.dy, a.ldy = _p(dy), ldy if ldy is not None else cout
     a.n, a.H, a.W, a.stride, a.cout, a.cin = n, H, W, stride, cout, cin
     a.wd = _p(wd)
