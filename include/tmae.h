@@ -371,7 +371,8 @@ int tmae_mha_fwd_lse(const void* qkv, void* out, float* lse, int B, int T, int H
 /* timm Attention backward: dqkv [B*T][3*H*dh] (dtype) from qkv, o (forward output), dO, lse */
 int tmae_mha_bwd(const void* qkv, const void* o, const void* dout, const float* lse, void* dqkv, int B, int T, int H,
                  int dh, float scale, int dtype, void* stream);
-/* kept-patch im2col for the patch-embed weight gradient: out[n*keep][C*P*P] (dtype) */
+/* kept-patch im2col for the patch-embed weight gradient: out[n*keep][Kw] (dtype), Kw = C*P*P rounded up to a
+ * multiple of 8 with a zero tail (patch 14: 588 -> 592) */
 int tmae_patch_gather(const float* imgs, const int64_t* ids_shuffle, void* out, int n, int C, int H, int W, int patch,
                       int L, int keep, int dtype, void* stream);
 

@@ -40,27 +40,52 @@ def run_train(m, imgs, noise, ratio):
     return loss.detach(), pred.detach(), mask, {n: p.grad for n, p in m.named_parameters() if p.requires_grad}
 
 
-def tiny(tmae, norm_pix, dec_dim=32):
+def tiny(tmae, norm_pix, dec_dim=32, patch=16):
     torch.manual_seed(21)
-    return tmae.MaskedAutoencoderViT(img_size=64, patch_size=16, in_chans=3, embed_dim=64, depth=2, num_heads=2,
+    return tmae.MaskedAutoencoderViT(img_size=4 * patch, patch_size=patch, in_chans=3, embed_dim=64, depth=2, num_heads=2,
                                      decoder_embed_dim=dec_dim, decoder_depth=2, decoder_num_heads=1, mlp_ratio=4.0,
                                      norm_layer=partial(torch.nn.LayerNorm, eps=1e-6), norm_pix_loss=norm_pix).to(DEV)
 
 
-@pytest.mark.parametrize("norm_pix", [False, True])
-def test_tiny_grads_f32_vs_oracle(tmae, norm_pix):
-    m = tiny(tmae, norm_pix)
-    imgs = torch.randn(3, 3, 64, 64, generator=torch.Generator().manual_seed(22))
+@pytest.mark.parametrize("norm_pix,patch", [(False, 16), (True, 16), (False, 14), (True, 14)])
+def test_tiny_grads_f32_vs_oracle(tmae, norm_pix, patch):
+    """patch 14 (588-value patch rows, zero-padded to 592 in the gathered patches, the weight copy and the weight
+    gradient) as well as 16"""
+    m = tiny(tmae, norm_pix, patch=patch)
+    imgs = torch.randn(3, 3, 4 * patch, 4 * patch, generator=torch.Generator().manual_seed(22))
     noise = torch.rand(3, 16, generator=torch.Generator().manual_seed(23))
-    rl, rp, rm, rg = oracle_grads(m, imgs, noise, 0.75, 16, 2, 1, 2, 2, norm_pix)
+    rl, rp, rm, rg = oracle_grads(m, imgs, noise, 0.75, patch, 2, 1, 2, 2, norm_pix)
     loss, pred, mask, grads = run_train(m, imgs, noise, 0.75)
     assert torch.equal(mask.cpu(), rm)
-    check(f"maxrel:mae_train_tiny_pred_np{int(norm_pix)}", maxrel(pred, rp), 1e-3)
+    sfx = f"np{int(norm_pix)}" + ("" if patch == 16 else f"_p{patch}")
+    check(f"maxrel:mae_train_tiny_pred_{sfx}", maxrel(pred, rp), 1e-3)
     assert abs(float(loss) - float(rl)) <= 1e-3 * abs(float(rl))
     worst = 0.0
     for name, g in grads.items():
         worst = max(worst, maxrel(g, rg[name]))
-    check(f"maxrel:mae_train_tiny_grads_np{int(norm_pix)}", worst, 1e-3)
+    check(f"maxrel:mae_train_tiny_grads_{sfx}", worst, 1e-3)
+
+
+def test_huge_patch14_grads_f32_vs_oracle(tmae):
+    """mae_vit_huge_patch14_dec512d8b (models_mae.py:239-244: patch 14, 588-value patch rows; 1280 wide, 16 heads
+    of 80, 32 blocks) trains: batch 1, f32, loss / pred / every parameter gradient against autograd through the
+    oracle"""
+    torch.manual_seed(29)
+    m = tmae.mae_vit_huge_patch14_dec512d8b().to(DEV)
+    imgs = torch.randn(1, 3, 224, 224, generator=torch.Generator().manual_seed(30))
+    noise = torch.rand(1, 256, generator=torch.Generator().manual_seed(31))
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    rl, rp, rm, rg = oracle_grads(m, imgs, noise, 0.75, 14, 16, 16, 32, 8, False)
+    loss, pred, mask, grads = run_train(m, imgs, noise, 0.75)
+    assert torch.equal(mask.cpu(), rm)
+    check("maxrel:mae_train_huge_pred", maxrel(pred, rp), 1e-3)
+    assert abs(float(loss) - float(rl)) <= 1e-3 * abs(float(rl))
+    worst, name_w = 0.0, None
+    for name, g in grads.items():
+        r = maxrel(g, rg[name])
+        if r > worst:
+            worst, name_w = r, name
+    check("maxrel:mae_train_huge_grads", worst, 1e-3, note=name_w)
 
 
 def test_vitb_grads_f32_vs_oracle(tmae):

@@ -486,6 +486,43 @@ def test_graphed_train_step_bitwise(dt):
         assert torch.equal(m1(imgs, scores)["x_hat"], m2(imgs, scores)["x_hat"])
 
 
+def test_graphed_train_step_lr_change_before_first_replay():
+    """a learning-rate change BEFORE the first replay re-captures at once: the launch tables the first capture
+    built (relayout, Adam) were never filled (their copy nodes had not run), so the second capture and an eager
+    forward in between must build their own.  Losses and weights stay bitwise equal to eager steps with the same
+    schedule (a reused, unfilled table would launch on garbage pointers)."""
+    from textmae_amd import engine
+    from textmae_amd.optim import configure_optimizers
+    from textmae_amd.rd_loss import RateDistortionLoss
+
+    crit = RateDistortionLoss(lmbda=1e-2)
+    m1, cfg = _model(SMALL, 25, torch.bfloat16)
+    m2, _ = _model(SMALL, 25, torch.bfloat16)
+    m1.distortion = m2.distortion = "ssim+l1"
+    batches = [_inputs(cfg, 2, 700 + i) for i in range(3)]
+    o1 = configure_optimizers(m1, lr=3e-3, aux_lr=1e-3, fused=True)
+    o2 = configure_optimizers(m2, lr=3e-3, aux_lr=1e-3, fused=True)
+    cu = lambda b: tuple(t.cuda() for t in b)  # noqa: E731
+    imgs, scores, zn, yn = cu(batches[0])
+    g = engine.GraphedTrainStep(m1, crit, *o1, imgs, scores, clip_max_norm=1.0, warmup=1, noise=(zn, yn))
+    # an eager training forward between the capture and the first replay (tables of the capture unfilled)
+    out = m1(imgs, scores, noise=(zn, yn))
+    del out
+    for grp in o1[0].param_groups:
+        grp["lr"] = 1e-3
+    la = []
+    for b in batches[1:]:
+        imgs, scores, zn, yn = cu(b)
+        la.append(float(g(imgs, scores, noise=(zn, yn))["loss"]))
+    lb = _train_steps(m2, *o2, batches[:1], crit)
+    for grp in o2[0].param_groups:
+        grp["lr"] = 1e-3
+    lb = _train_steps(m2, *o2, batches[1:], crit)
+    assert la == lb, (la, lb)
+    for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(p, q), n
+
+
 def test_graphed_train_step_device_noise_and_lr_change():
     """without injected noise the graph draws training noise from torch's graph-safe generator (a fresh draw
     per replay); changing the learning rate re-captures the step"""

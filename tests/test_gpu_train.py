@@ -282,21 +282,33 @@ def test_mha_bwd(T, T_, H, dh, dt):
 
 
 # ------------------------------------------------------------------------------ distortion
-@pytest.mark.parametrize("hw", [(40, 37), (100, 150), (256, 256)])
+@pytest.mark.parametrize("hw", [(40, 37), (100, 150), (256, 256), (100, 152, "offset")])
 def test_distortion_fwd_bwd_vs_oracle(hw):
-    """one tile, several 32 x 64 tiles with ragged edges, the bench's 256^2 (tiled kernels, distortion.hip)"""
+    """one tile, several 32 x 64 tiles with ragged edges, the bench's 256^2 (tiled kernels, distortion.hip); and
+    inputs that are contiguous views 4 B past a 16-B boundary (a sliced batch), which must take the per-element
+    path of the backward's 16-B accesses"""
     from oracle.thirdparty import ssim as ssim_ref
     from textmae_amd.distortion import ssim_l1_loss
 
-    H, W = hw
+    H, W = hw[:2]
+    offset = len(hw) > 2
     x = torch.rand(2, 3, H, W, generator=torch.Generator().manual_seed(30))
     y = (x + 0.1 * _rnd(2, 3, H, W, seed=31)).clamp(0, 1)
     xr = x.double().requires_grad_(True)
     s_ref = 1 - ssim_ref(xr, y.double(), data_range=1)
     l_ref = F.l1_loss(xr, y.double())
     (0.7 * s_ref + 1.3 * l_ref).backward()
-    xg = x.cuda().requires_grad_(True)
-    s, l = ssim_l1_loss(xg, y.cuda())
+    if offset:  # 1-float offset views: base pointers 4 B past a 16-B boundary
+        xb = torch.empty(x.numel() + 1, device="cuda")
+        yb = torch.empty(y.numel() + 1, device="cuda")
+        xg, yd = xb[1:].view_as(x), yb[1:].view_as(y)
+        xg.copy_(x)
+        yd.copy_(y)
+        assert xg.data_ptr() % 16 and yd.data_ptr() % 16
+        xg.requires_grad_(True)
+    else:
+        xg, yd = x.cuda().requires_grad_(True), y.cuda()
+    s, l = ssim_l1_loss(xg, yd)
     (0.7 * s + 1.3 * l).backward()
     torch.cuda.synchronize()
     assert abs(s.item() - s_ref.item()) < 1e-5 and abs(l.item() - l_ref.item()) < 1e-6

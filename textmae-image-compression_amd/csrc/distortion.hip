@@ -275,6 +275,7 @@ ssim_bwd_tile_kernel(const float* __restrict__ d, const float* __restrict__ x, c
   }
   __syncthreads();
   const float gs = gout ? gout[0] : 0.0f, gl = gout ? gout[1] : 0.0f;
+  const bool aligned16 = (((size_t)x | (size_t)y | (size_t)gx) & 15) == 0;
   // transposed horizontal pass + the combination with x and y: one item = one row x 4 consecutive columns, the
   // 14 v values of each map read as 16-B LDS loads, x / y / dx as 16-B global accesses
   for (int e = t; e < SS_TH * (SS_TW / 4); e += SS_NT) {
@@ -291,7 +292,8 @@ ssim_bwd_tile_kernel(const float* __restrict__ d, const float* __restrict__ x, c
         for (int u = 0; u < 4; ++u) vv[m][4 * q4 + u] = v4[u];
       }
     const size_t o = ((size_t)p * H + r) * W + c;
-    const bool full = c + 4 <= W && (W & 3) == 0;
+    // 16-B accesses only on 16-B aligned bases: an offset view (a sliced batch) takes the per-element path
+    const bool full = c + 4 <= W && (W & 3) == 0 && aligned16;
     f32x4 xv4, yv4, gv4;
     if (full) {
       xv4 = *reinterpret_cast<const f32x4*>(x + o);

@@ -1285,16 +1285,21 @@ extern "C" int tmae_bpp_bwd(const float* lik, const float* gout, float* dlik, lo
 
 // ================================================================== encoder / decoder glue
 // kept-patch im2col (timm PatchEmbed conv16/s16 over the kept patches, MCM.py:615 + gather 585-586):
-// out[b*keep + k][(c*P + py)*P + px] = img[b][c][hy*P + py][hx*P + px], patch ids_shuffle[b][k]
+// out[b*keep + k][(c*P + py)*P + px] = img[b][c][hy*P + py][hx*P + px], patch ids_shuffle[b][k]; rows are Kw =
+// C*P*P rounded up to a multiple of 8 values, the tail zero (ViT-H's patch 14: 588 -> 592, the GEMMs' 16-B rows)
 template <typename T>
 __global__ void __launch_bounds__(256)
 patch_gather_kernel(const float* __restrict__ img, const int64_t* __restrict__ ids, T* __restrict__ out, int n, int C,
                     int H, int W, int P, int L, int keep) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  const int KP = C * P * P;
-  if (i >= (long long)n * keep * KP) return;
-  const int col = (int)(i % KP);
-  const int row = (int)(i / KP);
+  const int KP = C * P * P, Kw = (KP + 7) / 8 * 8;
+  if (i >= (long long)n * keep * Kw) return;
+  const int col = (int)(i % Kw);
+  if (col >= KP) {
+    out[i] = to_out<T>(0.0f);
+    return;
+  }
+  const int row = (int)(i / Kw);
   const int b = row / keep, k = row - b * keep;
   const int p = (int)ids[(size_t)b * L + k];
   const int G = W / P;
@@ -1327,7 +1332,7 @@ patch_gather8_kernel(const float* __restrict__ img, const int64_t* __restrict__ 
 
 extern "C" int tmae_patch_gather(const float* imgs, const int64_t* ids_shuffle, void* out, int n, int C, int H, int W,
                                  int patch, int L, int keep, int dtype, void* stream) {
-  const long long total = (long long)n * keep * C * patch * patch;
+  const long long total = (long long)n * keep * ((C * patch * patch + 7) / 8 * 8);  // padded rows (Kw values)
   if (total == 0) return TMAE_OK;
   if (patch % 8 == 0 && W % 4 == 0 && ((size_t)imgs & 15) == 0 && total / 8 < (1ll << 31)) {
     const dim3 g8((unsigned)((total / 8 + 255) / 256));

@@ -120,7 +120,7 @@ class GraphedTrainStep:
         from .optim import bump_versions, reserve_capture_staging
 
         bump_versions(self.params)
-        reserve_capture_staging()
+        self._staging = reserve_capture_staging()  # the graph's copy nodes read it at every replay
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             out = self._step()
@@ -186,7 +186,7 @@ class GraphedMAEStep:
         cur.wait_stream(side)
         self.optimizer.zero_grad()
         bump_versions(self.params)
-        reserve_capture_staging()
+        self._staging = reserve_capture_staging()  # the graph's copy nodes read it at every replay
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             loss = self._step()

@@ -21,7 +21,7 @@ import torch
 
 from . import ops
 from . import train_ops as T
-from .mcm_train import _VitTrainBase, _Weights, _block_params
+from .mcm_train import _SIDE_SLOT_DIV, _VitTrainBase, _Weights, _block_params
 
 
 class MAETrainExec(_VitTrainBase):
@@ -33,9 +33,16 @@ class MAETrainExec(_VitTrainBase):
         self.P = m.patch_embed.patch_size[0]
         self.L = m.patch_embed.num_patches
         C = m.patch_embed.proj.in_channels
-        if (C * self.P * self.P) % 8:
-            raise ValueError(f"MAE training: patch rows of {C * self.P * self.P} values (a multiple of 8 needed by "
-                             "the weight-gradient GEMM; patch 14 trains nowhere in this build)")
+        # patch rows of KP = C*P*P values; the GEMMs take 16-B rows, so ViT-H's patch 14 (588 values) runs on rows
+        # padded to Kw = 592: zero-tailed gathered patches, a zero-tailed copy of the weight, and a [E][Kw] weight
+        # gradient of which the first KP columns are the parameter's
+        self.KP = C * self.P * self.P
+        self.Kw = -(-self.KP // 8) * 8
+        if self.KP != self.Kw and dtype != torch.float32:
+            # decoder_pred's 588 outputs are the K of its data gradient and the rows of its weight gradient, which
+            # the bf16 GEMMs take in 16-B rows only; the f32 path (4-value rows) trains patch 14
+            raise ValueError(f"MAE training with {self.KP}-value patch rows runs in compute_dtype=torch.float32 only")
+        self._wpe_pad = self._gpe_pad = None
         self._layout()
 
     def _grad_order(self):
@@ -70,8 +77,14 @@ class MAETrainExec(_VitTrainBase):
         pw = m.patch_embed.proj.weight
         pos = m.pos_embed.detach()
         tok = torch.empty((B * Te, E), dtype=torch.float32, device=self.device)
-        self.patches = T.patch_gather(imgs, shuf, self._e(B * keep, pw[0].numel()), keep, P, dt)
-        ops.patch_embed(imgs, shuf, W.nt(pw), m.patch_embed.proj.bias.detach(), pos, tok, keep, P, dt,
+        self.patches = T.patch_gather(imgs, shuf, self._e(B * keep, self.Kw), keep, P, dt)
+        wpe = W.nt(pw)
+        if self.Kw != self.KP:  # patch 14: the weight rows zero-tailed to Kw like the patches
+            if self._wpe_pad is None:
+                self._wpe_pad = self._z(E, self.Kw, dtype=dt)
+            self._wpe_pad[:, :self.KP].copy_(wpe)
+            wpe = self._wpe_pad
+        ops.patch_embed(imgs, shuf, wpe, m.patch_embed.proj.bias.detach(), pos, tok, keep, P, dt,
                         patches=self.patches)
         ops.cls_rows(tok, m.cls_token.detach(), pos, B, Te, E)
         self.enc = []
@@ -143,7 +156,14 @@ class MAETrainExec(_VitTrainBase):
             self._ready(_block_params(blk)[-1])
         # ---- patch embed (kept patches) + cls token
         pw = m.patch_embed.proj.weight
-        self._wg(dt_op, self.patches, E, pw[0].numel(), B * keep, G(pw), dt, lda=E, a_remap=(keep, Te, 1))
+        if self.Kw == self.KP:
+            self._wg(dt_op, self.patches, E, self.KP, B * keep, G(pw), dt, lda=E, a_remap=(keep, Te, 1))
+        else:  # patch 14: [E][Kw] into a scratch (same split plan as the side stream's), its first KP columns kept
+            if self._gpe_pad is None:
+                self._gpe_pad = torch.empty((E, self.Kw), dtype=torch.float32, device=self.device)
+            T.wgrad(dt_op, self.patches, E, self.Kw, B * keep, self._gpe_pad, dt, lda=E, a_remap=(keep, Te, 1),
+                    slot_div=_SIDE_SLOT_DIV)
+            T.relayout(self._gpe_pad, G(pw).view(E, self.KP), (E, self.KP), (self.Kw, 1))
         T.colsum(dt_tok, B * keep, E, G(m.patch_embed.proj.bias), row_group=keep, group_stride=Te, row_offset=1)
         T.colsum(dt_tok, B, E, G(m.cls_token).view(-1), row_group=1, group_stride=Te, row_offset=0)
         self._ready(m.cls_token)

@@ -25,7 +25,7 @@ import torch.nn as nn
 from . import _lib, ops
 from . import train_ops as T
 from .ops import ACT_GELU, ACT_NONE
-from .optim import device_table
+from .optim import device_table, table_usable
 
 
 # side-stream weight gradients size their split-K for half the chip's CU slots (the data-gradient chain holds the
@@ -126,13 +126,13 @@ class _Weights:
         if not rows:
             return
         key = tuple(ptrs)
-        if self._tab is None or self._tab[0] != key:
+        if self._tab is None or self._tab[0] != key or not table_usable(self._tab[3]):
             dev = stale[0][1].device
             owner = [t for t in range(len(rows)) for _ in range(rows[t + 1][11] - rows[t][11] if t + 1 < len(rows)
                                                                 else chunk - rows[t][11])]
             flat = [v for r in rows for v in r] + owner  # the rows, then each chunk's row (tmae.h)
-            tab, pinned = device_table(flat, dev)
-            self._tab = (key, tab, chunk, pinned)
+            tab, epoch = device_table(flat, dev)
+            self._tab = (key, tab, chunk, epoch)
         _lib.call("tmae_relayout_multi", self._tab[1].data_ptr(), len(rows), self._tab[2],
                   torch.cuda.current_stream().cuda_stream)
 

@@ -117,25 +117,28 @@ _PATCH_WORK: dict = {}
 
 def patch_embed(imgs, ids_shuffle, w, b, pos, tokens, keep, patch, dtype, patches=None):
     """kept-patch embedding (+ pos) into tokens rows 1..keep of every image.  Patches whose rows are whole 16-B
-    chunks (P % 8 == 0) are gathered first (into `patches` [n*keep][C*P*P] of dtype when given -- the training
-    forward keeps them for the weight gradient -- else a cached workspace) and projected by the LDS-DMA GEMM;
-    others (ViT-H's patch 14) are gathered value by value inside the GEMM."""
+    chunks (P % 8 == 0), and every patch size when `patches` is given, are gathered first (into `patches`
+    [n*keep][Kw] of dtype -- the training forward keeps them for the weight gradient -- else a cached workspace;
+    Kw = C*P*P rounded up to 8, zero tail) and projected by the LDS-DMA GEMM; otherwise (ViT-H's patch 14 at
+    inference) they are gathered value by value inside the GEMM."""
     n, C, H, W = imgs.shape
     D = w.shape[0]
     L = ids_shuffle.shape[1]
     if w.dim() != 2 or w.shape[1] != -(-C * patch * patch // 8) * 8 or not w.is_contiguous():
         raise ValueError(f"patch_embed: weight {tuple(w.shape)} must be contiguous [D][C*P*P rounded up to 8]")
-    KP = C * patch * patch
-    if patch % 8 == 0:
+    Kw = w.shape[1]  # C*P*P rounded up to 8 (the gathered rows' zero tail: patch 14, 588 -> 592)
+    if patch % 8 == 0 or patches is not None:
         if patches is None:
-            key = (imgs.device, dtype, n * keep * KP)
+            key = (imgs.device, dtype, n * keep * Kw)
             patches = _PATCH_WORK.get(key)
             if patches is None:
-                patches = _PATCH_WORK[key] = torch.empty((n * keep, KP), dtype=dtype, device=imgs.device)
+                patches = _PATCH_WORK[key] = torch.empty((n * keep, Kw), dtype=dtype, device=imgs.device)
             _lib.call("tmae_patch_gather", _need(imgs, torch.float32, "imgs").data_ptr(), ids_shuffle.data_ptr(),
                       patches.data_ptr(), n, C, H, W, patch, L, keep, dtype_code(dtype), _stream())
+        elif tuple(patches.shape) != (n * keep, Kw):
+            raise ValueError(f"patch_embed: gathered patches {tuple(patches.shape)} must be [{n * keep}][{Kw}]")
         _lib.call("tmae_patch_embed_gathered", patches.data_ptr(), ids_shuffle.data_ptr(), w.data_ptr(), b.data_ptr(),
-                  pos.data_ptr(), tokens.data_ptr(), n, KP, D, L, keep, dtype_code(dtype), _stream())
+                  pos.data_ptr(), tokens.data_ptr(), n, Kw, D, L, keep, dtype_code(dtype), _stream())
         return tokens
     _lib.call("tmae_patch_embed_fwd", _need(imgs, torch.float32, "imgs").data_ptr(), ids_shuffle.data_ptr(),
               w.data_ptr(), b.data_ptr(), pos.data_ptr(), tokens.data_ptr(), n, C, H, W, patch, D, L, keep,

@@ -36,16 +36,20 @@ class _PinnedArena:
     """pinned host staging for launch tables built while a stream is being captured: neither a pageable H2D copy
     nor a pinned allocation may happen during a capture, so the pinned buffer is reserved before it
     (``reserve_capture_staging``) and handed out by a bump allocator.  The graph's copy nodes read their slices
-    at every replay, so nothing is reused until the next ``reserve_capture_staging`` (a new capture)."""
+    at every replay, so every capture gets a FRESH buffer (never a reset of the previous one, which a graph still
+    alive would read) and the graph's owner keeps it alive.  ``epoch`` counts the captures: a table built inside
+    capture e is filled only by that graph's copy node, so it is valid inside capture e and nowhere else
+    (``table_usable``)."""
 
     def __init__(self):
-        self.buf, self.off = None, 0
+        self.buf, self.off, self.epoch = None, 0, 0
 
     def reserve(self, nbytes):
         n = (int(nbytes) + 7) // 8
-        if self.buf is None or self.buf.numel() < n:
-            self.buf = torch.empty(n, dtype=torch.int64).pin_memory()
+        self.buf = torch.empty(n, dtype=torch.int64).pin_memory()
         self.off = 0
+        self.epoch += 1
+        return self.buf
 
     def take(self, n):
         if self.buf is None or self.off + n > self.buf.numel():
@@ -60,20 +64,31 @@ _ARENA = _PinnedArena()
 
 
 def reserve_capture_staging(nbytes=8 << 20):
-    """reserve (and reset) the pinned staging that launch tables built inside a graph capture are copied from"""
-    _ARENA.reserve(nbytes)
+    """a fresh pinned staging buffer for the launch tables built inside the NEXT graph capture; the caller (the
+    graph's owner) keeps the returned buffer alive as long as the graph, whose copy nodes read it at every replay"""
+    return _ARENA.reserve(nbytes)
 
 
 def device_table(rows, device):
     """int64 rows -> a device table for a multi-tensor launch.  While a stream is being captured into a HIP graph
     the copy comes from the pinned staging arena (a pageable H2D copy or a pinned allocation cannot be captured);
-    returns (table, pinned slice or None)."""
+    returns (table, capture epoch or None).  Pass the epoch to ``table_usable`` before reusing a cached table."""
     h = torch.tensor(rows, dtype=torch.int64).reshape(-1)
     if device.type == "cuda" and torch.cuda.is_current_stream_capturing():
         p = _ARENA.take(h.numel())
         p.copy_(h)
-        return p.to(device, non_blocking=True), p
+        return p.to(device, non_blocking=True), _ARENA.epoch
     return h.to(device), None
+
+
+def table_usable(epoch):
+    """may a cached launch table built at capture ``epoch`` (None: built eagerly) be launched from now?  An eager
+    table is filled when it is made.  A table built inside a capture holds its rows only once that graph's copy
+    node has run, so it is reused only inside the same capture: not eagerly (before the first replay it is still
+    uninitialised) and not in a later capture (a re-capture before any replay would read the same garbage)."""
+    if epoch is None:
+        return True
+    return torch.cuda.is_current_stream_capturing() and epoch == _ARENA.epoch
 
 
 class FusedAdam(torch.optim.Optimizer):
@@ -116,7 +131,7 @@ class FusedAdam(torch.optim.Optimizer):
     def _table(self, gi, live):
         key = tuple((p.data_ptr(), p.grad.data_ptr()) for p in live)
         hit = self._tabs[gi]
-        if hit is not None and hit[0] == key:
+        if hit is not None and hit[0] == key and table_usable(hit[3]):
             return hit[1], hit[2]
         mb, vb, steps, off = self._flat[gi]
         rows, chunk = [], 0
@@ -126,8 +141,8 @@ class FusedAdam(torch.optim.Optimizer):
             rows.append([p.data_ptr(), p.grad.data_ptr(), mb[o:].data_ptr(), vb[o:].data_ptr(), n, chunk,
                          steps[i:].data_ptr()])
             chunk += (n + CHUNK - 1) // CHUNK
-        tab, pinned = device_table(rows, mb.device)
-        self._tabs[gi] = (key, tab, chunk, pinned)
+        tab, epoch = device_table(rows, mb.device)
+        self._tabs[gi] = (key, tab, chunk, epoch)
         return tab, chunk
 
     @torch.no_grad()
