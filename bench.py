@@ -160,6 +160,7 @@ class LaunchTimer:
         self.conv_bytes = 0
         self.stack_bytes = 0
         self.hbm_bytes = {}  # memory-bound families: algorithmic HBM bytes per forward
+        self.gemm_bytes = [0, 0]  # dense-source GEMM launches (PMC family "token_gemm"): [launches, algorithmic bytes]
 
     def _hbm(self, fam, nbytes):
         self.hbm_bytes[fam] = self.hbm_bytes.get(fam, 0) + nbytes
@@ -169,6 +170,16 @@ class LaunchTimer:
         if name == "tmae_linear_fwd" or name == "tmae_linear_residual_fwd":
             M, N, K = (a[13], a[14], a[15]) if name == "tmae_linear_fwd" else (a[6], a[7], a[8])
             fl = 2.0 * M * N * K
+            # algorithmic bytes: A + W + bias + the output (f32 residual: read and written)
+            if name == "tmae_linear_fwd":
+                es = 2 if a[17] == 1 else 4
+                nb = M * K * (4 if a[1] else es) + N * K * es + N * 4 + M * N * (4 if a[9] else es) + \
+                    (M * N * 4 if a[11] else 0)
+            else:
+                es = 2 if a[9] == 1 else 4
+                nb = M * K * es + N * K * es + N * 4 + 2 * M * N * 4
+            self.gemm_bytes[0] += 1
+            self.gemm_bytes[1] += nb
             for side, D, T in (("enc", E, Te), ("dec", Dd, Td)):
                 if M == B * T:
                     if name == "tmae_linear_fwd" and (N, K) == (3 * D, D):
@@ -221,12 +232,22 @@ class LaunchTimer:
         if name == "tmae_patch_embed_fwd":
             return "patch_embed", 2.0 * a[6] * a[13] * a[11] * a[7] * a[10] * a[10]
         if name == "tmae_patch_embed_gathered":  # (patches, ids, w, b, pos, tok, n, Kw, D, L, keep, ...)
+            es = 2 if a[11] == 1 else 4
+            self.gemm_bytes[0] += 1
+            self.gemm_bytes[1] += a[6] * a[10] * a[7] * es + a[8] * a[7] * es + a[6] * a[10] * a[8] * 4
             return "patch_embed", 2.0 * a[6] * a[10] * a[8] * a[7]
         if name == "tmae_patch_gather":  # the kept-patch gather in front of it (time only)
             return "patch_embed", 0.0
-        if name == "tmae_decoder_embed_fwd":
+        if name == "tmae_decoder_embed_fwd":  # (x, x_f32, w, b, pos, ids, out, n, ntok, L, Din, D, dtype, ...)
+            es = 2 if a[12] == 1 else 4
+            self.gemm_bytes[0] += 1
+            self.gemm_bytes[1] += a[7] * a[8] * a[10] * (4 if a[1] else es) + a[11] * a[10] * es + a[7] * a[8] * a[11] * 4
             return "dec_embed", 2.0 * a[7] * a[8] * a[10] * a[11]
-        if name in ("tmae_decoder_pred_fwd", "tmae_decoder_pred_cp_fwd"):
+        if name in ("tmae_decoder_pred_fwd", "tmae_decoder_pred_cp_fwd"):  # (x, w, b, imgs, n, L, Din, C, H, W, P, dt)
+            es = 2 if a[11] == 1 else 4
+            npix = a[7] * a[10] * a[10]
+            self.gemm_bytes[0] += 1
+            self.gemm_bytes[1] += a[4] * a[5] * a[6] * es + npix * a[6] * es + a[4] * a[5] * npix * 4
             return "dec_pred", 2.0 * a[4] * a[5] * a[6] * a[7] * a[10] * a[10]
         if name == "tmae_layernorm_fwd":
             rows, D = a[4], a[5]
@@ -262,14 +283,26 @@ class LaunchTimer:
                     "stride": c.stride, "out_f32": bool(c.y_f32), "addend": bool(c.addend)}
         return {}
 
-    def run(self, fn):
+    def run(self, fn, live=("lic_stack",)):
+        """classify every library launch of fn() (one eager forward); the launches of the `live` families are also
+        bracketed by HIP events on the stream they are launched on, so their duration INSIDE the forward (beside the
+        side stream's kernels, as in the graphed step) is measured live (self.live_us: family -> mean us)"""
         orig = self._lib.call
         calls = self.calls
+        evs = {}
 
         def record(name, *args):
             fam, fl = self.classify(name, args)
             calls.append((fam, fl, name, args))
-            return orig(name, *args)
+            if fam not in live:
+                return orig(name, *args)
+            st_ = torch.cuda.ExternalStream(args[-1]) if args[-1] else torch.cuda.current_stream()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(st_)
+            r = orig(name, *args)
+            b.record(st_)
+            evs.setdefault(fam, []).append((a, b))
+            return r
 
         self._lib.call = record
         try:
@@ -277,6 +310,7 @@ class LaunchTimer:
         finally:
             self._lib.call = orig
         torch.cuda.synchronize()
+        self.live_us = {f: 1e3 * sum(a.elapsed_time(b) for a, b in v) / len(v) for f, v in evs.items()}
         fams = {}
         for fam, fl, name, args in calls:
             t = fams.setdefault(fam, [[], 0.0])
@@ -336,13 +370,24 @@ def roofline_report(m, imgs, scores, batch, dump=None):
                            "latent-channel partial sums)",
             "lic_stack": " (lic_stack_kernel: whole cc_transform_mean/scale stacks, each serial slice's mean "
                          "stack chained into its lrp_transform stack, one workgroup per problem x image)"}
+    flops_launch = d["gflop"] * 1e9 / max(d["launches"], 1)
     roof = {"kernel": dom + desc.get(dom, ""),
             "bound": "mfma", "achieved": d["achieved"], "peak": PEAK_BF16 / 1e12, "unit": "TFLOP/s",
             "frac": d["frac"], "traffic": None, "launches_per_step": d["launches"],
             "avg_launch_us": round(d["time_us"] / max(d["launches"], 1), 2),
-            "flops_per_launch": round(d["gflop"] * 1e9 / max(d["launches"], 1)),
+            "flops_per_launch": round(flops_launch),
             "share_of_kernel_time": round(fam[dom][1] / total_t, 4),
             "kernel_time_per_step_us": round(total_t * 1e6, 1)}
+    if dom in getattr(lt, "live_us", {}):
+        # headline = the kernel as it runs INSIDE the forward (HIP events around each of its launches on its stream,
+        # beside the side stream's partial sums); the back-to-back replay of the family alone stays as a second figure
+        us = lt.live_us[dom]
+        roof.update({"achieved": round(flops_launch / (us * 1e-6) / 1e12, 2),
+                     "frac": round(flops_launch / (us * 1e-6) / PEAK_BF16, 4), "avg_launch_us": round(us, 2),
+                     "measured": "in the forward: HIP events around each launch on its stream (eager forward, the "
+                                 "partial sums running beside it on the side stream)",
+                     "achieved_replay": d["achieved"], "frac_replay": d["frac"],
+                     "avg_launch_us_replay": round(d["time_us"] / max(d["launches"], 1), 2)})
     for side in ("enc", "dec"):
         # qkv GEMM + attention core + proj; the bf16 forward runs qkv + core as ONE fused launch ({side}_qkv_attn)
         roof[f"attention_block_{side}"] = stat([f"{side}_qkv", f"{side}_attn_core", f"{side}_qkv_attn", f"{side}_proj"])
@@ -389,6 +434,15 @@ def roofline_report(m, imgs, scores, batch, dump=None):
             e["frac_in_forward"] = round(nbytes / max(n, 1) / (fwd[f]["avg_launch_us"] * 1e-6) / PEAK_HBM, 4)
         hbm[f] = e
     roof["hbm_bound"] = hbm
+    # the dense-source GEMMs (token GEMMs, patch / decoder embed, decoder pred, the 1x1 LIC GEMMs: PMC family
+    # "token_gemm") -- counter bytes against their algorithmic A + W + output bytes, per forward
+    if "token_gemm" in fam_pmc:
+        tg = fam_pmc["token_gemm"]
+        pf = tg.get("hbm_bytes_per_fwd", tg["hbm_bytes_per_launch"] * tg.get("launches_per_fwd", 1))
+        roof["token_gemm_traffic"] = {
+            "launches_per_fwd_classified": lt.gemm_bytes[0], "launches_per_fwd_pmc": tg.get("launches_per_fwd"),
+            "algorithmic_bytes_per_fwd": int(lt.gemm_bytes[1]), "traffic_bytes_per_fwd": int(pf),
+            "traffic_over_algorithmic": round(pf / max(lt.gemm_bytes[1], 1), 3), "source": pmc_src}
     if pmc_src or trace_src:
         roof["sources"] = {"pmc": pmc_src, "trace": trace_src}
     return roof
@@ -415,9 +469,10 @@ def train_bench(model, args, rank, world, dev, barrier):
     """the reference training step (utils/engine.py:72-91): forward, RateDistortionLoss (SSIM + L1 +
     bpp; VGG needs a weight download), aux loss, backward (HIP reverse pass; for world > 1 the RCCL
     gradient all-reduce runs inside it, bucketed), clip_grad_norm_(1.0), Adam, aux backward, aux Adam.
-    One rank: the whole step is one HIP graph (engine.GraphedTrainStep), replayed per batch; the crop
-    kernel runs before each replay.  More ranks: eager steps with the overlap timing of the gradient
-    all-reduce (parallel.GradSync.last_timing)."""
+    The whole step is one HIP graph (engine.GraphedTrainStep), replayed per batch, at any world size over RCCL:
+    the bucketed gradient all-reduces are captured inside the backward; the crop kernel runs before each
+    replay.  The all-reduce overlap numbers (parallel.GradSync.last_timing) come from one eager step of the same
+    kernels after the timed replays.  A gloo group (CPU rehearsals) runs eager steps."""
     from textmae_amd import engine
     from textmae_amd.data import SyntheticCropSet
     from textmae_amd.optim import configure_optimizers
@@ -436,7 +491,7 @@ def train_bench(model, args, rank, world, dev, barrier):
     data = SyntheticCropSet(dev, seed=2000, rank=rank, crop=args.img,
                             patch_size=model.encoder_embed.patch_size[0]).plan(args.train_warmup + args.train_steps + 1,
                                                                                args.train_batch)
-    use_graph = world == 1 and not args.no_graph
+    use_graph = not args.no_graph and (world == 1 or args.backend == "nccl")
     if use_graph:
         imgs, scores = data.next()
         gstep = engine.GraphedTrainStep(model, crit, opt, aux_opt, imgs, scores, clip_max_norm=1.0, warmup=1)
@@ -475,9 +530,13 @@ def train_bench(model, args, rank, world, dev, barrier):
         del gstep
         torch.cuda.empty_cache()
     if world > 1:
+        if use_graph:  # the captured step records no events: one eager step of the same kernels for the overlap
+            imgs, scores = data.next()
+            engine.train_step(model, crit, imgs, scores, opt, aux_opt, clip_max_norm=1.0)
         t = model.grad_sync.last_timing()
         if t:
-            rec["grad_allreduce"] = dict(t, source="last timed step, this rank's compute-stream events")
+            rec["grad_allreduce"] = dict(t, source="this rank's compute-stream events, " + (
+                "one eager step after the timed graph replays" if use_graph else "last timed step"))
     elif args.dp_rehearsal:
         rec["grad_allreduce"] = dp_rehearsal(model, crit, opt, aux_opt, data, dev)
     return rec
@@ -504,8 +563,29 @@ def dp_rehearsal(model, crit, opt, aux_opt, data, dev, steps=3):
             engine.train_step(model, crit, imgs, scores, opt, aux_opt, clip_max_norm=1.0)
         torch.cuda.synchronize()
         t = sync.last_timing()
-        return dict(t or {}, launched_total=sync.launched, world=1,
-                    source="one-rank nccl (RCCL) group, always_collective, last of 3 eager steps")
+        rec = dict(t or {}, launched_total=sync.launched, world=1,
+                   source="one-rank nccl (RCCL) group, always_collective, last of 3 eager steps")
+        # the DP step as the N > 1 ranks run it: ONE HIP graph holding the bucketed RCCL all-reduces
+        n0 = sync.launched
+        imgs, scores = data.next()
+        gstep = engine.GraphedTrainStep(model, crit, opt, aux_opt, imgs, scores, clip_max_norm=1.0, warmup=1)
+        captured = sync.launched - n0
+        for _ in range(2):
+            gstep(*data.next())
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            gstep(*data.next())
+        host = time.perf_counter() - t0
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        rec["graphed"] = {"hip_graph": True, "ms_per_step": round(el / steps * 1e3, 3),
+                          "host_enqueue_ms_per_step": round(host / steps * 1e3, 3),
+                          "collectives_in_graph": captured - (len(sync._bounds) - 1),  # minus the warm-up step's
+                          "buckets_issued_in_backward": sync.launched_in_backward,
+                          "source": f"GraphedTrainStep with the one-rank RCCL GradSync, {steps} replays"}
+        del gstep
+        return rec
     except Exception as e:  # the rehearsal must never cost the bench line
         return {"error": f"{type(e).__name__}: {e}"[:300]}
     finally:

@@ -180,6 +180,15 @@ typedef struct tmae_lic_stack_args {
   void* cy2; int cldy2;
   /* chain operands of problem (0, b2) are offset by b2 * these element strides (batched slices) */
   long long cs_x1, cs_yv, cs_src, cs_add, cs_y, cs_y2, cs_w[TMAE_LIC_STACK_MAXL], cs_b[TMAE_LIC_STACK_MAXL];
+  /* training forward (what the HIP backward reads, mcm_train.py): for every layer l but the last, the
+   * pre-activation (acc + bias [+ addend]) sv_pre[l] and the GELU output sv_act[l], bf16 [n*G*G][cout[l]] per
+   * problem at element strides sv_s[l]; an lrp stack's last layer also writes sv_t = the pre-tanh value, f32
+   * [n*G*G][cout] at strides sv_t_s.  Chain: the lrp pass's csv_pre / csv_act / csv_t, problem (0, b2) offset by
+   * b2 * cs_sv[l] / cs_t.  NULL: not written (inference). */
+  void* sv_pre[TMAE_LIC_STACK_MAXL]; void* sv_act[TMAE_LIC_STACK_MAXL]; long long sv_s[TMAE_LIC_STACK_MAXL][2];
+  float* sv_t; long long sv_t_s[2];
+  void* csv_pre[TMAE_LIC_STACK_MAXL]; void* csv_act[TMAE_LIC_STACK_MAXL]; long long cs_sv[TMAE_LIC_STACK_MAXL];
+  float* csv_t; long long cs_t;
 } tmae_lic_stack_args;
 #define TMAE_LIC_STACK_CHAIN 1
 int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream);
@@ -416,8 +425,9 @@ typedef struct tmae_conv_dgrad_args {
   const void* wd;
   void* out; int out_f32, ldo; const void* pre; int ldp;
   float* acc[3]; int ld_acc[3]; int lim[3];
-  /* nb = 2: a second problem of the same shape (no routes) at element offsets s_dy / s_wd / s_out / s_pre from
-     the first's dy / wd / out / pre -- the mean and scale stacks of one slice as one launch (0 or 1: one) */
+  /* nb > 1: nb problems of the same shape (no routes), problem j at element offsets j * s_dy / s_wd / s_out / s_pre
+     from the first's dy / wd / out / pre -- the mean and scale stacks of one slice (nb = 2), or of the batched
+     slices 6..11 (nb = 12) as one launch (0 or 1: one problem) */
   int nb; long long s_dy, s_wd, s_out, s_pre;
 } tmae_conv_dgrad_args;
 int tmae_conv_dgrad(const tmae_conv_dgrad_args* args, int dtype, void* stream);
@@ -428,7 +438,9 @@ int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0, int d1, in
 /* every relayout of a table in one launch: table[t] = {src, dst, dst_dtype | mode << 8, d1, d2, d3, s0, s1, s2, s3,
  * total, first_chunk} (int64, device memory), first_chunk = the chunks of the tensors before t (mode 0, a plain
  * or strided copy: ceil(total / 32768); mode 1, a 2-D transpose: 64 x 64 tiles; mode 2, a per-row transpose:
- * rows), then nchunks more int64: the row t of every chunk (ntensors * 12 + nchunks values in all) */
+ * rows; mode 3, a 3x3 conv weight [d1 = Cout][d2 = Cin][3][3] restricted to input channels [d3, d3 + s0) into
+ * tmae_lic_stack's fragment order, total = 9 * ceil(s0 / 32) * ceil(Cout / 16) * 512: ceil(total / 32768)),
+ * then nchunks more int64: the row t of every chunk (ntensors * 12 + nchunks values in all) */
 int tmae_relayout_multi(const long long* table, int ntensors, long long nchunks, void* stream);
 
 /* bias gradient: out[c] (=/+=) sum over rows r of x[(r/G)*Gs + off + r%G][c]; work >= 256*C floats */

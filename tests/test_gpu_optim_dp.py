@@ -404,6 +404,78 @@ def test_rccl_grad_sync_one_rank_bitwise(geom):
     assert np.array_equal(w0, w1)
 
 
+def _nccl_graph_worker(port, q):
+    """one-rank RCCL group: the captured DP step (GraphedTrainStep holding GradSync's bucketed all-reduces) against
+    eager DP steps (the same GradSync, always_collective) on the same batches and noise"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from textmae_amd import engine
+        from textmae_amd.optim import configure_optimizers
+        from textmae_amd.parallel import enable_data_parallel
+        from textmae_amd.rd_loss import RateDistortionLoss
+
+        crit = RateDistortionLoss(lmbda=1e-2)
+        res = {}
+        for mode in ("eager", "graph"):
+            m, cfg = _model(SMALL, 32, torch.bfloat16)
+            m.distortion = "ssim+l1"
+            sync = enable_data_parallel(m, bucket_mb=0.05, always_collective=True)
+            opt, aux = configure_optimizers(m, lr=2e-3, aux_lr=1e-3, fused=True)
+            batches = [_inputs(cfg, 2, 800 + i) for i in range(4)]
+            cu = lambda b: tuple(t.cuda() for t in b)  # noqa: E731
+            if mode == "eager":
+                losses = _train_steps(m, opt, aux, batches, crit)
+                info = {}
+            else:
+                imgs, scores, zn, yn = cu(batches[0])
+                n0 = sync.launched
+                g = engine.GraphedTrainStep(m, crit, opt, aux, imgs, scores, clip_max_norm=1.0, warmup=1,
+                                            noise=(zn, yn))
+                nb = len(sync._bounds) - 1
+                info = {"buckets": nb, "captured": sync.launched - n0 - nb, "in_backward": sync.launched_in_backward}
+                losses = [None]  # step 0 is the warm-up step inside the constructor
+                for b in batches[1:]:
+                    imgs, scores, zn, yn = cu(b)
+                    losses.append(float(g(imgs, scores, noise=(zn, yn))["loss"]))
+                n1 = sync.launched
+                torch.cuda.synchronize()
+                info["host_launches_during_replays"] = sync.launched - n1
+            w = torch.cat([p.detach().reshape(-1).float().cpu() for p in m.parameters()])
+            res[mode] = (losses, w.numpy(), info)
+        q.put(res)
+    except BaseException as e:  # report instead of leaving the parent waiting on the queue
+        q.put({"error": repr(e)[:2000]})
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_graphed_train_step_one_rank_bitwise():
+    """the DP training step as ONE HIP graph: GradSync's RCCL all-reduces (one-rank nccl group, short-circuit
+    bypassed) are captured from inside the backward (every bucket, most of them before the backward ends) and
+    replayed with the step; losses and post-step weights bitwise equal to eager DP steps"""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_graph_worker, args=(_port(), q))
+    p.start()
+    res = q.get(timeout=170)
+    p.join(timeout=60)
+    assert "error" not in res, res.get("error")
+    assert p.exitcode == 0
+    (le, we, _), (lg, wg, info) = res["eager"], res["graph"]
+    assert info["buckets"] > 4 and info["captured"] == info["buckets"], info
+    assert info["in_backward"] >= info["buckets"] // 2, info
+    assert lg[1:] == le[1:], (lg, le)
+    assert np.array_equal(we, wg)
+
+
 def test_bench_spawns_ranks_without_launcher():
     """``python bench.py --gpus 2`` with no torch.distributed launcher: bench starts two ranks itself
     (before any GPU call in the parent) and prints one line for the whole job"""

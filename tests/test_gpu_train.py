@@ -442,6 +442,35 @@ def test_mcm_train_bf16_close_to_f32():
     check("_rel2:flat16", _rel2(flat16, flat32), 3e-3)
 
 
+@pytest.mark.parametrize("geom", ["small", "vitb"])
+def test_train_fused_stacks_vs_per_layer(geom):
+    """the bf16 training forward's slice stacks on tmae_lic_stack (latent partial sums + chained / batched stacks
+    keeping every layer's pre-activation and output) against the same model on the per-layer conv launches: outputs
+    and every gradient within the bf16 rounding of the different summation order"""
+    from textmae_amd.mcm_train import TrainExec
+
+    cfgd = SMALL if geom == "small" else dict(img_size=256, num_keep_patches=144)
+    B = 2 if geom == "small" else 4
+    m, cfg, sd, imgs, scores, zn, yn, R = _model_and_oracle(cfgd, 9, B, torch.bfloat16)
+    res = {}
+    for fused in (True, False):
+        TrainExec.USE_LIC_STACK = fused
+        try:
+            m._train_exec = None
+            g, out, loss, aux = _hip_grads(m, imgs, scores, zn, yn, R)
+            assert m._train_exec._fused_ok() == fused
+        finally:
+            TrainExec.USE_LIC_STACK = True
+        res[fused] = (g, out["x_hat"].float().cpu(), out["likelihoods"]["y"].float().cpu())
+    (ga, xa, ya), (gb, xb, yb) = res[True], res[False]
+    check(f"_rel2:fused_train_x_hat_{geom}", _rel2(xa, xb), 2e-2)
+    check(f"_rel2:fused_train_ylik_{geom}", _rel2(ya, yb), 2e-2)
+    fa = torch.cat([ga[k].reshape(-1) for k in ga])
+    fb = torch.cat([gb[k].reshape(-1) for k in ga])
+    assert torch.isfinite(fa).all()
+    check(f"_rel2:fused_train_grads_{geom}", _rel2(fa, fb), 3e-2)
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_side_stream_wgrads_bitwise(dt):
     """weight gradients on the side stream (mcm_train._wg, deferred one-per-group forks) == the same backward
@@ -593,12 +622,32 @@ def test_weight_cache_refresh_modes(dt):
             assert torch.equal(W.conv(c), c.detach().permute(0, 2, 3, 1).reshape(co, 9 * ci).to(dt))
             assert torch.equal(W.conv_dg(c), c.detach().permute(1, 2, 3, 0).reshape(ci, 9 * co).to(dt))
 
+    # packed kinds of the fused training stacks: conv_dg problems back to back, the fragment order of
+    # tmae_lic_stack over an input-channel range (relayout mode 3), the latent-channel slice in conv layout
+    convb = torch.nn.Parameter(torch.randn(72, 40, 3, 3, generator=g).cuda())
+    from textmae_amd import ops
+
+    def check_packs():
+        torch.cuda.synchronize()
+        dg = W.packed([conv, convb], "conv_dg")
+        for j, c in enumerate((conv, convb)):
+            assert torch.equal(dg[j], c.detach().permute(1, 2, 3, 0).reshape(40, 9 * 72).to(dt))
+        for lo, n in ((8, 24), (0, 40), (16, 0)):
+            pk = W.packed([conv, convb], ("lic", lo, n))
+            for j, c in enumerate((conv, convb)):
+                assert torch.equal(pk[j], ops.pack_lic_stack_weight(c.detach()[:, lo:lo + n], dt)), (lo, n)
+        lat = W.packed([conv, convb], ("conv_lat", 24))
+        for j, c in enumerate((conv, convb)):
+            assert torch.equal(lat[j], c.detach()[:, :24].permute(0, 2, 3, 1).reshape(72, 9 * 24).to(dt))
+
     check_all()  # lazy first builds
+    check_packs()
     with torch.no_grad():
-        for p in (lin, conv, conv2):
+        for p in (lin, conv, conv2, convb):
             p.mul_(-1.5).add_(0.25)
-    bump_versions([lin, conv, conv2])
+    bump_versions([lin, conv, conv2, convb])
     W.refresh()  # one multi-tensor launch
     torch.cuda.synchronize()
     # the cached copies are returned as-is now (signatures current): they must hold the new values
     check_all()
+    check_packs()

@@ -91,6 +91,10 @@ class LicStackArgs(ctypes.Structure):
         ("cy2", P), ("cldy2", I),
         ("cs_x1", LL), ("cs_yv", LL), ("cs_src", LL), ("cs_add", LL), ("cs_y", LL), ("cs_y2", LL),
         ("cs_w", LL * LSTK_MAXL), ("cs_b", LL * LSTK_MAXL),
+        ("sv_pre", P * LSTK_MAXL), ("sv_act", P * LSTK_MAXL), ("sv_s", (LL * 2) * LSTK_MAXL),
+        ("sv_t", P), ("sv_t_s", LL * 2),
+        ("csv_pre", P * LSTK_MAXL), ("csv_act", P * LSTK_MAXL), ("cs_sv", LL * LSTK_MAXL),
+        ("csv_t", P), ("cs_t", LL),
     ]
 
 

@@ -63,30 +63,37 @@ __device__ __forceinline__ float eb_logits(const float* t, float v) {
   return (t[54] * h0 + t[55] * h1 + t[56] * h2) + t[57];
 }
 
-// z, zhat: NHWC [n*HW][C]; lik, noise: NCHW [n][C][HW]
+// z, zhat: NHWC [n*HW][C]; lik, noise: NCHW [n][C][HW].
+// One workgroup per (image, 64-channel block): element e = pix * 64 + c, so z / zhat are read / written in 256-B
+// channel runs, and the block's lik (and noise) region [b][c0 .. c0 + 63][0 .. HW) is one contiguous NCHW range
+// written by this workgroup alone.  (One thread per NHWC element, as before round 5, wrote each NCHW line from ~HW
+// workgroups on different XCDs at a 4 * HW-B stride: PMC 1.93x the algorithmic bytes.)
 __global__ void __launch_bounds__(256)
 eb_likelihood_kernel(const float* __restrict__ z, const float* __restrict__ tab, const float* __restrict__ noise,
-                     float* __restrict__ lik, void* __restrict__ zhat, int zhat_bf16, int C, int HW, int total) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int c = i % C, m = i / C;
-  const int b = m / HW, pix = m - b * HW;
-  const float* t = tab + (size_t)c * EB_PACK;
-  const float med = t[58];
-  const float zv = z[i];
-  const float q = rintf(zv - med) + med;
-  const size_t nchw = ((size_t)b * C + c) * HW + pix;
-  const float x = noise ? zv + noise[nchw] : q;
-  const float lower = eb_logits(t, x - 0.5f);
-  const float upper = eb_logits(t, x + 0.5f);
-  const float sum = lower + upper;
-  const float sgn = sum > 0.0f ? -1.0f : (sum < 0.0f ? 1.0f : -0.0f);
-  const float l = fabsf(sigmoid_t(sgn * upper) - sigmoid_t(sgn * lower));
-  lik[nchw] = fmaxf(l, 1e-9f);
-  // quantize_ste forward value: round(z - med) + med  (MCM.py:742-744)
-  if (zhat) {
-    if (zhat_bf16) ((bf16*)zhat)[i] = (bf16)q;
-    else ((float*)zhat)[i] = q;
+                     float* __restrict__ lik, void* __restrict__ zhat, int zhat_bf16, int C, int HW) {
+  const int nblk = (C + 63) >> 6;
+  const int b = blockIdx.x / nblk, c0 = (blockIdx.x - b * nblk) * 64;
+  for (int e = threadIdx.x; e < 64 * HW; e += 256) {
+    const int pix = e >> 6, c = c0 + (e & 63);
+    if (c >= C) continue;
+    const size_t i = ((size_t)b * HW + pix) * C + c;
+    const float* t = tab + (size_t)c * EB_PACK;
+    const float med = t[58];
+    const float zv = z[i];
+    const float q = rintf(zv - med) + med;
+    const size_t nchw = ((size_t)b * C + c) * HW + pix;
+    const float x = noise ? zv + noise[nchw] : q;
+    const float lower = eb_logits(t, x - 0.5f);
+    const float upper = eb_logits(t, x + 0.5f);
+    const float sum = lower + upper;
+    const float sgn = sum > 0.0f ? -1.0f : (sum < 0.0f ? 1.0f : -0.0f);
+    const float l = fabsf(sigmoid_t(sgn * upper) - sigmoid_t(sgn * lower));
+    lik[nchw] = fmaxf(l, 1e-9f);
+    // quantize_ste forward value: round(z - med) + med  (MCM.py:742-744)
+    if (zhat) {
+      if (zhat_bf16) ((bf16*)zhat)[i] = (bf16)q;
+      else ((float*)zhat)[i] = q;
+    }
   }
 }
 
@@ -95,10 +102,12 @@ extern "C" int tmae_eb_likelihood_fwd(const float* z, const tmae_eb_params* para
   TMAE_REQUIRE(params != nullptr && table != nullptr, "tmae_eb_likelihood_fwd: params/table required");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(eb_prep_kernel, dim3(ceil_div(C * EB_PACK, 256)), dim3(256), 0, st, *params, table, C);
-  const int total = n * HW * C;
-  if (total > 0)
-    hipLaunchKernelGGL(eb_likelihood_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, st, z, table, noise, lik,
-                       zhat, zhat_dtype == TMAE_BF16, C, HW, total);
+  const long long total = (long long)n * HW * C;
+  if (total > 0) {
+    TMAE_REQUIRE(total < (1ll << 31), "tmae_eb_likelihood_fwd: %lld elements exceed the 32-bit range", total);
+    hipLaunchKernelGGL(eb_likelihood_kernel, dim3(n * ceil_div(C, 64)), dim3(256), 0, st, z, table, noise, lik, zhat,
+                       zhat_dtype == TMAE_BF16, C, HW);
+  }
   TMAE_LAUNCH_CHECK("tmae_eb_likelihood_fwd");
 }
 

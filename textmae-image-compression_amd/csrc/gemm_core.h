@@ -403,8 +403,8 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
   constexpr bool XPART = BM % PR != 0;
   constexpr int ROWS = BN + BM;
   static_assert(TN >= 1 && TM >= 1 && WJ >= 1 && XJ >= 1 && BN % PR == 0 && BM % 8 == 0, "bad tile");
+  static_assert(!XPART || NS == 2, "partial DMA rounds need the uncounted 2-stage ring");
   static_assert(NS >= 2 && NS <= 4, "stages");
-  static_assert(!XPART || NS <= 3, "a partial DMA round: at most one younger stage in flight at a wait");
   __shared__ __attribute__((aligned(16))) uint4 lds[NS * ROWS * 8];
 
   const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
@@ -479,22 +479,15 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
     // step kt reads stage kt % NS and issues step kt + NS - 1 into the stage step kt - 1 read (retired by
     // the barrier that closed step kt - 1)
     constexpr int PER = WJ + XJ;  // LDS-DMA instructions per wave per stage
-    // with a partial token-side round (the 8-wave 256 x 160 tile: rows 128..159 by waves 0..3) the waves that
-    // skip it count one instruction less per stage: the counted wait is per wave (wave-uniform scalar branch)
-    const bool short_wave = XPART && PR * (XJ - 1) + 8 * (int)wave_u >= BM;
-    auto ring_wait = [&](int younger) {
-      if (XPART && short_wave) gemm_ring_wait<PER - 1, NS>(younger);
-      else gemm_ring_wait<PER, NS>(younger);
-    };
     set_rows(tn, tm);
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
       if (s < nk) issue(s, s);
-    ring_wait(min(NS - 2, nk - 1));
+    gemm_ring_wait<PER, NS>(min(NS - 2, nk - 1));
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + NS - 1 < nk) issue((kt + NS - 1) % NS, kt + NS - 1);
       mfma_tile<T, BN, WN, WM, TN, TM>(lds + (kt % NS) * ROWS * 8, wn, wm, lane, acc);
-      ring_wait(min(kt + NS - 1, nk - 1) - (kt + 1));
+      gemm_ring_wait<PER, NS>(min(kt + NS - 1, nk - 1) - (kt + 1));
     }
   }
   static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= NS * ROWS * 128, "epilogue region exceeds the LDS ring");
@@ -582,10 +575,9 @@ struct TileChoice { int bn, bm, nw; };
 // The 8-wave 256 x 192 tile (waves 2 x 4, 128 x 48 each) exists for the tail: 9280- and 16448-row token
 // GEMMs whose 256 x 256 tile count lands just past a multiple of 256 CUs (enc qkv 333 tiles = 1.3
 // rounds, dec fc1 520 = 2.03, dec proj/fc2 130 = 0.5).
-static constexpr int kNumTiles = 11;
-static constexpr int kTileCand[kNumTiles][3] = {{256, 256, 8}, {128, 128, 4}, {64, 128, 4}, {32, 128, 4},
-                                                {64, 64, 4},   {32, 64, 4},   {256, 192, 8}, {128, 160, 4},
-                                                {128, 192, 4}, {256, 160, 8}, {256, 128, 8}};
+static constexpr int kNumTiles = 9;
+static constexpr int kTileCand[kNumTiles][3] = {{256, 256, 8}, {128, 128, 4}, {64, 128, 4}, {32, 128, 4}, {64, 64, 4},
+                                                {32, 64, 4},   {256, 192, 8}, {128, 160, 4}, {128, 192, 4}};
 // candidates only the bf16 LDS-DMA path instantiates
 static inline bool tile_bf16_only(int i) { return kTileCand[i][2] == 8 || i >= 7; }
 // eff = per-CU throughput relative to two 128 x 128 workgroups.  Forced-tile runs of the bench's token
@@ -614,14 +606,7 @@ static inline bool tile_bf16_only(int i) { return kTileCand[i][2] == 8 || i >= 7
 #endif
 static inline TileChoice choose_tile(int M, int N, int K, int batch, bool allow_big) {
   const double kf = 1.0 + 0.12 * std::log2(std::max(K, 768) / 768.0);
-#ifndef TMAE_E160_8
-#define TMAE_E160_8 0.0
-#endif
-#ifndef TMAE_E128_8
-#define TMAE_E128_8 0.0
-#endif
-  const double eff[kNumTiles] = {1.10 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, 1.08 * kf, 1.22, 1.25, TMAE_E160_8,
-                                 TMAE_E128_8};
+  const double eff[kNumTiles] = {1.10 * kf, 1.0, 0.86, 0.70, 0.72, 0.55, 1.08 * kf, 1.22, 1.25};
   constexpr int forced = TMAE_GEMM_TILE;
   if (forced >= 0 && forced < kNumTiles && (allow_big || !tile_bf16_only(forced)))
     return TileChoice{kTileCand[forced][0], kTileCand[forced][1], kTileCand[forced][2]};
@@ -658,16 +643,6 @@ static int launch_one(const char* name, const WS& ws, const XS& xs, const EPI& e
         TMAE_LAUNCH_CHECK(name);
       }
     }
-    // 8-wave tiles (one workgroup per CU) whose 3-stage ring fits the CU's 160 KiB: two K-steps of LDS-DMA in
-    // flight under the current MFMAs
-    constexpr bool deep8 = sizeof(T) == 2 && NW == 8 && (BN + BM) * 128 * 3 <= 160 * 1024;
-    if constexpr (deep8) {
-      if (ceil_div(K, 8 * Elt<T>::EPC) >= 3) {
-        hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, NW, WS, XS, EPI, 3>), dim3(tiles, n1 * n2),
-                           dim3(64 * NW), 0, st, ws, xs, epi, M, N, K, n2);
-        TMAE_LAUNCH_CHECK(name);
-      }
-    }
     hipLaunchKernelGGL((gemm_glds_kernel<T, BN, BM, WGN, NW, WS, XS, EPI>), dim3(tiles, n1 * n2), dim3(64 * NW), 0,
                        st, ws, xs, epi, M, N, K, n2);
   } else {
@@ -685,8 +660,6 @@ static int launch_gemm(const char* name, const T* w, long long ws1, long long ws
   const TileChoice tc = choose_tile(M, N, K, n1 * n2, GLDS && sizeof(T) == 2);
   if constexpr (GLDS && sizeof(T) == 2) {
     if (tc.nw == 8 && tc.bm == 192) return launch_one<GLDS, T, 256, 192, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
-    if (tc.nw == 8 && tc.bm == 160) return launch_one<GLDS, T, 256, 160, 4, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
-    if (tc.nw == 8 && tc.bm == 128) return launch_one<GLDS, T, 256, 128, 4, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 4 && tc.bm == 160) return launch_one<GLDS, T, 128, 160, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 4 && tc.bm == 192) return launch_one<GLDS, T, 128, 192, 2, 4>(name, ws, xs, epi, M, N, K, n1, n2, st);
     if (tc.nw == 8) return launch_one<GLDS, T, 256, 256, 2, 8>(name, ws, xs, epi, M, N, K, n1, n2, st);

@@ -58,6 +58,9 @@ struct LstkOut {
   int ld_src;
   void* y2;
   int ldy2;
+  bf16* sp;   // training: this layer's pre-activation, bf16 [rows][cout] (NULL: not kept)
+  bf16* sa;   // training: its GELU output
+  float* st;  // training, lrp last layer: the pre-tanh value, f32 [rows][cout]
 };
 
 #ifndef LSTK_OPT
@@ -212,6 +215,10 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
       const f32x2 lo = gelu2_bf16out(v.xy), hi = gelu2_bf16out(v.zw);
       bf16x4 q;
       q[0] = (bf16)lo.x; q[1] = (bf16)lo.y; q[2] = (bf16)hi.x; q[3] = (bf16)hi.y;
+      if (o.sp && okc[i] && pix(j) < npix) {  // training: keep the GELU input and output for the backward
+        store4(o.sp + grow(j) * L.cout + cc[i], v);
+        *reinterpret_cast<bf16x4*>(o.sa + grow(j) * L.cout + cc[i]) = q;
+      }
       return q;
     };
     if (NF == 2 && (L.cout & 7) == 0 && !(LSTK_OPT & 1)) {
@@ -253,6 +260,7 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
 #pragma unroll
         for (int e = 0; e < 4; ++e) r[e] += 0.5f * tanhf(v[e]);
         if (okc[i] && pix(j) < npix) {
+          if (o.st) store4(o.st + grow(j) * L.cout + cc[i], v);
           store4(reinterpret_cast<bf16*>(o.y) + grow(j) * o.ldy + cc[i], r);
           if (o.y2) store4(reinterpret_cast<bf16*>(o.y2) + grow(j) * o.ldy2 + cc[i], r);
         }
@@ -410,6 +418,16 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
       }
       L.cin = cin;
       const bool first = l == 0, last = l + 1 == nl;
+      if (pass == 0) {
+        o.sp = a->sv_pre[l] && !last ? reinterpret_cast<bf16*>(a->sv_pre[l]) + b1 * a->sv_s[l][0] + b2 * a->sv_s[l][1]
+                                     : nullptr;
+        o.sa = o.sp ? reinterpret_cast<bf16*>(a->sv_act[l]) + b1 * a->sv_s[l][0] + b2 * a->sv_s[l][1] : nullptr;
+        o.st = a->sv_t && last ? a->sv_t + b1 * a->sv_t_s[0] + b2 * a->sv_t_s[1] : nullptr;
+      } else {
+        o.sp = a->csv_pre[l] && !last ? reinterpret_cast<bf16*>(a->csv_pre[l]) + b2 * a->cs_sv[l] : nullptr;
+        o.sa = o.sp ? reinterpret_cast<bf16*>(a->csv_act[l]) + b2 * a->cs_sv[l] : nullptr;
+        o.st = a->csv_t && last ? a->csv_t + b2 * a->cs_t : nullptr;
+      }
       const unsigned in_off = (l & 1) ? (unsigned)BUF : 0u, out_off = (l & 1) ? 0u : (unsigned)BUF;
       const int nfr = (L.cout + 15) >> 4;
       const int nkc = pad32(L.cin) >> 5;
@@ -495,6 +513,11 @@ extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
                    "tmae_lic_stack: chain layer %d", l);
   }
   if (a.addend) TMAE_REQUIRE(a.ld_add % 4 == 0, "tmae_lic_stack: addend stride %d", a.ld_add);
+  for (int l = 0; l < a.nlayers; ++l)
+    TMAE_REQUIRE(!a.sv_pre[l] == !a.sv_act[l], "tmae_lic_stack: layer %d keeps pre-activation and output together", l);
+  for (int l = 0; l < a.cn && (a.flags & TMAE_LIC_STACK_CHAIN); ++l)
+    TMAE_REQUIRE(!a.csv_pre[l] == !a.csv_act[l], "tmae_lic_stack: chain layer %d keeps pre and output together", l);
+  TMAE_REQUIRE(!a.sv_t || a.lrp_src, "tmae_lic_stack: sv_t is the lrp stack's pre-tanh value");
   const int nwg = a.n * a.nb1 * a.nb2;
   hipLaunchKernelGGL(lic_stack_kernel, dim3(nwg), dim3(NW * 64), 0, (hipStream_t)stream, a);
   TMAE_LAUNCH_CHECK("tmae_lic_stack");

@@ -348,7 +348,8 @@ static int conv_dgrad_t(const tmae_conv_dgrad_args& a, hipStream_t st) {
   const int M = xs.rows, K = xs.K, N = a.cin;
   const int nb = a.nb > 1 ? a.nb : 1;
   const char* nm = "tmae_conv_dgrad";
-  TMAE_REQUIRE(nb <= 2 && (nb == 1 || !a.acc[0]), "tmae_conv_dgrad: batched (nb = %d) launches take no routes", nb);
+  TMAE_REQUIRE(nb <= 65535 && (nb == 1 || !a.acc[0]), "tmae_conv_dgrad: batched (nb = %d) launches take no routes",
+               nb);
   if (a.acc[0]) {
     TMAE_REQUIRE(a.lim[0] % 8 == 0 && a.lim[1] % 8 == 0 && a.lim[2] == a.cin && a.lim[0] <= a.lim[1] &&
                      a.lim[1] <= a.lim[2],
@@ -538,6 +539,27 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
         if (to_bf16) relayout_store<bf16>(dstp, ob + (size_t)t * A + a, sm[a * B + t]);
         else relayout_store<float>(dstp, ob + (size_t)t * A + a, sm[a * B + t]);
       }
+    return;
+  }
+  if (mode == 3) {
+    // a 3x3 conv weight [Cout = d1][Cin_tot = d2][3][3] (f32), input channels [d3, d3 + s0), into tmae_lic_stack's
+    // MFMA fragment order [tap][k-step][cout fragment][lane = 16 fq + fr][8]: element e of lane (fq, fr) in
+    // fragment f, k-step kc = W[16 f + fr][d3 + 32 kc + 8 fq + e][tap], zero past Cout / the channel range
+    // (ops.pack_lic_stack_weight's layout, built on the device so a training step re-packs without host work)
+    const unsigned cout = d1, cin_tot = d2, lo = d3, cn = (unsigned)s0;
+    const unsigned nfr = (cout + 15) / 16;
+    const unsigned nkc = (cn + 31) / 32;
+    const unsigned base3 = chunk * 32768u;
+    for (unsigned k = tid; k < 32768u; k += 256u) {
+      const unsigned i = base3 + k;
+      if (i >= total) break;
+      const unsigned e8 = i & 7u, lane = (i >> 3) & 63u, r = i >> 9;  // r = (tap * nkc + kc) * nfr + f
+      const unsigned f = r % nfr, tk = r / nfr, kc = tk % nkc, tap = tk / nkc;
+      const unsigned co = 16 * f + (lane & 15u), ci = 32 * kc + 8 * (lane >> 4) + e8;
+      const float v = (co < cout && ci < cn) ? src[((size_t)co * cin_tot + lo + ci) * 9 + tap] : 0.0f;
+      if (to_bf16) ((bf16*)e[1])[i] = (bf16)v;
+      else ((float*)e[1])[i] = v;
+    }
     return;
   }
   const unsigned base = chunk * 32768u;

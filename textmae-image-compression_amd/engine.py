@@ -76,14 +76,18 @@ class GraphedTrainStep:
     version counters (the update kernel writes through raw pointers; the executors' weight caches are keyed on
     the versions, so an eager forward after replays re-lays out the new weights).  The learning rates, betas,
     eps and weight decays are baked into the graph: when any of them changes, the step is captured again.
-    Data parallelism (a GradSync with more than one rank) is not captured: use ``train_step`` there."""
+    Data parallelism over RCCL is captured too: GradSync's bucketed all-reduces are issued from inside the captured
+    backward, so every replay runs them on the process group's stream under the remaining backward kernels, joined
+    before clip / Adam (one ``graph.replay()`` per step at any world size, like the reference's one loop body,
+    utils/engine.py:75-91).  The RCCL communicator exists before the capture (the eager warm-up step's
+    collectives).  A gloo group (host-staged all-reduce) is refused: use ``train_step`` there."""
 
     def __init__(self, model, criterion, optimizer, aux_optimizer, samples, total_scores, clip_max_norm=1.0,
                  warmup=1, noise=None):
         sync = getattr(model, "grad_sync", None)
-        if sync is not None and (sync.world() > 1 or sync.always_collective):
-            raise ValueError("GraphedTrainStep: the data-parallel gradient all-reduce is not captured; "
-                             "use engine.train_step with data parallelism")
+        if sync is not None and not sync.capturable():
+            raise ValueError("GraphedTrainStep: a gloo gradient all-reduce (host-staged) is not capturable; use "
+                             "engine.train_step, or the nccl (RCCL) backend whose collectives the graph holds")
         if not samples.is_cuda:
             raise ValueError("GraphedTrainStep needs device inputs")
         self.model, self.criterion = model, criterion

@@ -64,12 +64,16 @@ class _Weights:
         else:
             dst, job = make(w)
         if job is not None:
-            T.relayout(w, dst, *job)
+            if job[0] == "lic":  # first build of a fragment-order pack (later ones: relayout_multi mode 3)
+                _, co, ci, lo, n = job
+                dst.copy_(ops.pack_lic_stack_weight(w[:, lo:lo + n], self.dtype))
+            else:
+                T.relayout(w, dst, *job)
         self.cache[key] = [sig, dst, p, job]
         return dst
 
     def packed(self, params, kind):
-        """one buffer holding the `kind` layouts ("conv" or "bias") of `params` back to back, so a batched
+        """one buffer holding the `kind` layouts ("conv", "conv_dg" or "bias") of `params` back to back, so a batched
         launch reaches problem j at a constant stride; each row is also that parameter's cache entry"""
         key = (tuple(id(p) for p in params), kind)
         buf = self.packs.get(key)
@@ -79,6 +83,31 @@ class _Weights:
                 co, ci = p0.shape[:2]
                 buf = torch.empty((len(params), co, 9 * ci), dtype=self.dtype, device=p0.device)
                 job = ((co, 3, 3, ci), (ci * 9, 3, 1, 9))
+            elif kind == "conv_dg":  # the transposed-conv data-gradient layout of conv_dg(), problems back to back
+                co, ci = p0.shape[:2]
+                buf = torch.empty((len(params), ci, 9 * co), dtype=self.dtype, device=p0.device)
+                job = ((ci * 9, 1, 1, co), (1, 0, 0, ci * 9))
+            elif isinstance(kind, tuple) and kind[0] == "lic":  # ("lic", lo, n): input channels [lo, lo + n) packed
+                co = p0.shape[0]
+                lo, n = kind[1], kind[2]
+                total = 9 * (-(-n // 32)) * (-(-co // 16)) * 512
+                buf = torch.empty((len(params), total), dtype=self.dtype, device=p0.device)
+                for j, p in enumerate(params):
+                    self.cache[(id(p), kind)] = [None, buf[j], p, ("lic", co, p.shape[1], lo, n)]
+                self.packs[key] = buf
+                for p in params:
+                    self._get(p, kind, None)
+                return buf
+            elif isinstance(kind, tuple) and kind[0] == "conv_lat":  # ("conv_lat", n): input channels [0, n), conv layout
+                co, n = p0.shape[0], kind[1]
+                buf = torch.empty((len(params), co, 9 * n), dtype=self.dtype, device=p0.device)
+                for j, p in enumerate(params):
+                    ci = p.shape[1]
+                    self.cache[(id(p), kind)] = [None, buf[j], p, ((co, 3, 3, n), (ci * 9, 3, 1, 9))]
+                self.packs[key] = buf
+                for p in params:
+                    self._get(p, kind, None)
+                return buf
             else:
                 buf = torch.empty((len(params), p0.numel()), dtype=torch.float32, device=p0.device)
                 job = ((p0.numel(),), (1,))
@@ -105,6 +134,14 @@ class _Weights:
             sig, dst, p, job = e
             e[0] = (p.data_ptr(), p._version)
             if job is None:
+                continue
+            if job[0] == "lic":  # tmae_lic_stack fragment order (relayout mode 3)
+                _, co, ci, lo, n = job
+                total = 9 * (-(-n // 32)) * (-(-co // 16)) * 512
+                rows.append([p.data_ptr(), dst.data_ptr(), ops.dtype_code(dst.dtype) | (3 << 8), co, ci, lo, n, 0, 0, 0,
+                             total, chunk])
+                ptrs.append((p.data_ptr(), dst.data_ptr()))
+                chunk += (total + 32767) // 32768
                 continue
             dims, strides = job
             d = list(dims) + [1] * (4 - len(dims))
@@ -567,7 +604,127 @@ class TrainExec(_VitTrainBase):
             x = out
         return saved
 
+    USE_LIC_STACK = True  # test hook: False runs the per-layer conv launches in the bf16 training forward too
+
+    def _fused_ok(self):
+        m = self.m
+        return (self.dtype == torch.bfloat16 and self.USE_LIC_STACK and self.sw % 8 == 0 and m.num_slices > self.ms
+                and ops.lic_stack_fits(self.g, self.sw * (self.ms + 1), self.mid))
+
+    def _slices_fwd_fused(self):
+        """the slice loop on the fused stacks (lic_stack.hip), as the inference forward runs it (mcm.py _slices), with
+        every layer's pre-activation and GELU output kept for the backward (tmae_lic_stack_args.sv_*):
+          * the latent-channel parts of every slice's first convs (mean + lrp on latent_means, scale on latent_scales)
+            as two conv launches into the partial-sum buffer P, added by each stack's layer-0 epilogue;
+          * slices 0..ms-1: ONE launch each -- the mean stack's workgroups go on with the slice's lrp stack, the scale
+            stack beside them; their Gaussian likelihoods in one launch after the loop;
+          * slices ms..S-1 batched: one launch for their 2 x nbs mean / scale stacks, the likelihoods, one for their
+            lrp stacks.
+        Weights are packed in fragment order by the per-step relayout (relayout mode 3).  Returns nothing; fills
+        self.sl with the records _slices_bwd reads (same shapes as _slices_fwd's)."""
+        m, dt, W, B, g = self.m, self.dtype, self.w, self.batch, self.g
+        M, S, sw, ms, Mp, HW = m.latent_depth, m.num_slices, self.sw, self.ms, self.Mp, g * g
+        mid = self.mid
+        c0, nl = mid[0], len(mid)
+        esz, e4 = self.LMS.element_size(), 4
+        lms = self.LMS.data_ptr()
+        cm = [_convs(m.cc_transform_mean[i]) for i in range(S)]
+        cs = [_convs(m.cc_transform_scale[i]) for i in range(S)]
+        cl = [_convs(m.lrp_transform[i]) for i in range(S)]
+        self.YPT = self._e(Mp, M)
+        self.YPRE = torch.empty((Mp, M), dtype=torch.float32, device=self.device)
+        self.YH = self._e(Mp, M)
+        self.YLIK = torch.empty((B, M, g, g), dtype=torch.float32, device=self.device)
+        # ---- latent-channel partial sums P = [mean (S c0) | lrp (S c0) | scale (S c0)] (no bias: layer 0 adds it)
+        Pw = 3 * S * c0
+        off_mean, off_lrp, off_scale = 0, S * c0, 2 * S * c0
+        P = torch.empty((Mp, Pw), dtype=torch.float32, device=self.device)
+        self._P = P
+        pb = P.data_ptr()
+        w_ml = W.packed([c[0].weight for c in cm] + [c[0].weight for c in cl], ("conv_lat", M))
+        w_s = W.packed([c[0].weight for c in cs], ("conv_lat", M))
+        ops.conv3x3(self.LMS, M, 2 * M, B, g, g, w_ml, None, pb, Pw, S * c0, dt, y_f32=True, nb=(1, 2),
+                    strides={"w": (0, S * w_ml[0].numel()), "y": (0, S * c0)})
+        ops.conv3x3(self.LS, M, 2 * M, B, g, g, w_s, None, pb + off_scale * 4, Pw, S * c0, dt, y_f32=True)
+
+        def stack_weights(convs_per_problem, lo, n0):
+            """per layer: packed weights of the problems (layer 0: input channels [lo, lo + n0)) and biases"""
+            ws, bs = [], []
+            for l in range(nl):
+                kind = ("lic", lo, n0) if l == 0 else ("lic", 0, mid[l - 1])
+                ws.append(W.packed([c[l].weight for c in convs_per_problem], kind))
+                bs.append(W.packed([c[l].bias for c in convs_per_problem], "bias"))
+            return ws, bs
+
+        def save_bufs(lead):
+            """pre / act per non-last layer, [*lead][Mp][cout] bf16"""
+            return [(self._e(*lead, Mp, c), self._e(*lead, Mp, c)) for c in mid[:-1]]
+
+        self.sl = [None] * S
+        # ---- slices 0..ms-1: chained launches
+        MS = torch.empty((2, ms, Mp, sw), dtype=torch.float32, device=self.device)
+        for i in range(ms):
+            ny = sw * i
+            ws, bs = stack_weights([cm[i], cs[i]], M, ny)
+            lw, lb = stack_weights([cl[i]], M, ny + sw)
+            st = {"a": (off_scale - off_mean, c0), "y": (ms * Mp * sw, 0)}
+            for l in range(nl):
+                st[f"w{l}"] = (ws[l][0].numel(), 0)
+                st[f"b{l}"] = (bs[l][0].numel(), 0)
+            sv_ms = save_bufs((2,))
+            sv_l = save_bufs(())
+            t = torch.empty((Mp, sw), dtype=torch.float32, device=self.device)
+            ch = dict(w=[w[0] for w in lw], b=[b[0] for b in lb], couts=mid, x1=lms + M * esz, c1=ny, ld1=2 * M,
+                      y=self.Y32.data_ptr() + i * sw * e4, ldy=M, add=pb + (off_lrp + i * c0) * e4, ld_add=Pw,
+                      ypre=self.YPRE.data_ptr() + i * sw * e4, ld_ypre=M, out=self.YH.data_ptr() + i * sw * esz,
+                      ld_out=M, out2=lms + (M + i * sw) * esz, ld_out2=2 * M)
+            save = {"layers": [(pre, act, (Mp * c, 0)) for (act, pre), c in zip(sv_ms, mid)],
+                    "chain": [(pre, act, 0) for act, pre in sv_l], "chain_t": t}
+            ops.lic_stack(B, g, lms + M * esz, ny, 2 * M, [w[0] for w in ws], [b[0] for b in bs], mid, MS[0, i], sw,
+                          True, addend=pb + (off_mean + i * c0) * e4, ld_add=Pw, nb=(2, 1), strides=st, chain=ch,
+                          save=save)
+            self.sl[i] = {"mean": [(a[0], p_[0]) for a, p_ in sv_ms] + [MS[0, i]],
+                          "scale": [(a[1], p_[1]) for a, p_ in sv_ms] + [MS[1, i]],
+                          "lrp": list(sv_l) + [t]}
+        # Gaussian likelihoods + y_hat_pre (YPT, the backward's lrp input; YPRE) of the chained slices
+        ops.gc_slices(self.Y32, M, 0, MS[0], MS[1], Mp * sw, sw, self.y_noise, self.YLIK, M, self.YPT, dt, M,
+                      self.YPRE, M, B, HW, ms, sw)
+        # ---- slices ms..S-1 batched on the support slots 0..ms-1
+        i0, nbs = ms, S - ms
+        bs_ = range(i0, S)
+        ws, bsb = stack_weights([cm[i] for i in bs_] + [cs[i] for i in bs_], M, sw * ms)
+        st = {"a": (off_scale - off_mean, c0), "y": (nbs * Mp * sw, Mp * sw)}
+        for l in range(nl):
+            st[f"w{l}"] = (nbs * ws[l][0].numel(), ws[l][0].numel())
+            st[f"b{l}"] = (nbs * bsb[l][0].numel(), bsb[l][0].numel())
+        MSB = torch.empty((2, nbs, Mp, sw), dtype=torch.float32, device=self.device)
+        sv_b = save_bufs((2, nbs))
+        ops.lic_stack(B, g, lms + M * esz, sw * ms, 2 * M, [w[0] for w in ws], [b[0] for b in bsb], mid, MSB, sw, True,
+                      addend=pb + (off_mean + i0 * c0) * e4, ld_add=Pw, nb=(2, nbs), strides=st,
+                      save={"layers": [(pre, act, (nbs * Mp * c, Mp * c)) for (act, pre), c in zip(sv_b, mid)]})
+        ops.gc_slices(self.Y32, M, i0 * sw, MSB[0], MSB[1], Mp * sw, sw, self.y_noise, self.YLIK, M, self.YPT, dt, M,
+                      self.YPRE, M, B, HW, nbs, sw)
+        lw, lb = stack_weights([cl[i] for i in bs_], M, sw * ms + sw)
+        st = {"a": (0, c0), "y": (0, sw), "src": (0, sw), "x2": (0, sw)}
+        for l in range(nl):
+            st[f"w{l}"] = (0, lw[l][0].numel())
+            st[f"b{l}"] = (0, lb[l][0].numel())
+        sv_lb = save_bufs((nbs,))
+        tb = torch.empty((nbs, Mp, sw), dtype=torch.float32, device=self.device)
+        ops.lic_stack(B, g, lms + M * esz, sw * ms, 2 * M, [w[0] for w in lw], [b[0] for b in lb], mid,
+                      self.YH.data_ptr() + i0 * sw * esz, M, False, x2=self.YPT.data_ptr() + i0 * sw * esz, c2=sw,
+                      ld2=M, addend=pb + (off_lrp + i0 * c0) * e4, ld_add=Pw,
+                      lrp_src=self.YPRE.data_ptr() + i0 * sw * e4, ld_src=M, nb=(1, nbs), strides=st,
+                      save={"layers": [(pre, act, (0, Mp * c)) for (act, pre), c in zip(sv_lb, mid)], "t": tb,
+                            "t_s": (0, Mp * sw)})
+        for j, i in enumerate(bs_):
+            self.sl[i] = {"mean": [(a[0, j], p_[0, j]) for a, p_ in sv_b] + [MSB[0, j]],
+                          "scale": [(a[1, j], p_[1, j]) for a, p_ in sv_b] + [MSB[1, j]],
+                          "lrp": [(a[j], p_[j]) for a, p_ in sv_lb] + [tb[j]]}
+
     def _slices_fwd(self):
+        if self._fused_ok():
+            return self._slices_fwd_fused()
         m, dt, W, B, g = self.m, self.dtype, self.w, self.batch, self.g
         M, S, sw, ms, Mp, HW = m.latent_depth, m.num_slices, self.sw, self.ms, self.Mp, self.g * self.g
         esz = self.LMS.element_size()
@@ -925,7 +1082,12 @@ class TrainExec(_VitTrainBase):
         main = torch.cuda.current_stream(self.device) if conc else None
         joined = None
         GS = torch.empty((Mp, M), dtype=torch.float32, device=self.device)
-        for i in reversed(range(S)):
+        # slices ms..S-1 were run batched in the forward (they condition on the fixed support slots 0..ms-1): their
+        # backward is batched too, every data gradient of layers 4..1 one launch for all of them
+        nser = ms if S - ms > 1 else S
+        if nser < S:
+            self._batched_bwd(nser, S - nser, dYH, dylik, DY, dLM, dLS, dSUP, dSUP2, GS)
+        for i in reversed(range(nser)):
             # fresh per slice: the side stream's weight gradients of slice i + 1 may still read the last ones
             dT = self._e(Mp, sw)
             dMU, dSG = self._e(Mp, sw), self._e(Mp, sw)
@@ -971,6 +1133,85 @@ class TrainExec(_VitTrainBase):
         if joined is not None:
             main.wait_event(joined)
         return DY, dLM, dLS
+
+    def _batched_bwd(self, i0, nbs, dYH, dylik, DY, dLM, dLS, dSUP, dSUP2, GS):
+        """backward of the batched slices i0..i0+nbs-1 (_batched_fwd): per slice the lrp backward, then the lrp stacks'
+        layers 4..1 as ONE nbs-problem data-gradient launch each, their first layers one by one (routes into the
+        shared latent / support gradients, slices in descending order), the Gaussian backward per slice, then the
+        mean and scale stacks' layers 4..1 as ONE 2 nbs-problem launch each and their first layers one by one (mean
+        before scale per slice).  Weight gradients per problem on the side stream, as for the serial slices."""
+        m, dt, W, G, B, g = self.m, self.dtype, self.w, self.grad, self.batch, self.g
+        M, sw, ms, Mp, HW = m.latent_depth, self.sw, self.ms, self.Mp, g * g
+        esz = self.LMS.element_size()
+        lms = self.LMS.data_ptr()
+        k = ms
+        sl = list(range(i0, i0 + nbs))
+        recs = [self.sl[i] for i in sl]
+        cl = [_convs(m.lrp_transform[i]) for i in sl]
+        cm = [_convs(m.cc_transform_mean[i]) for i in sl]
+        cs = [_convs(m.cc_transform_scale[i]) for i in sl]
+
+        def stride(views, what):
+            """constant element stride between consecutive problems' views (the batched forward's buffers)"""
+            d = {(b.data_ptr() - a.data_ptr()) for a, b in zip(views, views[1:])}
+            e = views[0].element_size()
+            if len(d) > 1 or (d and next(iter(d)) % e):
+                raise RuntimeError(f"batched slice backward: {what} not at a constant stride")
+            return (next(iter(d)) // e) if d else 0
+
+        def stacks(convs, saved, dtop, what):
+            """layers 4..1 of len(convs) same-shape stacks, problem p's saved activations saved[p]; dtop [P][Mp][cout]"""
+            P = len(convs)
+            d = dtop
+            for l in range(4, 0, -1):
+                cin, cout = convs[0][l].in_channels, convs[0][l].out_channels
+                for p_ in range(P):
+                    c = convs[p_][l]
+                    self._wg(d[p_], saved[p_][l - 1][0], cout, 9 * cin, Mp, G(c.weight), dt,
+                             conv=dict(c1=cin, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
+                wd = W.packed([c[l].weight for c in convs], "conv_dg")
+                pres = [saved[p_][l - 1][1] for p_ in range(P)]
+                dx = self._e(P, Mp, cin)
+                T.conv_dgrad(d[0], wd[0], B, g, g, 1, cout, cin, dt, out=dx[0], pre=pres[0],
+                             batch=(P, Mp * cout, wd[0].numel(), Mp * cin, stride(pres, what + " pre")))
+                d = dx
+            return d
+
+        # ---- lrp: y_hat = y_hat_pre + 0.5 tanh(t) backward, per slice (no support gradients beyond slot ms - 1)
+        dT = self._e(nbs, Mp, sw)
+        for j, i in enumerate(sl):
+            T.lrp_bwd(recs[j]["lrp"][-1], sw, dT[j], sw, Mp, sw, dt, g16=dYH.data_ptr() + i * sw * esz, ld16=M,
+                      gsum=GS.data_ptr() + i * sw * 4, ldgs=M)
+        dl = stacks(cl, [r["lrp"] for r in recs], dT, "lrp")
+        for j in reversed(range(nbs)):
+            i, c = sl[j], cl[j][0]
+            x2, c2 = self.YPT.data_ptr() + i * sw * esz, sw
+            cin, cout = M + sw * k + c2, c.out_channels
+            self._wg(dl[j], self.LMS, cout, 9 * cin, Mp, G(c.weight), dt, ldb=2 * M,
+                     conv=dict(x2=x2, c1=M + sw * k, ld2=M, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
+            T.conv_dgrad(dl[j], W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt,
+                         routes=[(dLM, M, M), (dSUP, M, sw * k), (GS.data_ptr() + i * sw * 4, M, sw)])
+        self._wg_flush()
+        # ---- GaussianConditional + quantize_ste per slice -> d mu, d sigma of every problem ([mean | scale][slice])
+        dMS = self._e(2, nbs, Mp, sw)
+        for j, i in enumerate(sl):
+            T.gc_bwd(self.Y32, M, i * sw, recs[j]["mean"][-1], recs[j]["scale"][-1], sw, self.y_noise, M, dylik, GS, M,
+                     DY, M, dMS[0, j], dMS[1, j], sw, B, HW, sw, dt)
+        dms = stacks(cm + cs, [r["mean"] for r in recs] + [r["scale"] for r in recs], dMS.view(2 * nbs, Mp, sw),
+                     "mean/scale")
+        for j in reversed(range(nbs)):
+            for t, (convs, first, routes) in enumerate(((cm[j], (self.LMS, M + sw * k, 2 * M, None, 0, 0),
+                                                         [(dLM, M, M), (dSUP, M, sw * k)]),
+                                                        (cs[j], (self.LS, M, 2 * M, lms + M * esz, sw * k, 2 * M),
+                                                         [(dLS, M, M), (dSUP2, M, sw * k)]))):
+                c, d = convs[0], dms[t * nbs + j]
+                x1, c1, ld1, x2, c2, ld2 = first
+                cin, cout = c1 + c2, c.out_channels
+                self._wg(d, x1, cout, 9 * cin, Mp, G(c.weight), dt, ldb=ld1,
+                         conv=dict(x2=x2, c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
+                T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
+            self._wg_flush()
+            self._ready(cs[j][0].bias)  # every gradient of slices >= i0 + j is final (DP hand-off per slice)
 
     def _stack_bwd_pair(self, a, b):
         """_stack_bwd of two stacks with the same layer shapes (a slice's mean and scale stacks): the data gradients

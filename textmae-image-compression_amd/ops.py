@@ -263,10 +263,12 @@ def pack_lic_stack_weight(w: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor
 
 
 def lic_stack(n, G, x1, c1, ld1, weights, biases, couts, y, ldy, y_f32, x2=None, c2=0, ld2=0, addend=None, ld_add=0,
-              lrp_src=None, ld_src=0, y2=None, ldy2=0, nb=(1, 1), strides=None, chain=None):
+              lrp_src=None, ld_src=0, y2=None, ldy2=0, nb=(1, 1), strides=None, chain=None, save=None):
     """One slice-transform stack per (problem, image) (tmae_lic_stack).  weights: packed per layer
     (pack_lic_stack_weight, problems stacked); `strides` maps operand (x1, x2, w0..w4, b0..b4, a, y, src, y2)
-    -> (s1, s2) element strides of the nb[0] x nb[1] problems.  Pointers: tensors or raw addresses."""
+    -> (s1, s2) element strides of the nb[0] x nb[1] problems.  Pointers: tensors or raw addresses.
+    save (training): {"layers": [(pre, act, (s1, s2)) per non-last layer], "t": pre-tanh f32, "t_s": (s1, s2),
+    "chain": [(pre, act, s) per lrp layer], "chain_t": ..., "chain_t_s": s} -- what the HIP backward reads."""
     a = LicStackArgs()
     a.n, a.G, a.nlayers = n, G, len(couts)
     a.nb1, a.nb2 = nb
@@ -299,6 +301,18 @@ def lic_stack(n, G, x1, c1, ld1, weights, biases, couts, y, ldy, y_f32, x2=None,
             getattr(a, f"{name[0]}_s")[int(name[1:])][:] = (s1, s2)
         else:
             getattr(a, f"{name}_s")[:] = (s1, s2)
+    if save is not None:  # training: per layer (pre, act, (s1, s2)) of the problems, and the lrp pre-tanh t
+        for l, (pre, act, st) in enumerate(save.get("layers", [])):
+            a.sv_pre[l], a.sv_act[l] = _p(pre), _p(act)
+            a.sv_s[l][:] = st
+        if save.get("t") is not None:
+            a.sv_t = _p(save["t"])
+            a.sv_t_s[:] = save.get("t_s", (0, 0))
+        for l, (pre, act, st) in enumerate(save.get("chain", [])):
+            a.csv_pre[l], a.csv_act[l] = _p(pre), _p(act)
+            a.cs_sv[l] = st
+        if save.get("chain_t") is not None:
+            a.csv_t, a.cs_t = _p(save["chain_t"]), save.get("chain_t_s", 0)
     _lib.call("tmae_lic_stack", ctypes.byref(a), _stream())
 
 

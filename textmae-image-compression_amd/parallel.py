@@ -47,6 +47,12 @@ class GradSync:
     def world(self):
         return dist.get_world_size(self.group) if dist.is_initialized() else 1
 
+    def capturable(self):
+        """can a HIP graph hold this step's collectives?  RCCL's can (backend "nccl"); gloo's go through host memory"""
+        if self.world() <= 1 and not (self.always_collective and dist.is_initialized()):
+            return True  # no collective is issued
+        return dist.get_backend(self.group) == "nccl"
+
     def _begin(self, flat):
         if self.flat is None or self.flat.data_ptr() != flat.data_ptr() or self.flat.numel() != flat.numel():
             n = flat.numel()
@@ -62,6 +68,12 @@ class GradSync:
         e.record(torch.cuda.current_stream(self.flat.device))
         return e
 
+    def _timed(self):
+        """timing events on this backward: not inside a HIP graph capture (a captured step's overlap is read from an
+        eager step of the same kernels, bench.py)"""
+        return self.timing and self.flat is not None and self.flat.is_cuda and \
+            not torch.cuda.is_current_stream_capturing()
+
     def attach(self, flat):
         """start a backward over `flat` (called by the executor before the first ready())"""
         self._begin(flat)
@@ -73,12 +85,16 @@ class GradSync:
         if W <= 1 and not (self.always_collective and dist.is_initialized()):
             return
         self.launched += 1
-        if self.timing and self.flat.is_cuda and self._first is None:
+        if self._timed() and self._first is None:
             self._first = self._event()
         if dist.get_backend(self.group) == "nccl":
+            # also under a HIP graph capture (engine.GraphedTrainStep): RCCL's kernels on the process group's stream
+            # join the capture through its event wait on the compute stream, and Work.wait() below joins it back
             op = dist.ReduceOp.AVG if self.average else dist.ReduceOp.SUM
             self._work.append(dist.all_reduce(t, op=op, group=self.group, async_op=True))
         else:  # gloo (CPU rehearsal, or several ranks sharing one GPU in tests): SUM then scale
+            if t.is_cuda and torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("GradSync: a gloo all-reduce (host-staged) cannot be captured into a HIP graph")
             _host_all_reduce_sum(t, self.group)
             if self.average:
                 t.div_(W)
@@ -94,7 +110,7 @@ class GradSync:
 
     def finish(self):
         """launch the remaining buckets and order the compute stream after every collective"""
-        timed = self.timing and self.flat is not None and self.flat.is_cuda
+        timed = self._timed()
         end = self._event() if timed else None  # the backward's last kernel is enqueued before this point
         self._finishing = True
         try:

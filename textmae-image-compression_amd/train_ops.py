@@ -131,11 +131,15 @@ def dgrad_linear(dy, wt, M, N, K, dtype, out=None, pre=None, acc32=None, ldy=Non
 
 
 def conv_dgrad(dy, wd, n, H, W, stride, cout, cin, dtype, out=None, pre=None, ldy=None, ldo=None, ldp=None,
-               routes=None, out_f32=None, second=None):
+               routes=None, out_f32=None, second=None, batch=None):
     """dx [n*H*W][cin] of a 3x3 conv from dy [n*Ho*Wo][cout]; wd = weight as [cin][3][3][cout] (dtype).
     routes: [(acc_f32, ld, ncols), ...] (<= 3, f32 +=, consecutive input-channel ranges).
-    second = (dy2, wd2, out2, pre2): a second problem of the same shape and layout in the same launch (no routes)"""
+    second = (dy2, wd2, out2, pre2): a second problem of the same shape and layout in the same launch (no routes).
+    batch = (nb, s_dy, s_wd, s_out, s_pre): nb problems, problem j's dy / wd / out / pre j * s elements past the
+    first's (no routes)"""
     a = ConvDgradArgs()
+    if batch is not None:
+        a.nb, a.s_dy, a.s_wd, a.s_out, a.s_pre = batch
     if second is not None:
         def off(t2, t1, what):
             if t2.dtype != t1.dtype:

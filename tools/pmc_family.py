@@ -21,9 +21,14 @@ def per_family(path, counter):
     for r in csv.DictReader(open(path)):
         if r.get("Counter_Name") != counter:
             continue
-        disp[r["Dispatch_Id"]] += float(r["Counter_Value"])
-        names[r["Dispatch_Id"]] = r["Kernel_Name"]
-    fwd = sum(1 for d, n in names.items() if "ids_shuffle" in n) or 1
+        disp[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+        names[int(r["Dispatch_Id"])] = r["Kernel_Name"]
+    # tools/fwd_only.py runs whole forwards and nothing else: the first one (weight init and re-layout, workspace
+    # set-up) is a warm-up, so counting starts at the SECOND forward's ids_shuffle dispatch
+    starts = sorted(d for d, n in names.items() if "ids_shuffle" in n)
+    first = starts[1] if len(starts) > 1 else (starts[0] if starts else 0)
+    disp = {d: v for d, v in disp.items() if d >= first}
+    fwd = max(len(starts) - 1, 1)
     fam = defaultdict(lambda: [0, 0.0])
     for d, v in disp.items():
         f = family(names[d])
@@ -50,9 +55,9 @@ def main():
                                 "hbm_bytes_per_launch": int(byts / n), "hbm_bytes_per_fwd": int(byts / n * lpf)}
     d = out["per_family"].get(fam)
     out["hbm_bytes_per_launch"] = d["hbm_bytes_per_launch"] if d else None
-    out["note"] = ("FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, summed over the family's dispatches of an "
-                   "eager (--no-graph --no-roofline) bench run of whole forwards, divided by its launch count; Infinity-Cache hits are counted as "
-                   "fetches by these counters")
+    out["note"] = ("FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, summed over the family's dispatches of a run of "
+                   "whole eager forwards and nothing else (tools/fwd_only.py; dispatches before the first ids_shuffle "
+                   "dropped), divided by its launch count; Infinity-Cache hits are counted as fetches by these counters")
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 4:
         json.dump(out, open(sys.argv[4], "w"), indent=1)
