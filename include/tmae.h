@@ -403,9 +403,14 @@ typedef struct tmae_wgrad_args {
   float* bias_out; int bias_accumulate;
   int slot_div;  /* split-K sized for 1 / slot_div of the CU slots (0 or 1: the whole chip); a weight gradient on
                     a side stream shares the chip, and fewer splits write and reduce fewer partial slabs */
+  /* nb > 1: nb problems of the same shape in one launch (the same layer of several slices' stacks), problem j's
+   * a / b / b2 / out / bias_out at j * s_a / s_b / s_b2 / s_out / s_bias elements past the first's (work holds
+   * nb problems' slabs: tmae_wgrad_workspace x nb) */
+  int nb; long long s_a, s_b, s_b2, s_out, s_bias;
 } tmae_wgrad_args;
 int tmae_wgrad(const tmae_wgrad_args* args, int dtype, void* stream);
 long long tmae_wgrad_workspace(int M, int N, int K, int dtype);
+long long tmae_wgrad_workspace_nb(int M, int N, int K, int dtype, int slot_div, int nb);
 
 /* data gradient of y = x w^T: dx[M][K] = dy[M][N] wt[K][N]^T (wt = w transposed, dtype); dy rows remapped
  * like tmae_linear_fwd.  out (dtype, or f32 with out_f32) = dx * gelu'(pre) when pre is given (the GELU

@@ -103,6 +103,42 @@ def test_wgrad_conv(T, stride, dt):
     check("_rel:out", _rel(out, ref), (1e-5 if dt == torch.float32 else 2e-3))
 
 
+@pytest.mark.parametrize("two_src", [False, True])
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_wgrad_conv_batched(T, two_src, dt):
+    """tmae_wgrad_args.nb: the weight (and bias) gradients of several same-shape 3x3 convs in ONE launch, each
+    problem's dy / input / second input / output / bias at constant element strides (a shared input at stride 0,
+    as the slices' first layers read LMS), every problem against its own f64 reference"""
+    P, n, H, cin, cout = 4, 2, 12, 48, 40
+    c2 = 16 if two_src else 0
+    xs = [_rnd(n, cin - c2, H, H, seed=40 + j) for j in range(P)]
+    xs[1] = xs[0] if two_src else xs[1]
+    x2s = [_rnd(n, c2, H, H, seed=50 + j) for j in range(P)] if two_src else None
+    dys = [_rnd(n, cout, H, H, seed=60 + j) for j in range(P)]
+    q = lambda t: t.to(dt).float()  # noqa: E731
+    nhwc = lambda t: q(t).permute(0, 2, 3, 1).contiguous().reshape(-1, t.shape[1])  # noqa: E731
+    if two_src:  # the first input shared by every problem (stride 0), the second one per problem
+        x1 = nhwc(xs[0]).cuda().to(dt)
+        x2 = torch.stack([nhwc(t) for t in x2s]).cuda().to(dt)
+        refs_x = [torch.cat([q(xs[0]), q(x2s[j])], 1) for j in range(P)]
+    else:
+        x1 = torch.stack([nhwc(t) for t in xs]).cuda().to(dt)
+        refs_x = [q(xs[j]) for j in range(P)]
+    dy = torch.stack([nhwc(t) for t in dys]).cuda().to(dt)
+    out = torch.empty(P, cout, cin, 3, 3, device="cuda")
+    bias = torch.empty(P, cout, device="cuda")
+    npix = n * H * H
+    conv = dict(c1=cin - c2, H=H, W=H, cin=cin, x2=x2[0] if two_src else None, ld2=c2)
+    T.wgrad(dy[0], x1 if two_src else x1[0], cout, 9 * cin, npix, out[0], dt, conv=conv, layout="conv", bias=bias[0],
+            ldb=cin - c2, batch=(P, npix * cout, 0 if two_src else npix * cin, npix * c2, cout * cin * 9, cout))
+    torch.cuda.synchronize()
+    for j in range(P):
+        ref = torch.nn.grad.conv2d_weight(refs_x[j].double(), (cout, cin, 3, 3), q(dys[j]).double(), padding=1).float()
+        check("_rel:batched_w", _rel(out[j], ref), (1e-5 if dt == torch.float32 else 2e-3))
+        rb = q(dys[j]).double().sum((0, 2, 3)).float()
+        check("_rel:batched_b", _rel(bias[j], rb), (1e-5 if dt == torch.float32 else 1e-4))
+
+
 # bias gradient formed inside the weight-gradient GEMM (bf16: MFMAs against an all-ones fragment, one owner
 # wave per fragment, folded in split order by tn_reduce; f32: column sums after the GEMM).  Shapes: one and
 # many N tiles, M past the last whole M tile, more than 16 K splits (the 16 / 4-split fold), the 8-wave

@@ -50,6 +50,7 @@ class WgradArgs(ctypes.Structure):
         ("out", P), ("o_base", LL), ("o_sm", LL), ("o_sc", LL), ("o_st", LL), ("o_cp", I), ("accumulate", I),
         ("bias_out", P), ("bias_accumulate", I),
         ("slot_div", I),
+        ("nb", I), ("s_a", LL), ("s_b", LL), ("s_b2", LL), ("s_out", LL), ("s_bias", LL),
     ]
 
 
@@ -197,6 +198,7 @@ SIGNATURES = {
 
 # entry points that return a value rather than a status
 VALUE_FUNCS = {"tmae_wgrad_workspace": ([I, I, I, I], ctypes.c_longlong),
+               "tmae_wgrad_workspace_nb": ([I, I, I, I, I, I], ctypes.c_longlong),
                "tmae_metrics_workspace": ([I, I, I, I], ctypes.c_longlong),
                "tmae_image_scores_workspace": ([I, I, I, I], ctypes.c_longlong),
                "tmae_qkv_attn_supported": ([I, I, I], ctypes.c_int)}

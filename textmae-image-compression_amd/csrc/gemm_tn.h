@@ -25,6 +25,8 @@
 template <typename T> struct KDenseSrc {
   const T* p;
   int ld, cols, G, Gs, off;
+  long long sb = 0;  // element offset of problem z (batched launches: blockIdx.z)
+  __device__ void batch(int z) { p += z * sb; }
   __device__ const void* addr(int k, int c) const {
     if (c >= cols) return g_tmae_zero_page;
     const int sk = (k / G) * Gs + off + (k % G);
@@ -54,6 +56,11 @@ template <typename T> struct KConvSrc {
   const T* x1;
   const T* x2;
   int c1, ld1, ld2, Cin, H, W, Ho, Wo, stride, cols;
+  long long sb1 = 0, sb2 = 0;  // element offsets of problem z's x1 / x2 (batched launches)
+  __device__ void batch(int z) {
+    x1 += z * sb1;
+    if (x2) x2 += z * sb2;
+  }
   __device__ const void* addr(int k, int c) const {
     if (c >= cols) return g_tmae_zero_page;
     const int tap = c / Cin, ci = c - tap * Cin;
@@ -141,7 +148,11 @@ gemm_tn_bf16_kernel(AS as, BS bs, EpiSplitWs epi, int M, int N, int K, int kchun
   tile_order(xcd_remap(blockIdx.x, gridDim.x), ntn, ntm, tn, tm);
   const int k0 = blockIdx.y * kchunk, k1 = min(K, k0 + kchunk);
   const int nk = k1 > k0 ? (k1 - k0 + BK - 1) / BK : 0;
-  epi.ws += (size_t)blockIdx.y * epi.slab;
+  // problem z of a batched launch: its sources, its [splits] slabs and its bias slab
+  as.batch(blockIdx.z);
+  bs.batch(blockIdx.z);
+  epi.ws += ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * epi.slab;
+  if (epi.bws) epi.bws += (size_t)blockIdx.z * gridDim.y * M;
   // bias fragments owned by this wave (wave-uniform): j with j % P == r % P
   const int bias_P = ntn * WGN, bias_r = tn * WGN + wn;
 
@@ -302,7 +313,7 @@ gemm_tn_f32_kernel(AS as, BS bs, EpiSplitWs epi, int M, int N, int K, int kchunk
 // ------------------------------------------------------------------ launch
 struct TnPlan { int bn, bm, nw, splits, kchunk; };
 
-static inline TnPlan tn_plan(int M, int N, int K, bool bf, int slot_div = 1) {
+static inline TnPlan tn_plan(int M, int N, int K, bool bf, int slot_div = 1, int nb = 1) {
   TnPlan p;
   if (!bf) {
     p.bn = 64; p.bm = 64; p.nw = 4;
@@ -312,7 +323,7 @@ static inline TnPlan tn_plan(int M, int N, int K, bool bf, int slot_div = 1) {
     if (u256 > 0.7 && t256 * 8 >= 64) { p.bn = 256; p.bm = 256; p.nw = 8; }
     else { p.bn = 128; p.bm = 128; p.nw = 4; }
   }
-  const int tiles = ceil_div(N, p.bn) * ceil_div(M, p.bm);
+  const int tiles = ceil_div(N, p.bn) * ceil_div(M, p.bm) * std::max(1, nb);  // nb problems share the slots
   const int slots = (p.nw == 8 ? 256 : 512) / std::max(1, slot_div);
   const int kmin = bf ? 256 : 128;
   // splits: as many as fit ONE round of the slots (floor): with the ceiling, tiles * splits overshot the
@@ -330,22 +341,22 @@ static inline TnPlan tn_plan(int M, int N, int K, bool bf, int slot_div = 1) {
 // bws (bias slab [splits][M]) non-null: the kernel also forms the column sums of A (BIAS instantiation)
 template <class AS, class BS>
 static int launch_tn_bf16(const TnPlan& p, const AS& as, const BS& bs, float* ws, float* bws, int M, int N, int K,
-                          hipStream_t st) {
+                          hipStream_t st, int nb = 1) {
   const int tiles = ceil_div(N, p.bn) * ceil_div(M, p.bm);
   EpiSplitWs e{ws, N, (long long)M * N, bws, M};
   if (p.nw == 8) {
     if (bws)
-      hipLaunchKernelGGL((gemm_tn_bf16_kernel<256, 256, 2, 8, true, AS, BS>), dim3(tiles, p.splits), dim3(512), 0, st,
+      hipLaunchKernelGGL((gemm_tn_bf16_kernel<256, 256, 2, 8, true, AS, BS>), dim3(tiles, p.splits, nb), dim3(512), 0, st,
                          as, bs, e, M, N, K, p.kchunk);
     else
-      hipLaunchKernelGGL((gemm_tn_bf16_kernel<256, 256, 2, 8, false, AS, BS>), dim3(tiles, p.splits), dim3(512), 0, st,
+      hipLaunchKernelGGL((gemm_tn_bf16_kernel<256, 256, 2, 8, false, AS, BS>), dim3(tiles, p.splits, nb), dim3(512), 0, st,
                          as, bs, e, M, N, K, p.kchunk);
   } else {
     if (bws)
-      hipLaunchKernelGGL((gemm_tn_bf16_kernel<128, 128, 2, 4, true, AS, BS>), dim3(tiles, p.splits), dim3(256), 0, st,
+      hipLaunchKernelGGL((gemm_tn_bf16_kernel<128, 128, 2, 4, true, AS, BS>), dim3(tiles, p.splits, nb), dim3(256), 0, st,
                          as, bs, e, M, N, K, p.kchunk);
     else
-      hipLaunchKernelGGL((gemm_tn_bf16_kernel<128, 128, 2, 4, false, AS, BS>), dim3(tiles, p.splits), dim3(256), 0, st,
+      hipLaunchKernelGGL((gemm_tn_bf16_kernel<128, 128, 2, 4, false, AS, BS>), dim3(tiles, p.splits, nb), dim3(256), 0, st,
                          as, bs, e, M, N, K, p.kchunk);
   }
   TMAE_LAUNCH_CHECK("tmae_wgrad");

@@ -6,7 +6,8 @@
 
 static int tmae_wgrad_reduce(const float* ws, int splits, int M, int N, float* out, long long base, long long sm,
                              long long sc, long long st, int cp, int accumulate, const float* bws, float* bias_out,
-                             int bias_accumulate, hipStream_t s);
+                             int bias_accumulate, hipStream_t s, int nb = 1, long long s_out = 0,
+                             long long s_bias = 0);
 static int colsum_into(const void* x, int x_dtype, int ld, int rows, int C, int row_group, int group_stride,
                        int row_offset, float* work, long long work_elems, float* out, int accumulate, hipStream_t st);
 static int tmae_ln_fold(const float* part, int waves, int D, float* dg, float* db, int accumulate, hipStream_t st);
@@ -49,17 +50,34 @@ __device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) {
 
 // ================================================================== weight gradients (split-K TN GEMM)
 template <typename T>
-static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
+static int wgrad_t(const tmae_wgrad_args& a0, hipStream_t st) {
   const int e = Elt<T>::EPC;
+  const int nb = a0.nb > 1 ? a0.nb : 1;
+  if (nb > 1 && sizeof(T) == 4) {
+    // the f32 parity path: one launch per problem (same per-problem sums as the bf16 batched launch's plan)
+    for (int j = 0; j < nb; ++j) {
+      tmae_wgrad_args b = a0;
+      b.nb = 1;
+      b.a = (const T*)a0.a + j * a0.s_a;
+      b.b = (const T*)a0.b + j * a0.s_b;
+      if (a0.b2) b.b2 = (const T*)a0.b2 + j * a0.s_b2;
+      b.out = a0.out + j * a0.s_out;
+      if (a0.bias_out) b.bias_out = a0.bias_out + j * a0.s_bias;
+      const int rc = wgrad_t<T>(b, st);
+      if (rc != TMAE_OK) return rc;
+    }
+    return TMAE_OK;
+  }
+  const tmae_wgrad_args& a = a0;
   TMAE_REQUIRE(a.M % e == 0 && a.N % e == 0 && a.lda % e == 0, "tmae_wgrad: M=%d / N=%d / lda must be multiples of %d",
                a.M, a.N, e);
   TMAE_REQUIRE(a.a_G > 0 && a.o_cp > 0, "tmae_wgrad: bad row group / column period");
   const bool bf = sizeof(T) == 2;
-  const TnPlan p = tn_plan(a.M, a.N, a.K, bf, a.slot_div);
-  const long long slabs = (long long)p.splits * a.M * a.N;
-  TMAE_REQUIRE(slabs + (long long)p.splits * a.M <= a.work_elems, "tmae_wgrad: workspace too small (%lld < %lld)",
-               a.work_elems, slabs + (long long)p.splits * a.M);
-  // bias column sums: in the bf16 kernel (slab [splits][M] after the partial tiles); the f32 parity path
+  const TnPlan p = tn_plan(a.M, a.N, a.K, bf, a.slot_div, nb);
+  const long long slabs = (long long)nb * p.splits * a.M * a.N;
+  TMAE_REQUIRE(slabs + (long long)nb * p.splits * a.M <= a.work_elems, "tmae_wgrad: workspace too small (%lld < %lld)",
+               a.work_elems, slabs + (long long)nb * p.splits * a.M);
+  // bias column sums: in the bf16 kernel (slabs [nb][splits][M] after the partial tiles); the f32 parity path
   // runs the column-sum kernels on A after the GEMM
   float* bws = (a.bias_out && bf) ? a.work + slabs : nullptr;
   // KDenseSrc::addr_in forms element offsets in 32-bit unsigned arithmetic: the last source row the K range
@@ -72,6 +90,7 @@ static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
   TMAE_REQUIRE(last_elem(a.a_G, a.a_Gs, a.a_off, a.lda, a.M) < (1ull << 32),
                "tmae_wgrad: operand A spans 2^32 elements or more (32-bit source offsets)");
   KDenseSrc<T> as{(const T*)a.a, a.lda, a.M, a.a_G, a.a_Gs, a.a_off};
+  as.sb = a.s_a;
   int rc;
   if (a.b_conv) {
     TMAE_REQUIRE(a.b_Cin % e == 0 && a.b_c1 % e == 0 && a.ldb % e == 0, "tmae_wgrad: conv channels");
@@ -81,19 +100,21 @@ static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
     bs.x1 = (const T*)a.b; bs.x2 = (const T*)a.b2; bs.c1 = a.b_c1; bs.ld1 = a.ldb; bs.ld2 = a.b_ld2; bs.Cin = a.b_Cin;
     bs.H = a.b_H; bs.W = a.b_W; bs.stride = a.b_stride;
     bs.Ho = (a.b_H + 2 - 3) / a.b_stride + 1; bs.Wo = (a.b_W + 2 - 3) / a.b_stride + 1; bs.cols = a.N;
-    rc = bf ? launch_tn_bf16(p, as, bs, a.work, bws, a.M, a.N, a.K, st)
+    bs.sb1 = a.s_b; bs.sb2 = a.s_b2;
+    rc = bf ? launch_tn_bf16(p, as, bs, a.work, bws, a.M, a.N, a.K, st, nb)
             : launch_tn_f32(p, as, bs, a.work, a.M, a.N, a.K, st);
   } else {
     TMAE_REQUIRE(a.ldb % e == 0 && a.b_G > 0, "tmae_wgrad: ldb");
     TMAE_REQUIRE(last_elem(a.b_G, a.b_Gs, a.b_off, a.ldb, a.N) < (1ull << 32),
                  "tmae_wgrad: operand B spans 2^32 elements or more (32-bit source offsets)");
     KDenseSrc<T> bs{(const T*)a.b, a.ldb, a.N, a.b_G, a.b_Gs, a.b_off};
-    rc = bf ? launch_tn_bf16(p, as, bs, a.work, bws, a.M, a.N, a.K, st)
+    bs.sb = a.s_b;
+    rc = bf ? launch_tn_bf16(p, as, bs, a.work, bws, a.M, a.N, a.K, st, nb)
             : launch_tn_f32(p, as, bs, a.work, a.M, a.N, a.K, st);
   }
   if (rc != TMAE_OK) return rc;
   rc = tmae_wgrad_reduce(a.work, p.splits, a.M, a.N, a.out, a.o_base, a.o_sm, a.o_sc, a.o_st, a.o_cp, a.accumulate,
-                         bws, bws ? a.bias_out : nullptr, a.bias_accumulate, st);
+                         bws, bws ? a.bias_out : nullptr, a.bias_accumulate, st, nb, a.s_out, a.s_bias);
   if (rc != TMAE_OK || !a.bias_out || bf) return rc;
   // f32: the partial-tile slabs are consumed; their space is the column sums' workspace
   return colsum_into(a.a, TMAE_F32, a.lda, a.K, a.M, a.a_G, a.a_Gs, a.a_off, a.work, a.work_elems, a.bias_out,
@@ -109,9 +130,14 @@ static int wgrad_t(const tmae_wgrad_args& a, hipStream_t st) {
 __global__ void __launch_bounds__(256)
 tn_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N, float* __restrict__ out, long long base,
                  long long sm, long long sc, long long st, int cp, int accumulate, const float* __restrict__ bws,
-                 float* __restrict__ bias_out, int bias_accumulate) {
+                 float* __restrict__ bias_out, int bias_accumulate, long long s_out, long long s_bias) {
   const long long t = (long long)blockIdx.x * 256 + threadIdx.x;
   const long long tot = (long long)M * N, tot4 = tot >> 2;
+  // problem blockIdx.y of a batched weight gradient: its slabs, its bias slab, its parameter
+  ws += (size_t)blockIdx.y * splits * tot;
+  out += blockIdx.y * s_out;
+  if (bws) bws += (size_t)blockIdx.y * splits * M;
+  if (bias_out) bias_out += blockIdx.y * s_bias;
   if (t >= tot4) {
     const long long m = t - tot4;
     if (!bias_out || m >= M) return;
@@ -180,11 +206,11 @@ tn_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N, float* 
 
 static int tmae_wgrad_reduce(const float* ws, int splits, int M, int N, float* out, long long base, long long sm,
                              long long sc, long long st, int cp, int accumulate, const float* bws, float* bias_out,
-                             int bias_accumulate, hipStream_t s) {
+                             int bias_accumulate, hipStream_t s, int nb, long long s_out, long long s_bias) {
   const long long tot = (long long)M * N / 4 + (bias_out ? M : 0);  // threads (N % 8 == 0: wgrad_t)
   if (tot == 0) return TMAE_OK;
-  hipLaunchKernelGGL(tn_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, ws, splits, M, N, out,
-                     base, sm, sc, st, cp, accumulate, bws, bias_out, bias_accumulate);
+  hipLaunchKernelGGL(tn_reduce_kernel, dim3((unsigned)((tot + 255) / 256), nb), dim3(256), 0, s, ws, splits, M, N, out,
+                     base, sm, sc, st, cp, accumulate, bws, bias_out, bias_accumulate, s_out, s_bias);
   TMAE_LAUNCH_CHECK("tmae_wgrad");
 }
 
@@ -198,6 +224,15 @@ extern "C" int tmae_wgrad(const tmae_wgrad_args* a, int dtype, void* stream) {
 extern "C" long long tmae_wgrad_workspace(int M, int N, int K, int dtype) {
   const TnPlan p = tn_plan(M, N, K, dtype == TMAE_BF16);
   return (long long)p.splits * M * N + (long long)p.splits * M;  // partial tiles + bias column-sum slab
+}
+
+/* the same for nb problems of one batched launch at 1 / slot_div of the slots */
+extern "C" long long tmae_wgrad_workspace_nb(int M, int N, int K, int dtype, int slot_div, int nb) {
+  nb = nb > 1 ? nb : 1;
+  const TnPlan p = tn_plan(M, N, K, dtype == TMAE_BF16, slot_div, nb);
+  const TnPlan p1 = tn_plan(M, N, K, dtype == TMAE_BF16);
+  const long long one = (long long)p1.splits * M * N + (long long)p1.splits * M;  // the f32 per-problem path
+  return std::max((long long)nb * p.splits * ((long long)M * N + M), one);
 }
 
 // ================================================================== data gradients (NT core on transposed weights)

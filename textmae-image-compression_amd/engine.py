@@ -12,6 +12,8 @@ Logging (MetricLogger / TensorBoard) is out of scope.
 """
 from __future__ import annotations
 
+import time
+
 import torch
 
 from . import distributed
@@ -125,6 +127,14 @@ class GraphedTrainStep:
 
         bump_versions(self.params)
         self._staging = reserve_capture_staging()  # the graph's copy nodes read it at every replay
+        sync = getattr(self.model, "grad_sync", None)
+        if sync is not None and sync.world() >= 1 and (sync.world() > 1 or sync.always_collective):
+            # the warm-up step's RCCL works sit in the process group's watchdog until it sees them complete; it
+            # queries their end events, recorded on the process group's stream -- which the capture below turns
+            # into a capturing stream, where such a query fails (hipErrorCapturedEvent) and takes the watchdog
+            # down.  Let every eager collective finish and the watchdog (100 ms poll) retire it first.
+            torch.cuda.synchronize()
+            time.sleep(0.5)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             out = self._step()

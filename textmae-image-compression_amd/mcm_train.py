@@ -221,6 +221,9 @@ class _VitTrainBase:
     needs) / backward."""
 
     _side = None          # side stream of the weight gradients (_wg), made by _side_begin
+    # split-K of the ViT blocks' weight gradients sized for 1 / VIT_WG_SLOT_DIV of the CU slots (test / A-B hook;
+    # the side stream shares the chip with the data-gradient chain)
+    VIT_WG_SLOT_DIV = _SIDE_SLOT_DIV
     _side_used = False
     _pending = ()
     _queued = ()
@@ -299,8 +302,45 @@ class _VitTrainBase:
         a block): a captured graph pays a cross-queue dependency per fork.  `a` (this layer's output gradient, a
         fresh tensor of the chain) is kept alive until the join; every other operand is a saved activation."""
         if self._side is None:  # same split plan as the side stream's, so both modes sum in the same order
-            return T.wgrad(a, *args, slot_div=_SIDE_SLOT_DIV, **kw)
+            kw.setdefault("slot_div", _SIDE_SLOT_DIV)
+            return T.wgrad(a, *args, **kw)
         self._queued.append((a, args, kw))
+
+    def _wg_many(self, items, M, N, K, dt, conv=None, **kw):
+        """the weight gradients of several problems of one shape (the same layer of several slices' stacks): ONE
+        batched launch (tmae_wgrad_args.nb) when every operand and output sits at a constant element stride from
+        the previous problem's, else one launch each.  items: dicts a (output gradient), b (layer input), out / bias
+        (the parameter's gradient views), x2 (conv second input pointer or None)."""
+        P = len(items)
+
+        def ptr(v):
+            return v if isinstance(v, int) else v.data_ptr()
+
+        def stride(key, esz):
+            vals = [it.get(key) for it in items]
+            if vals[0] is None:
+                return 0 if all(v is None for v in vals) else None
+            d = {ptr(b) - ptr(a) for a, b in zip(vals, vals[1:])}
+            if P == 1:
+                return 0
+            if len(d) != 1 or next(iter(d)) % esz:
+                return None
+            return next(iter(d)) // esz
+
+        eb = items[0]["b"].element_size()
+        st = [stride("a", items[0]["a"].element_size()), stride("b", eb), stride("x2", eb), stride("out", 4),
+              stride("bias", 4)]
+        if P > 1 and None not in st:
+            # the launch reads problems 1.. through pointer strides: keep their output gradients (fresh tensors of the
+            # chain, unlike the saved activations) alive until the join, as _wg_flush does for the first one's
+            self._keep.extend(it["a"] for it in items[1:] if not isinstance(it["a"], int))
+            it = items[0]
+            cv = dict(conv, x2=it.get("x2")) if conv is not None else None
+            self._wg(it["a"], it["b"], M, N, K, it["out"], dt, bias=it.get("bias"), conv=cv, batch=(P, *st), **kw)
+            return
+        for it in items:
+            cv = dict(conv, x2=it.get("x2")) if conv is not None else None
+            self._wg(it["a"], it["b"], M, N, K, it["out"], dt, bias=it.get("bias"), conv=cv, **kw)
 
     def _wg_flush(self, last=False):
         """close the queued group: record its fork point on the compute stream now, but enqueue the group on the
@@ -317,7 +357,8 @@ class _VitTrainBase:
             self._side.wait_event(ev)
             with torch.cuda.stream(self._side):
                 for a, args, kw in group:
-                    T.wgrad(a, *args, ws_slot=4, slot_div=_SIDE_SLOT_DIV, **kw)
+                    kw.setdefault("slot_div", _SIDE_SLOT_DIV)
+                    T.wgrad(a, *args, ws_slot=4, **kw)
                     self._keep.append(a)
                     self._side_calls += 1
             self._side_used = True
@@ -362,11 +403,12 @@ class _VitTrainBase:
         H = blk.attn.num_heads
         f32 = dt == torch.float32
         # fc2 (+ GELU of fc1 in the data-gradient epilogue)
-        self._wg(dres_op, s.h, D, hid, rows, G(blk.mlp.fc2.weight), dt)  # fc2.bias: folded into norm2's backward
+        sd = self.VIT_WG_SLOT_DIV
+        self._wg(dres_op, s.h, D, hid, rows, G(blk.mlp.fc2.weight), dt, slot_div=sd)  # fc2.bias: in norm2's backward
         dh = self._e(rows, hid)
         T.dgrad_linear(dres_op, W.t(blk.mlp.fc2.weight), rows, D, hid, dt, out=dh, pre=s.hpre)
         # fc1
-        self._wg(dh, s.a2, hid, D, rows, G(blk.mlp.fc1.weight), dt, bias=G(blk.mlp.fc1.bias))
+        self._wg(dh, s.a2, hid, D, rows, G(blk.mlp.fc1.weight), dt, bias=G(blk.mlp.fc1.bias), slot_div=sd)
         da2 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dh, W.t(blk.mlp.fc1.weight), rows, hid, D, dt, out=da2)
         # norm2 + residual
@@ -375,7 +417,7 @@ class _VitTrainBase:
         T.layernorm_bwd(s.xmid, blk.norm2.weight, da2, dmid, rows, D, blk.norm2.eps, G(blk.norm2.weight),
                         G(blk.norm2.bias), dres=dres, dxop=None if f32 else dmid_op, dres_colsum=G(blk.mlp.fc2.bias))
         # proj
-        self._wg(dmid_op, s.att, D, D, rows, G(blk.attn.proj.weight), dt)  # proj.bias: folded into norm1's backward
+        self._wg(dmid_op, s.att, D, D, rows, G(blk.attn.proj.weight), dt, slot_div=sd)  # proj.bias: in norm1's bwd
         datt = self._e(rows, D)
         T.dgrad_linear(dmid_op, W.t(blk.attn.proj.weight), rows, D, D, dt, out=datt)
         # attention core
@@ -383,7 +425,7 @@ class _VitTrainBase:
         T.mha_bwd(s.qkv, s.att, datt, s.lse, dqkv, B, Tn, H, D // H, blk.attn.scale, dt)
         # qkv
         self._wg(dqkv, s.a1, 3 * D, D, rows, G(blk.attn.qkv.weight), dt,
-                bias=G(blk.attn.qkv.bias) if blk.attn.qkv.bias is not None else None)
+                 bias=G(blk.attn.qkv.bias) if blk.attn.qkv.bias is not None else None, slot_div=sd)
         da1 = torch.empty((rows, D), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dqkv, W.t(blk.attn.qkv.weight), rows, 3 * D, D, dt, out=da1)
         # norm1 + residual
@@ -1081,6 +1123,7 @@ class TrainExec(_VitTrainBase):
         dSUP2 = self._z(Mp, M)  # also without the stream: the same sums in the same order either way
         main = torch.cuda.current_stream(self.device) if conc else None
         joined = None
+        deferred = []  # eager only: (slice, mean stack's, scale stack's layer 4..1 weight gradients)
         GS = torch.empty((Mp, M), dtype=torch.float32, device=self.device)
         # slices ms..S-1 were run batched in the forward (they condition on the fixed support slots 0..ms-1): their
         # backward is batched too, every data gradient of layers 4..1 one launch for all of them
@@ -1118,20 +1161,29 @@ class TrainExec(_VitTrainBase):
                 self._stack_bwd_pair(mean_args, scale_args)
                 self._ready(_convs(m.cc_transform_scale[i])[0].bias)
                 continue
-            # eager: the scale stack on its own stream, the mean stack first on the compute stream
+            # eager: the scale stack on its own stream, the mean stack first on the compute stream.  Their layers
+            # 4..1 weight gradients wait for the final join and then run as the same 2-problem launches a captured
+            # step issues (_stack_bwd_pair), so eager and graphed steps sum them with one split plan; the DP
+            # hand-offs of these slices follow them.
             fork = torch.cuda.Event()
             fork.record(main)
-            self._stack_bwd(*mean_args)
+            im, is_ = [], []
+            self._stack_bwd(*mean_args, defer=im)
             ss = self._scale_stream
             ss.wait_event(fork)
             with torch.cuda.stream(ss):
-                self._stack_bwd(*scale_args)
+                self._stack_bwd(*scale_args, defer=is_)
             joined = torch.cuda.Event()
             joined.record(ss)
             self._keep.append(dSG)  # read on the scale stream; freed after the backward's join
-            self._ready(_convs(m.cc_transform_scale[i])[0].bias)
+            deferred.append((i, im, is_))
         if joined is not None:
             main.wait_event(joined)
+        for i, im, is_ in deferred:
+            for (ia, shp), (ib, _) in zip(im, is_):
+                self._wg_many([ia, ib], *shp, layout="conv")
+            self._wg_flush()
+            self._ready(_convs(m.cc_transform_scale[i])[0].bias)
         return DY, dLM, dLS
 
     def _batched_bwd(self, i0, nbs, dYH, dylik, DY, dLM, dLS, dSUP, dSUP2, GS):
@@ -1159,16 +1211,19 @@ class TrainExec(_VitTrainBase):
                 raise RuntimeError(f"batched slice backward: {what} not at a constant stride")
             return (next(iter(d)) // e) if d else 0
 
-        def stacks(convs, saved, dtop, what):
-            """layers 4..1 of len(convs) same-shape stacks, problem p's saved activations saved[p]; dtop [P][Mp][cout]"""
+        def stacks(convs, saved, dtop, what, groups=1):
+            """layers 4..1 of len(convs) same-shape stacks, problem p's saved activations saved[p]; dtop [P][Mp][cout];
+            the weight gradients of each of `groups` consecutive problem groups (lrp / mean / scale) as one batched
+            launch per layer"""
             P = len(convs)
             d = dtop
             for l in range(4, 0, -1):
                 cin, cout = convs[0][l].in_channels, convs[0][l].out_channels
-                for p_ in range(P):
-                    c = convs[p_][l]
-                    self._wg(d[p_], saved[p_][l - 1][0], cout, 9 * cin, Mp, G(c.weight), dt,
-                             conv=dict(c1=cin, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
+                q = P // groups
+                for g0 in range(0, P, q):
+                    self._wg_many([{"a": d[p_], "b": saved[p_][l - 1][0], "out": G(convs[p_][l].weight),
+                                    "bias": G(convs[p_][l].bias)} for p_ in range(g0, g0 + q)],
+                                  cout, 9 * cin, Mp, dt, conv=dict(c1=cin, H=g, W=g, cin=cin), layout="conv")
                 wd = W.packed([c[l].weight for c in convs], "conv_dg")
                 pres = [saved[p_][l - 1][1] for p_ in range(P)]
                 dx = self._e(P, Mp, cin)
@@ -1183,12 +1238,13 @@ class TrainExec(_VitTrainBase):
             T.lrp_bwd(recs[j]["lrp"][-1], sw, dT[j], sw, Mp, sw, dt, g16=dYH.data_ptr() + i * sw * esz, ld16=M,
                       gsum=GS.data_ptr() + i * sw * 4, ldgs=M)
         dl = stacks(cl, [r["lrp"] for r in recs], dT, "lrp")
+        cin, cout = M + sw * k + sw, cl[0][0].out_channels
+        self._wg_many([{"a": dl[j], "b": self.LMS, "x2": self.YPT.data_ptr() + i * sw * esz, "out": G(cl[j][0].weight),
+                        "bias": G(cl[j][0].bias)} for j, i in enumerate(sl)],
+                      cout, 9 * cin, Mp, dt, conv=dict(c1=M + sw * k, ld2=M, H=g, W=g, cin=cin), layout="conv",
+                      ldb=2 * M)
         for j in reversed(range(nbs)):
             i, c = sl[j], cl[j][0]
-            x2, c2 = self.YPT.data_ptr() + i * sw * esz, sw
-            cin, cout = M + sw * k + c2, c.out_channels
-            self._wg(dl[j], self.LMS, cout, 9 * cin, Mp, G(c.weight), dt, ldb=2 * M,
-                     conv=dict(x2=x2, c1=M + sw * k, ld2=M, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
             T.conv_dgrad(dl[j], W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt,
                          routes=[(dLM, M, M), (dSUP, M, sw * k), (GS.data_ptr() + i * sw * 4, M, sw)])
         self._wg_flush()
@@ -1198,18 +1254,20 @@ class TrainExec(_VitTrainBase):
             T.gc_bwd(self.Y32, M, i * sw, recs[j]["mean"][-1], recs[j]["scale"][-1], sw, self.y_noise, M, dylik, GS, M,
                      DY, M, dMS[0, j], dMS[1, j], sw, B, HW, sw, dt)
         dms = stacks(cm + cs, [r["mean"] for r in recs] + [r["scale"] for r in recs], dMS.view(2 * nbs, Mp, sw),
-                     "mean/scale")
+                     "mean/scale", groups=2)
+        firsts = ((cm, (self.LMS, M + sw * k, 2 * M, None, 0, 0), lambda j: [(dLM, M, M), (dSUP, M, sw * k)]),
+                  (cs, (self.LS, M, 2 * M, lms + M * esz, sw * k, 2 * M), lambda j: [(dLS, M, M), (dSUP2, M, sw * k)]))
+        for t, (convs, first, _) in enumerate(firsts):
+            x1, c1, ld1, x2, c2, ld2 = first
+            cin, cout = c1 + c2, convs[0][0].out_channels
+            self._wg_many([{"a": dms[t * nbs + j], "b": x1, "x2": x2, "out": G(convs[j][0].weight),
+                            "bias": G(convs[j][0].bias)} for j in range(nbs)],
+                          cout, 9 * cin, Mp, dt, conv=dict(c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv", ldb=ld1)
         for j in reversed(range(nbs)):
-            for t, (convs, first, routes) in enumerate(((cm[j], (self.LMS, M + sw * k, 2 * M, None, 0, 0),
-                                                         [(dLM, M, M), (dSUP, M, sw * k)]),
-                                                        (cs[j], (self.LS, M, 2 * M, lms + M * esz, sw * k, 2 * M),
-                                                         [(dLS, M, M), (dSUP2, M, sw * k)]))):
-                c, d = convs[0], dms[t * nbs + j]
-                x1, c1, ld1, x2, c2, ld2 = first
-                cin, cout = c1 + c2, c.out_channels
-                self._wg(d, x1, cout, 9 * cin, Mp, G(c.weight), dt, ldb=ld1,
-                         conv=dict(x2=x2, c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
-                T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
+            for t, (convs, first, routes) in enumerate(firsts):
+                c, d = convs[j][0], dms[t * nbs + j]
+                cin, cout = first[1] + first[4], c.out_channels
+                T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes(j))
             self._wg_flush()
             self._ready(cs[j][0].bias)  # every gradient of slices >= i0 + j is final (DP hand-off per slice)
 
@@ -1220,10 +1278,10 @@ class TrainExec(_VitTrainBase):
         dt, W, G, B, g, Mp = self.dtype, self.w, self.grad, self.batch, self.g, self.Mp
         (ca, sa, da, fa, ra), (cb, sb, db, fb, rb) = a, b
         for l in range(4, 0, -1):
-            for c, saved, d in ((ca[l], sa, da), (cb[l], sb, db)):
-                cin = c.in_channels
-                self._wg(d, saved[l - 1][0], c.out_channels, 9 * cin, Mp, G(c.weight), dt,
-                         conv=dict(c1=cin, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
+            cin = ca[l].in_channels
+            self._wg_many([{"a": d, "b": saved[l - 1][0], "out": G(c.weight), "bias": G(c.bias)}
+                           for c, saved, d in ((ca[l], sa, da), (cb[l], sb, db))],
+                          ca[l].out_channels, 9 * cin, Mp, dt, conv=dict(c1=cin, H=g, W=g, cin=cin), layout="conv")
             cin, cout = ca[l].in_channels, ca[l].out_channels
             assert (cb[l].in_channels, cb[l].out_channels) == (cin, cout)
             dxa, dxb = self._e(Mp, cin), self._e(Mp, cin)
@@ -1238,15 +1296,21 @@ class TrainExec(_VitTrainBase):
             T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
         self._wg_flush()
 
-    def _stack_bwd(self, convs, saved, dtop, first, routes):
+    def _stack_bwd(self, convs, saved, dtop, first, routes, defer=None):
+        """backward of one 5-layer slice stack; with `defer` (a list) the weight gradients of layers 4..1 are
+        appended to it as (_wg_many item, shape args) instead of being queued"""
         dt, W, G, B, g, Mp = self.dtype, self.w, self.grad, self.batch, self.g, self.Mp
         d = dtop
         for l in range(4, 0, -1):
             c = convs[l]
             cin, cout = c.in_channels, c.out_channels
             act_prev, pre_prev = saved[l - 1]
-            self._wg(d, act_prev, cout, 9 * cin, Mp, G(c.weight), dt, conv=dict(c1=cin, H=g, W=g, cin=cin),
-                    layout="conv", bias=G(c.bias))
+            if defer is not None:
+                defer.append(({"a": d, "b": act_prev, "out": G(c.weight), "bias": G(c.bias)},
+                              (cout, 9 * cin, Mp, dt, dict(c1=cin, H=g, W=g, cin=cin))))
+            else:
+                self._wg(d, act_prev, cout, 9 * cin, Mp, G(c.weight), dt, conv=dict(c1=cin, H=g, W=g, cin=cin),
+                         layout="conv", bias=G(c.bias))
             dx = self._e(Mp, cin)
             T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, out=dx, pre=pre_prev)
             d = dx

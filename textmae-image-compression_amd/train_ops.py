@@ -74,15 +74,18 @@ def patch_gather(imgs, ids, out, keep, patch, dtype):
 # ------------------------------------------------------------------------------------- gradients
 def wgrad(a, b, M, N, K, out, dtype, lda=None, ldb=None, a_remap=(None, 0, 0), b_remap=(None, 0, 0), conv=None,
           layout="dense", cin_total=None, ci_off=0, accumulate=False, bias=None, bias_accumulate=False, ws_slot=1,
-          slot_div=1):
+          slot_div=1, batch=None):
     """out <- sum_k A(k, m) B(k, n) in the parameter's layout; bias (optional) <- sum_k A(k, m), the bias
     gradient of the layer whose output gradient A is, formed by the same GEMM.
     layout: "dense" (out [M][N]), "dense_t" (out [N][M]: ConvTranspose2d 1x1 weights), "conv"
     (out [M][cin_total][3][3], columns of B = tap * Cin + ci land at input channel ci_off + ci).
-    conv = dict(x2=None, c1=..., ld2=0, H=, W=, stride=, cin=) selects the implicit im2col of B."""
+    conv = dict(x2=None, c1=..., ld2=0, H=, W=, stride=, cin=) selects the implicit im2col of B.
+    batch = (nb, s_a, s_b, s_b2, s_out, s_bias): nb problems of this shape in one launch, problem j's operands /
+    outputs j * s elements past the first's (the same layer of several slices' stacks)."""
     dev = out.device
     code = dtype_code(dtype)
-    need = _lib.value("tmae_wgrad_workspace", M, N, K, code)
+    nb = batch[0] if batch is not None else 1
+    need = _lib.value("tmae_wgrad_workspace_nb", M, N, K, code, int(slot_div), nb)
     ws = scratch(dev, need, slot=ws_slot)  # slot 4: the side stream's weight gradients (mcm_train._wg)
     args = WgradArgs()
     args.a, args.lda = _p(a), (lda if lda is not None else M)
@@ -117,6 +120,8 @@ def wgrad(a, b, M, N, K, out, dtype, lda=None, ldb=None, a_remap=(None, 0, 0), b
     args.bias_out = _p(bias)
     args.bias_accumulate = int(bias_accumulate)
     args.slot_div = int(slot_div)
+    if batch is not None:
+        args.nb, args.s_a, args.s_b, args.s_b2, args.s_out, args.s_bias = batch
     _lib.call("tmae_wgrad", ctypes.byref(args), code, _stream())
     return out
 
