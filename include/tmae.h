@@ -193,6 +193,26 @@ typedef struct tmae_lic_stack_args {
 #define TMAE_LIC_STACK_CHAIN 1
 int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream);
 
+/* Latent-channel partial sums of the slice stacks' first convs (mcm.py _Executor._slices / mcm_train
+ * _slices_fwd_fused; the convs of MCM.py:761-781 restricted to their first `cin` input channels = the
+ * latent_means / latent_scales part of the torch.cat): for problem j < nb (<= 4),
+ *   y[row][16 f + c] = sum_{tap, ci < cin} W_f[c][ci][tap] x_j[row shifted by tap][ci]   (f32, no bias)
+ * over the G x G grid (G*G <= 144, zero padding) of n images, for the weight fragments
+ * f = f_off[j] + f_lo .. f_off[j] + f_hi - 1 of w: blocks of nfr fragments, block b = f / nfr at element
+ * b * blk, each packed in tmae_lic_stack's order [tap 9][k-step cin/32][fragment nfr][lane 64][8] (one block
+ * per stack's latent part, [mean | lrp | scale] x slices, so column 16 f of y is that stack's block of the
+ * partial-sum buffer).  x_j: bf16 NHWC rows ldx apart, cin a multiple of 32 and <= 384; nfr, f_lo, f_hi
+ * and every f_off[j] even.  One workgroup = one image x 16 fragments. */
+#define TMAE_LIC_LATENT_MAXP 4
+typedef struct tmae_lic_latent_args {
+  int n, G, cin, nb;
+  const void* x[TMAE_LIC_LATENT_MAXP]; int ldx;
+  const void* w; int nfr; long long blk;
+  int f_off[TMAE_LIC_LATENT_MAXP]; int f_lo, f_hi;
+  float* y; int ldy;
+} tmae_lic_latent_args;
+int tmae_lic_latent(const tmae_lic_latent_args* args, void* stream);
+
 /* GaussianConditional likelihood + y_hat quantisation for `nslices` consecutive slices of width sw
  * (MCM.py:767-776): lik[NCHW channel yoff + j*sw + c] = GC(y~, max(sigma, .11), mu), LowerBound 1e-9;
  * yhat (dtype yhat_dtype, optional) and yhat32 (f32, optional) [pixel][channel] = round(y - mu) + mu.

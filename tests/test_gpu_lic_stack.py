@@ -104,6 +104,56 @@ def test_lic_stack_vs_torch(tmae, G, c1, c2, nb, mode):
     check(f"lic_stack_maxrel_{mode}", err, STACK_MAXREL)
 
 
+LATENT_MAXREL = 1e-5  # f32 sums of bf16 products in another order than conv2d: ~10x the measured 1.1e-6
+
+
+@pytest.mark.parametrize("G,cin,nfr,nblk,nb,f_lo,f_hi", [
+    (12, 384, 14, 36, 3, 14, 28),    # the bench geometry: slice 1's mean / lrp / scale blocks
+    (12, 384, 14, 36, 3, 84, 168),   # slices 6..11 (6 tiles of 16 fragments, the last one partial)
+    (12, 96, 4, 6, 2, 0, 8),         # odd k-step count per tap (cin 96 -> 3)
+    (8, 64, 6, 3, 1, 0, 6),          # 8x8 grid (K = 64), two k-steps per tap
+    (6, 32, 2, 4, 2, 2, 4),          # small grid, one k-step, a launch starting past block 0
+])
+def test_lic_latent_vs_torch(tmae, G, cin, nfr, nblk, nb, f_lo, f_hi):
+    """tmae_lic_latent (the latent partial sums of every stack's first conv, mcm.py _slices) against torch's fp32
+    conv2d of the same bf16-rounded operands: every block of the packing one stack, problem j reading its own
+    input and the blocks from f_off[j]; columns outside the launch's fragments untouched"""
+    from textmae_amd import ops
+
+    torch.manual_seed(G * 1000 + cin)
+    n = 5
+    rows = n * G * G
+    ldx = cin + 32
+    xs = [_bf(torch.randn(rows, ldx, device=DEV)) for _ in range(nb)]
+    co = 16 * nfr
+    ws = [_bf(torch.randn(co, cin + 16, 3, 3, device=DEV) / (9 * cin) ** 0.5) for _ in range(nblk)]
+    wpk = torch.stack([ops.pack_lic_stack_weight(w[:, :cin]) for w in ws]).contiguous()
+    per = nblk // nb  # blocks per problem
+    f_off = [j * per * nfr for j in range(nb)]
+    ldy = nblk * co + 8
+    y = torch.full((rows, ldy), float("nan"), device=DEV)
+    ops.lic_latent(n, G, [x.to(torch.bfloat16) for x in xs], ldx, cin, wpk, nfr, wpk[0].numel(), f_off, f_lo, f_hi,
+                   y, ldy)
+    torch.cuda.synchronize()
+    err = 0.0
+    for j in range(nb):
+        h = xs[j][:, :cin].reshape(n, G, G, cin).permute(0, 3, 1, 2)
+        f = f_off[j] + f_lo
+        while f < f_off[j] + f_hi:
+            b, fi = divmod(f, nfr)
+            nf = min(nfr - fi, f_off[j] + f_hi - f)
+            ref = F.conv2d(h, ws[b][16 * fi:16 * (fi + nf), :cin], padding=1).permute(0, 2, 3, 1).reshape(rows, -1)
+            got = y[:, 16 * f:16 * (f + nf)]
+            err = max(err, _maxrel(got, ref))
+            f += nf
+    check("lic_latent_maxrel", err, LATENT_MAXREL)
+    # columns of the fragments outside [f_lo, f_hi) of every problem keep their NaN
+    mask = torch.ones(ldy, dtype=torch.bool, device=DEV)
+    for j in range(nb):
+        mask[16 * (f_off[j] + f_lo):16 * (f_off[j] + f_hi)] = False
+    assert torch.isnan(y[:, mask]).all()
+
+
 def test_lic_stack_rejects_oversized(tmae):
     from textmae_amd import ops
 

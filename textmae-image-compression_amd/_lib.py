@@ -99,6 +99,17 @@ class LicStackArgs(ctypes.Structure):
     ]
 
 
+class LicLatentArgs(ctypes.Structure):
+    """mirror of tmae_lic_latent_args"""
+    _fields_ = [
+        ("n", I), ("G", I), ("cin", I), ("nb", I),
+        ("x", P * 4), ("ldx", I),
+        ("w", P), ("nfr", I), ("blk", LL),
+        ("f_off", I * 4), ("f_lo", I), ("f_hi", I),
+        ("y", P), ("ldy", I),
+    ]
+
+
 class EBParams(ctypes.Structure):
     _fields_ = [("matrix", ctypes.c_void_p * 5), ("bias", ctypes.c_void_p * 5), ("factor", ctypes.c_void_p * 4),
                 ("quantiles", ctypes.c_void_p)]
@@ -122,6 +133,7 @@ SIGNATURES = {
     "tmae_decoder_pred_cp_fwd": [P, P, P, P, I, I, I, I, I, I, I, I, P],
     "tmae_conv3x3": [ctypes.POINTER(ConvArgs), I, P],
     "tmae_lic_stack": [ctypes.POINTER(LicStackArgs), P],
+    "tmae_lic_latent": [ctypes.POINTER(LicLatentArgs), P],
     "tmae_gc_slices_fwd": [P, I, I, P, P, LL, I, P, P, I, P, I, I, P, I, I, I, I, I, P],
     "tmae_eb_likelihood_fwd": [P, ctypes.POINTER(EBParams), P, P, P, I, P, I, I, I, P],
     "tmae_eb_aux_loss": [ctypes.POINTER(EBParams), P, P, P, I, P],

@@ -522,3 +522,179 @@ extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
   hipLaunchKernelGGL(lic_stack_kernel, dim3(nwg), dim3(NW * 64), 0, (hipStream_t)stream, a);
   TMAE_LAUNCH_CHECK("tmae_lic_stack");
 }
+
+// ================================================================== latent-channel partial sums
+// tmae_lic_latent: the first convs' latent part of every slice stack as ONE packed conv (cin <= 384, one image x 16
+// output fragments per workgroup).  The halo kernel (conv_halo.h) it replaces stages the weight slab of every
+// (64-channel chunk, tap) step through LDS behind a barrier: operands of both sides read from LDS and a barrier per
+// step.  Here, as in lic_stack, the image's input rows stay in LDS for the whole K sweep and every wave streams its
+// own two weight fragments per K-step from L2 into registers: no barrier inside the sweep, B reads shared by two
+// MFMAs.  Summation order per output: taps outer, 32-channel steps inner.
+namespace llat {
+constexpr int NW = 8, FPW = 2 * NW;  // fragments per workgroup (one pair per wave)
+constexpr int MAXCIN = 384;
+constexpr unsigned PMAX = lstk::pitch(MAXCIN);
+constexpr unsigned ZOFF = lstk::MAXPIX * PMAX;  // 16 zero rows past the 144 input rows
+constexpr unsigned TMASK = ZOFF + 16 * PMAX;
+constexpr int LDS_BYTES = TMASK + 320;
+}  // namespace llat
+__device__ __forceinline__ constexpr unsigned llat_zoff() { return llat::ZOFF; }
+__device__ __forceinline__ constexpr unsigned llat_tmask() { return llat::TMASK; }
+
+// one wave: output fragments f0, f0 + 1 x all 9 pixel fragments over the 9 x NKC K-steps.  The tap loop is rolled
+// (108 unrolled steps at cin 384 left the ring arrays in scratch); inside a tap the NKC steps are unrolled, and
+// with D | NKC the A ring's slots stay static registers across taps (step s in slot (s mod NKC) mod D).
+template <int NKC>
+__device__ __forceinline__ void llat_item(const bf16* w, int nfr, long long blk, int f0, const unsigned char* lb,
+                                          unsigned pin, int G, int npix, int img, float* y, int ldy, int lane) {
+  constexpr int MF = 9, NS = 9 * NKC;
+  constexpr int D = NKC % 4 == 0 ? 4 : NKC % 3 == 0 ? 3 : NKC % 2 == 0 ? 2 : (NKC <= 7 ? NKC : 1);
+  asm volatile("" : "+v"(lane));
+  const int fr = lane & 15, fq = lane >> 4;
+  f32x4 acc[2][MF];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < MF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const unsigned sstride = (unsigned)nfr * 512u;
+  const bf16* wl[2];
+  bf16x8 ar[D][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int b = f0 / nfr, fi = f0 - b * nfr + i;  // f0 even, nfr even: the pair shares a block
+    wl[i] = w + b * blk + ((size_t)fi * 64 + lane) * 8;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      ar[d][i] = *reinterpret_cast<const bf16x8*>(wl[i]);
+      wl[i] += sstride;
+    }
+  }
+  unsigned tmask[MF];
+#pragma unroll
+  for (int j = 0; j < MF; ++j) tmask[j] = *reinterpret_cast<const unsigned short*>(lb + llat_tmask() + 2 * (16 * j + fr));
+  auto row = [&](int t, int j) -> unsigned {
+    const int p = 16 * j + fr, sh = (t / 3 - 1) * G + (t % 3 - 1);
+    const unsigned r = (unsigned)(p + sh);
+    return ((tmask[j] >> t) & 1u ? r * pin : llat_zoff() + (r & 15u) * pin) + 16u * fq;
+  };
+  bf16x8 bv[2][MF];
+  unsigned rb[MF];
+#pragma unroll
+  for (int j = 0; j < MF; ++j) {
+    rb[j] = row(0, j);
+    bv[0][j] = *reinterpret_cast<const bf16x8*>(lb + rb[j]);
+  }
+  for (int t = 0; t < 9; ++t) {
+    unsigned rn[MF];
+#pragma unroll
+    for (int j = 0; j < MF; ++j) rn[j] = row(t + 1 < 9 ? t + 1 : t, j);
+#pragma unroll
+    for (int kc = 0; kc < NKC; ++kc) {
+      if (kc + 1 < NKC) {
+#pragma unroll
+        for (int j = 0; j < MF; ++j) bv[(kc + 1) & 1][j] = *reinterpret_cast<const bf16x8*>(lb + rb[j] + 64u * (kc + 1));
+      } else if (t + 1 < 9) {
+#pragma unroll
+        for (int j = 0; j < MF; ++j) bv[(kc + 1) & 1][j] = *reinterpret_cast<const bf16x8*>(lb + rn[j]);
+      }
+      bf16x8 a0[2];
+      const bool more = t * NKC + kc + D < NS;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a0[i] = ar[kc % D][i];
+        if (more) {
+          ar[kc % D][i] = *reinterpret_cast<const bf16x8*>(wl[i]);
+          wl[i] += sstride;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < MF; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[i], bv[kc & 1][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (NKC & 1) {  // odd step count per tap: the next tap's first B fragments went to buffer 1
+#pragma unroll
+      for (int j = 0; j < MF; ++j) bv[0][j] = bv[1][j];
+    }
+#pragma unroll
+    for (int j = 0; j < MF; ++j) rb[j] = rn[j];
+  }
+  // lane: channels 16 (f0 + i) + 4 fq .. + 3 of pixel 16 j + fr
+#pragma unroll
+  for (int j = 0; j < MF; ++j) {
+    const int p = 16 * j + fr;
+    if (p < npix) {
+      float* yr = y + ((size_t)img * npix + p) * ldy + 16 * f0 + 4 * fq;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) store4(yr + 16 * i, acc[i][j]);
+    }
+  }
+}
+
+template <int NKC>
+__global__ void __launch_bounds__(llat::NW * 64) lic_latent_kernel(tmae_lic_latent_args a) {
+  using namespace llat;
+  __shared__ __attribute__((aligned(16))) uint4 lds[LDS_BYTES / 16];
+  unsigned char* lb = reinterpret_cast<unsigned char*>(lds);
+  const int n = a.n, G = a.G, npix = G * G, cin = 32 * NKC;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);  // tile-major: an XCD's run shares its tiles' weights in L2
+  const int tile = t / n, img = t - tile * n, prob = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const unsigned pin = lstk::pitch(cin);
+  for (int i = tid; i < 16 * (int)pin / 16; i += NW * 64) reinterpret_cast<uint4*>(lds)[ZOFF / 16 + i] = uint4{0, 0, 0, 0};
+  for (int p = tid; p < 160; p += NW * 64) {
+    unsigned m = 0;
+    if (p < npix) {
+      const int py = p / G, px = p - py * G;
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int yy = py + k / 3 - 1, xx = px + k % 3 - 1;
+        m |= ((unsigned)yy < (unsigned)G && (unsigned)xx < (unsigned)G) ? (1u << k) : 0u;
+      }
+    }
+    *reinterpret_cast<unsigned short*>(lb + TMASK + 2 * p) = (unsigned short)m;
+  }
+  {
+    const bf16* x = reinterpret_cast<const bf16*>(a.x[prob]);
+    constexpr int q = 4 * NKC;  // 16-B pieces per row
+    for (int i = tid; i < npix * q; i += NW * 64) {
+      const int p = i / q, ch = 8 * (i - p * q);
+      *reinterpret_cast<uint4*>(lb + p * pin + 2 * ch) =
+          *reinterpret_cast<const uint4*>(x + ((size_t)img * npix + p) * a.ldx + ch);
+    }
+  }
+  __syncthreads();
+  const int fb = a.f_off[prob] + a.f_lo, f0 = fb + tile * FPW + 2 * wave;
+  if (f0 >= a.f_off[prob] + a.f_hi) return;  // past this launch's fragments (no barrier follows)
+  llat_item<NKC>(reinterpret_cast<const bf16*>(a.w), a.nfr, a.blk, f0, lb, pin, G, npix, img, a.y, a.ldy, lane);
+}
+
+extern "C" int tmae_lic_latent(const tmae_lic_latent_args* args, void* stream) {
+  TMAE_REQUIRE(args != nullptr, "tmae_lic_latent: args is NULL");
+  const tmae_lic_latent_args& a = *args;
+  TMAE_REQUIRE(a.G >= 1 && a.G * a.G <= lstk::MAXPIX, "tmae_lic_latent: grid %dx%d", a.G, a.G);
+  TMAE_REQUIRE(a.cin >= 32 && a.cin % 32 == 0 && a.cin <= llat::MAXCIN, "tmae_lic_latent: cin %d (multiple of 32, <= %d)",
+               a.cin, llat::MAXCIN);
+  TMAE_REQUIRE(a.nb >= 1 && a.nb <= TMAE_LIC_LATENT_MAXP && a.n >= 1, "tmae_lic_latent: %d problems, %d images", a.nb,
+               a.n);
+  TMAE_REQUIRE(a.w && a.y && a.ldx % 8 == 0 && a.ldx >= a.cin && a.ldy % 4 == 0, "tmae_lic_latent: operands / strides");
+  TMAE_REQUIRE(a.nfr >= 2 && a.nfr % 2 == 0 && a.f_lo >= 0 && a.f_hi > a.f_lo && a.f_lo % 2 == 0 && a.f_hi % 2 == 0,
+               "tmae_lic_latent: fragments [%d, %d) of blocks of %d (even)", a.f_lo, a.f_hi, a.nfr);
+  TMAE_REQUIRE(a.blk >= 9LL * (a.cin / 32) * a.nfr * 512 || a.f_off[0] + a.f_hi <= a.nfr, "tmae_lic_latent: block stride");
+  for (int j = 0; j < a.nb; ++j)
+    TMAE_REQUIRE(a.x[j] && a.f_off[j] >= 0 && a.f_off[j] % 2 == 0, "tmae_lic_latent: problem %d", j);
+  const int ntile = (a.f_hi - a.f_lo + llat::FPW - 1) / llat::FPW;
+  const dim3 grid(a.n * ntile, a.nb);
+  hipStream_t st = (hipStream_t)stream;
+  switch (a.cin / 32) {
+#define LLAT_CASE(K) \
+  case K: hipLaunchKernelGGL(lic_latent_kernel<K>, grid, dim3(llat::NW * 64), 0, st, a); break;
+    LLAT_CASE(1) LLAT_CASE(2) LLAT_CASE(3) LLAT_CASE(4) LLAT_CASE(5) LLAT_CASE(6)
+    LLAT_CASE(7) LLAT_CASE(8) LLAT_CASE(9) LLAT_CASE(10) LLAT_CASE(11) LLAT_CASE(12)
+#undef LLAT_CASE
+    default: break;
+  }
+  TMAE_LAUNCH_CHECK("tmae_lic_latent");
+}

@@ -324,6 +324,7 @@ class _Executor:
     # per-layer conv launches (the f32 parity path's structure) or the unchained serial slices
     USE_LIC_STACK = True
     USE_LIC_CHAIN = True
+    USE_LIC_LATENT = True  # False: the latent partial sums on the halo conv (conv_halo.h)
 
     def __init__(self, m: MCM, batch, dtype, device):
         self.m, self.batch, self.dtype, self.device = m, batch, dtype, device
@@ -452,6 +453,12 @@ class _Executor:
         self.w_pre_ml = cast(torch.cat([cw(mean[i][0].weight, 0, M) for i in range(S)]
                                        + [cw(lrp[i][0].weight, 0, M) for i in range(S)]))
         self.w_pre_s = cast(torch.cat([cw(scale[i][0].weight, 0, M) for i in range(S)]))
+        # the same latent parts in fragment order, one block per stack [mean | lrp | scale] x slices (tmae_lic_latent)
+        c0 = self.mid[0]
+        self.w_lat = None
+        if dt == torch.bfloat16 and self.USE_LIC_LATENT and ops.lic_latent_fits(self.g, M) and c0 % 32 == 0:
+            self.w_lat = torch.stack([ops.pack_lic_stack_weight(t[i][0].weight[:, :M])
+                                      for t in (mean, lrp, scale) for i in range(S)]).contiguous()
         # per-slice y_hat-channel parts + the remaining layers, packed for batched launches
         self.ms_first, self.ms_layers, self.lrp_first, self.lrp_layers = [], [], [], []
         for i in range(ms):
@@ -736,6 +743,11 @@ class _Executor:
         wrow = self.w_pre_ml[0].numel()
 
         def pre(i0, i1):
+            if self.w_lat is not None:  # every stack's block of slices [i0, i1) in one launch
+                nfs = c0 // 16
+                ops.lic_latent(B, g, [self.LM, self.LM, self.LS], M, M, self.w_lat, nfs, self.w_lat[0].numel(),
+                               [0, S * nfs, 2 * S * nfs], i0 * nfs, i1 * nfs, pbase, Pw)
+                return
             n = (i1 - i0) * c0
             ops.conv3x3(self.LM, M, M, B, g, g, self.w_pre_ml[i0 * c0:], None, pbase + (off_mean + i0 * c0) * eP, Pw,
                         n, dt, y_f32=True, nb=(1, 2), strides={"w": (0, S * c0 * wrow), "y": (0, S * c0)})

@@ -647,6 +647,7 @@ class TrainExec(_VitTrainBase):
         return saved
 
     USE_LIC_STACK = True  # test hook: False runs the per-layer conv launches in the bf16 training forward too
+    USE_LIC_LATENT = True  # False: the latent partial sums as two implicit-GEMM conv launches
 
     def _fused_ok(self):
         m = self.m
@@ -683,11 +684,19 @@ class TrainExec(_VitTrainBase):
         P = torch.empty((Mp, Pw), dtype=torch.float32, device=self.device)
         self._P = P
         pb = P.data_ptr()
-        w_ml = W.packed([c[0].weight for c in cm] + [c[0].weight for c in cl], ("conv_lat", M))
-        w_s = W.packed([c[0].weight for c in cs], ("conv_lat", M))
-        ops.conv3x3(self.LMS, M, 2 * M, B, g, g, w_ml, None, pb, Pw, S * c0, dt, y_f32=True, nb=(1, 2),
-                    strides={"w": (0, S * w_ml[0].numel()), "y": (0, S * c0)})
-        ops.conv3x3(self.LS, M, 2 * M, B, g, g, w_s, None, pb + off_scale * 4, Pw, S * c0, dt, y_f32=True)
+        if self.USE_LIC_LATENT and ops.lic_latent_fits(g, M) and c0 % 32 == 0:
+            # one tmae_lic_latent launch: a block per stack's latent part, [mean | lrp | scale] x slices
+            w_lat = W.packed([c[0].weight for c in cm] + [c[0].weight for c in cl] + [c[0].weight for c in cs],
+                             ("lic", 0, M))
+            nfs = c0 // 16
+            ops.lic_latent(B, g, [self.LMS, self.LMS, self.LS], 2 * M, M, w_lat, nfs, w_lat[0].numel(),
+                           [0, S * nfs, 2 * S * nfs], 0, S * nfs, pb, Pw)
+        else:
+            w_ml = W.packed([c[0].weight for c in cm] + [c[0].weight for c in cl], ("conv_lat", M))
+            w_s = W.packed([c[0].weight for c in cs], ("conv_lat", M))
+            ops.conv3x3(self.LMS, M, 2 * M, B, g, g, w_ml, None, pb, Pw, S * c0, dt, y_f32=True, nb=(1, 2),
+                        strides={"w": (0, S * w_ml[0].numel()), "y": (0, S * c0)})
+            ops.conv3x3(self.LS, M, 2 * M, B, g, g, w_s, None, pb + off_scale * 4, Pw, S * c0, dt, y_f32=True)
 
         def stack_weights(convs_per_problem, lo, n0):
             """per layer: packed weights of the problems (layer 0: input channels [lo, lo + n0)) and biases"""

@@ -262,6 +262,27 @@ def pack_lic_stack_weight(w: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor
     return t.view(-1).to(dtype)
 
 
+def lic_latent_fits(G, cin):
+    """True when tmae_lic_latent takes the latent partial sums of this shape (bf16, cin a multiple of 32)"""
+    return G * G <= LSTK_MAXPIX and cin % 32 == 0 and 32 <= cin <= 384
+
+
+def lic_latent(n, G, xs, ldx, cin, w, nfr, blk, f_off, f_lo, f_hi, y, ldy):
+    """Latent-channel partial sums (tmae_lic_latent): for problem j, y[:, 16 f ..] (f32) = the 3x3 conv of xs[j]'s
+    channels [0, cin) with the packed weight fragments f_off[j] + [f_lo, f_hi) of w: blocks of nfr fragments blk
+    elements apart (pack_lic_stack_weight of each stack's latent part, stacked).  Pointers: tensors or raw
+    addresses."""
+    a = _lib.LicLatentArgs()
+    a.n, a.G, a.cin, a.nb = n, G, cin, len(xs)
+    for j, (x, fo) in enumerate(zip(xs, f_off)):
+        a.x[j] = _p(x)
+        a.f_off[j] = fo
+    a.ldx, a.w, a.nfr, a.blk = ldx, _p(w), nfr, blk
+    a.f_lo, a.f_hi = f_lo, f_hi
+    a.y, a.ldy = _p(y), ldy
+    _lib.call("tmae_lic_latent", ctypes.byref(a), _stream())
+
+
 def lic_stack(n, G, x1, c1, ld1, weights, biases, couts, y, ldy, y_f32, x2=None, c2=0, ld2=0, addend=None, ld_add=0,
               lrp_src=None, ld_src=0, y2=None, ldy2=0, nb=(1, 1), strides=None, chain=None, save=None):
     """One slice-transform stack per (problem, image) (tmae_lic_stack).  weights: packed per layer

@@ -27,9 +27,9 @@ def parse(st):
 
 
 def run(st):
-    saved = {k: getattr(mcm_train._VitTrainBase, k) for k in parse(st)}
+    saved = {k: getattr(mcm_train.TrainExec, k) for k in parse(st)}
     for k, v in parse(st).items():
-        setattr(mcm_train._VitTrainBase, k, v)
+        setattr(mcm_train.TrainExec, k, v)
     try:
         torch.manual_seed(0)
         m = textmae_amd.MCM(img_size=256, num_keep_patches=144).cuda().train()
@@ -52,7 +52,7 @@ def run(st):
         return ms
     finally:
         for k, v in saved.items():
-            setattr(mcm_train._VitTrainBase, k, v)
+            setattr(mcm_train.TrainExec, k, v)
 
 
 res = {st: [] for st in settings}
