@@ -229,6 +229,12 @@ class LaunchTimer:
                                              + sum(9 * c2[l] * c2[l + 1] * 2 for l in range(c.cn))
                                              + (px * c2[1] * 4 if c.cadd else 0))
             return "lic_stack", fl
+        if name == "tmae_lic_latent":
+            c = a[0]._obj
+            px, ncol = c.n * c.G * c.G, 16 * (c.f_hi - c.f_lo)
+            # algorithmic bytes: each problem's input map, its weight fragments, the f32 output columns
+            self.conv_bytes += c.nb * (px * c.cin * 2 + ncol * 9 * c.cin * 2 + px * ncol * 4)
+            return "lic_latent", 2.0 * c.nb * px * ncol * 9 * c.cin
         if name == "tmae_patch_embed_fwd":
             return "patch_embed", 2.0 * a[6] * a[13] * a[11] * a[7] * a[10] * a[10]
         if name == "tmae_patch_embed_gathered":  # (patches, ids, w, b, pos, tok, n, Kw, D, L, keep, ...)
@@ -352,7 +358,7 @@ def roofline_report(m, imgs, scores, batch, dump=None):
     agg = {"token_gemm": [k for k in mf if k.split("_")[-1] in ("qkv", "proj", "fc1", "fc2")],
            "token_gemm_with_qkv_attn": [k for k in mf if k.split("_")[-1] in ("qkv", "proj", "fc1", "fc2")
                                         or k.endswith("qkv_attn")],
-           "lic_conv3x3": ["lic_conv3x3"], "lic_3x3_all": ["lic_conv3x3", "lic_stack"]}
+           "lic_conv3x3": ["lic_conv3x3"], "lic_3x3_all": ["lic_conv3x3", "lic_latent", "lic_stack"]}
 
     def stat(keys):
         n = sum(fam[k][0] for k in keys if k in fam)
@@ -366,8 +372,8 @@ def roofline_report(m, imgs, scores, batch, dump=None):
     total_t = sum(v[1] for v in fam.values())  # replayed families only (entropy models / ids excluded)
     dom = max(fam, key=lambda k: fam[k][1] if fam[k][2] > 0 else -1)
     d = stat([dom])
-    desc = {"lic_conv3x3": " (conv_halo_kernel + conv-source GEMM tiles: h_a / h_s and the slice stacks' "
-                           "latent-channel partial sums)",
+    desc = {"lic_conv3x3": " (conv_halo_kernel + conv-source GEMM tiles: h_a / h_s)",
+            "lic_latent": " (lic_latent_kernel: the slice stacks' latent-channel partial sums)",
             "lic_stack": " (lic_stack_kernel: whole cc_transform_mean/scale stacks, each serial slice's mean "
                          "stack chained into its lrp_transform stack, one workgroup per problem x image)"}
     flops_launch = d["gflop"] * 1e9 / max(d["launches"], 1)

@@ -4,6 +4,7 @@ ids-shuffle kernel (once per MCM forward).
 
 Kernel name -> family (the shape -> family mapping of bench.py, by what the trace can tell apart):
   lic_conv3x3     conv_halo_kernel<...> and every GEMM tile with a ConvSrc operand source
+  lic_latent      lic_latent_kernel<...> (the slice stacks' latent partial sums)
   enc_attn_core   mha_fwd_bf16_kernel<64>        dec_attn_core  mha_fwd_bf16_kernel<32>
   layernorm       layernorm_kernel
   gc_slices       gc_slices_kernel               eb_likelihood  eb_prep_kernel + eb_likelihood_kernel
@@ -28,6 +29,8 @@ from collections import defaultdict
 def family(name):
     if "lic_stack_kernel" in name:
         return "lic_stack"
+    if "lic_latent_kernel" in name:
+        return "lic_latent"
     if "conv_halo_kernel" in name or ("gemm" in name and "ConvSrc" in name):
         return "lic_conv3x3"
     if "qkv_attn_kernel" in name:  # fused qkv GEMM + attention (bf16 inference): dh 64 encoder, dh 32 decoder
