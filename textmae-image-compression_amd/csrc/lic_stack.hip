@@ -68,7 +68,7 @@ struct LstkOut {
 #endif
 #ifndef LSTK_DIAG
 #define LSTK_DIAG 0  // phase isolation builds (tools/lstk_diag.sh): 4 = no MFMA, 8 = no B reads, 16 = no A loads,
-                     // 32 = no epilogue
+                     // 32 = no epilogue, 64 = no layer-0 addend loads, 128 = no GELU (bias only)
 #endif
 
 __device__ __forceinline__ bf16x8 lstk_lds8(const unsigned char* lb, unsigned off) {
@@ -199,7 +199,7 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
   auto pix = [&](int j) { return 16 * (j0 + j) + fr; };
   auto grow = [&](int j) { return (size_t)img * npix + (size_t)min(pix(j), npix - 1); };
   if (!last) {
-    if (first && o.add) {
+    if (first && o.add && !(LSTK_DIAG & 64)) {
       f32x4 ad[NF][MF];
 #pragma unroll
       for (int i = 0; i < NF; ++i)
@@ -212,7 +212,11 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
     }
     auto gelu4 = [&](int i, int j) {
       const f32x4 v = acc[i][j] + bias[i];
+#if LSTK_DIAG & 128
+      const f32x2 lo = v.xy, hi = v.zw;
+#else
       const f32x2 lo = gelu2_bf16out(v.xy), hi = gelu2_bf16out(v.zw);
+#endif
       bf16x4 q;
       q[0] = (bf16)lo.x; q[1] = (bf16)lo.y; q[2] = (bf16)hi.x; q[3] = (bf16)hi.y;
       if (o.sp && okc[i] && pix(j) < npix) {  // training: keep the GELU input and output for the backward
