@@ -191,6 +191,13 @@ typedef struct tmae_lic_stack_args {
   float* csv_t; long long cs_t;
 } tmae_lic_stack_args;
 #define TMAE_LIC_STACK_CHAIN 1
+/* TMAE_LIC_STACK_BWD (training backward, mcm_train.py): the stack's data-gradient chain through LDS.  x1 = the
+ * gradient of the stack's output (channels [0, c1)); layer l is the transposed conv of forward layer L-1-l
+ * (weights packed transposed and tap-flipped, textmae_amd.ops.pack_lic_stack_weight_t), cout[l] its output
+ * channels; its epilogue multiplies by GELU'(sv_pre[l]) (the forward's saved bf16 pre-activation of those
+ * channels) and writes the result, bf16, to sv_act[l] (the weight gradient's operand; strides sv_s[l]) and, but
+ * for the last layer, into LDS as the next layer's input.  No bias, addend, lrp, chain or y. */
+#define TMAE_LIC_STACK_BWD 2
 int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream);
 
 /* Latent-channel partial sums of the slice stacks' first convs (mcm.py _Executor._slices / mcm_train

@@ -154,6 +154,47 @@ def test_lic_latent_vs_torch(tmae, G, cin, nfr, nblk, nb, f_lo, f_hi):
     assert torch.isnan(y[:, mask]).all()
 
 
+def _gelu_grad(x):
+    return 0.5 * (1.0 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+
+
+@pytest.mark.parametrize("G,P", [(12, 2), (12, 3), (8, 1)])
+def test_lic_stack_bwd_vs_torch(tmae, G, P):
+    """TMAE_LIC_STACK_BWD (the fused data-gradient chain of a stack's layers 4..1, mcm_train._fused_dgrads) against
+    torch: per layer dx = conv_transpose2d(d, W) (conv2d's input gradient) * GELU'(pre), rounded to bf16 as the
+    kernel keeps it in LDS; every layer's output compared (the weight gradients' operands)"""
+    from textmae_amd import ops
+
+    torch.manual_seed(7 + G + P)
+    n = 3
+    rows = n * G * G
+    chans = [224] + MID  # forward layer l: chans[l] -> chans[l + 1]; the backward runs 4..1
+    ws = [[_bf(torch.randn(chans[l + 1], chans[l], 3, 3, device=DEV) / (9 * chans[l]) ** 0.5) for l in range(5)]
+          for _ in range(P)]
+    pres = {l: _bf(torch.randn(P, rows, chans[l + 1], device=DEV)) for l in range(4)}  # GELU inputs of layers 0..3
+    dtop = _bf(torch.randn(P, rows, chans[5], device=DEV))
+    wpk = [torch.stack([ops.pack_lic_stack_weight_t(ws[p][l]) for p in range(P)]).contiguous() for l in (4, 3, 2, 1)]
+    outs = [torch.full((P, rows, chans[l + 1]), float("nan"), device=DEV).to(torch.bfloat16) for l in (3, 2, 1, 0)]
+    st = {"x1": (rows * chans[5], 0)}
+    for k, l in enumerate((3, 2, 1, 0)):
+        st[f"w{k}"] = (wpk[k][0].numel(), 0)
+        st[f"s{k}"] = (rows * chans[l + 1], 0)
+    ops.lic_stack_bwd(n, G, dtop.to(torch.bfloat16), chans[5], chans[5], wpk, [chans[l + 1] for l in (3, 2, 1, 0)],
+                      [pres[l].to(torch.bfloat16) for l in (3, 2, 1, 0)], outs, nb=(P, 1), strides=st)
+    torch.cuda.synchronize()
+    err = 0.0
+    for p in range(P):
+        d = dtop[p]
+        for k, l in enumerate((3, 2, 1, 0)):  # forward layer l + 1's input gradient -> layer l's pre-activation gradient
+            w = ws[p][l + 1]
+            h = d.view(n, G, G, -1).permute(0, 3, 1, 2)
+            dx = F.conv_transpose2d(h, w, padding=1).permute(0, 2, 3, 1).reshape(rows, -1)
+            ref = dx * _gelu_grad(pres[l][p])
+            err = max(err, _maxrel(outs[k][p].float(), ref))
+            d = _bf(ref)
+    check("lic_stack_bwd_maxrel", err, STACK_MAXREL)
+
+
 def test_lic_stack_rejects_oversized(tmae):
     from textmae_amd import ops
 

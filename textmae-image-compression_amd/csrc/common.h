@@ -99,6 +99,42 @@ __device__ __forceinline__ void gelu8_bf16out(f32x4& lo, f32x4& hi) {
   hi.xy = gelu2_bf16out(hi.xy);
   hi.zw = gelu2_bf16out(hi.zw);
 }
+// GELU derivative (training data gradients: the GEMM epilogues in train.hip, the fused stack backward)
+__device__ __forceinline__ float gelu_grad(float x) {
+  // d/dx [0.5 x (1 + erf(x / sqrt2))] = Phi(x) + x phi(x); erf by Abramowitz-Stegun 7.1.26 like gelu_erf
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = __builtin_amdgcn_exp2f(-z * z * 1.44269504088896341f);  // exp(-x^2 / 2)
+  const float erf_abs = fmaf(-p, e, 1.0f);
+  const float cdf = x >= 0.0f ? 0.5f + 0.5f * erf_abs : 0.5f * p * e;
+  return cdf + x * e * 0.39894228040143267794f;
+}
+
+// gelu_grad on two values with packed f32 math (v_pk_fma / v_pk_mul): the same approximation as the scalar
+// form, ~12 VALU issues per element instead of ~19; the data-gradient epilogues apply it to every fc1 / conv
+// element
+__device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) {
+  const f32x2 z = (f32x2){fabsf(x.x), fabsf(x.y)} * 0.70710678118654752440f;
+  const f32x2 d = __builtin_elementwise_fma((f32x2){0.3275911f, 0.3275911f}, z, (f32x2){1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = __builtin_elementwise_fma((f32x2){1.061405429f, 1.061405429f}, t, (f32x2){-1.453152027f, -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, (f32x2){1.421413741f, 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, (f32x2){-0.284496736f, -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, (f32x2){0.254829592f, 0.254829592f});
+  p *= t;
+  const f32x2 a = -z * z * 1.44269504088896341f;
+  const f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+  const f32x2 erf_abs = __builtin_elementwise_fma(-p, e, (f32x2){1.0f, 1.0f});
+  const f32x2 pos = 0.5f + 0.5f * erf_abs, neg = 0.5f * p * e;
+  const f32x2 cdf = {x.x >= 0.0f ? pos.x : neg.x, x.y >= 0.0f ? pos.y : neg.y};
+  return cdf + x * e * 0.39894228040143267794f;
+}
+
 // the GELU an epilogue storing OT applies
 template <typename OT> __device__ __forceinline__ float gelu_for(float x) {
   if constexpr (sizeof(OT) == 2) return gelu_bf16out(x);

@@ -61,6 +61,7 @@ struct LstkOut {
   bf16* sp;   // training: this layer's pre-activation, bf16 [rows][cout] (NULL: not kept)
   bf16* sa;   // training: its GELU output
   float* st;  // training, lrp last layer: the pre-tanh value, f32 [rows][cout]
+  int bwd;    // TMAE_LIC_STACK_BWD: out = acc * GELU'(sp) -> sa (global) and, but for the last layer, LDS
 };
 
 #ifndef LSTK_OPT
@@ -194,10 +195,34 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
   for (int i = 0; i < NF; ++i) {
     cc[i] = 16 * (f0 + i) + 4 * fq;
     okc[i] = cc[i] < L.cout;
-    bias[i] = load4f(L.b + (okc[i] ? cc[i] : 0));
+    bias[i] = o.bwd ? f32x4{0.f, 0.f, 0.f, 0.f} : load4f(L.b + (okc[i] ? cc[i] : 0));
   }
   auto pix = [&](int j) { return 16 * (j0 + j) + fr; };
   auto grow = [&](int j) { return (size_t)img * npix + (size_t)min(pix(j), npix - 1); };
+  if (o.bwd) {
+    // data gradient: the forward's GELU inputs of these channels, loaded for the whole item first
+    f32x4 pv[NF][MF];
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int j = 0; j < MF; ++j) pv[i][j] = load4f(o.sp + grow(j) * L.cout + (okc[i] ? cc[i] : 0));
+    const int pout = pitch(L.cout);
+#pragma unroll
+    for (int i = 0; i < NF; ++i)
+#pragma unroll
+      for (int j = 0; j < MF; ++j) {
+        const f32x2 g0 = gelu_grad2(pv[i][j].xy), g1 = gelu_grad2(pv[i][j].zw);
+        f32x4 v = acc[i][j];
+        v[0] *= g0.x; v[1] *= g0.y; v[2] *= g1.x; v[3] *= g1.y;
+        bf16x4 q;
+        q[0] = (bf16)v[0]; q[1] = (bf16)v[1]; q[2] = (bf16)v[2]; q[3] = (bf16)v[3];
+        if (okc[i] && pix(j) < npix) {
+          *reinterpret_cast<bf16x4*>(o.sa + grow(j) * L.cout + cc[i]) = q;
+          if (!last) *reinterpret_cast<bf16x4*>(lb + out_off + pix(j) * pout + 2 * cc[i]) = q;
+        }
+      }
+    return;
+  }
   if (!last) {
     if (first && o.add && !(LSTK_DIAG & 64)) {
       f32x4 ad[NF][MF];
@@ -352,12 +377,14 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
   int cin = cin0;
   for (int pass = 0; pass < (chain ? 2 : 1); ++pass) {
     LstkOut o;
+    o.bwd = (a->flags & TMAE_LIC_STACK_BWD) != 0;
     if (pass == 0) {
       o.add = a->addend ? a->addend + b1 * a->a_s[0] + b2 * a->a_s[1] : nullptr;
       o.ld_add = a->ld_add;
       o.y_f32 = a->y_f32;
-      o.y = o.y_f32 ? (void*)(reinterpret_cast<float*>(a->y) + b1 * a->y_s[0] + b2 * a->y_s[1])
-                    : (void*)(reinterpret_cast<bf16*>(a->y) + b1 * a->y_s[0] + b2 * a->y_s[1]);
+      o.y = !a->y ? nullptr
+            : o.y_f32 ? (void*)(reinterpret_cast<float*>(a->y) + b1 * a->y_s[0] + b2 * a->y_s[1])
+                      : (void*)(reinterpret_cast<bf16*>(a->y) + b1 * a->y_s[0] + b2 * a->y_s[1]);
       o.ldy = a->ldy;
       o.src = a->lrp_src ? a->lrp_src + b1 * a->src_s[0] + b2 * a->src_s[1] : nullptr;
       o.ld_src = a->ld_src;
@@ -413,7 +440,7 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
       LstkLayer L;
       if (pass == 0) {
         L.w = reinterpret_cast<const bf16*>(a->w[l]) + b1 * a->w_s[l][0] + b2 * a->w_s[l][1];
-        L.b = a->bias[l] + b1 * a->b_s[l][0] + b2 * a->b_s[l][1];
+        L.b = a->bias[l] ? a->bias[l] + b1 * a->b_s[l][0] + b2 * a->b_s[l][1] : nullptr;
         L.cout = a->cout[l];
       } else {
         L.w = reinterpret_cast<const bf16*>(a->cw[l]) + b2 * a->cs_w[l];
@@ -423,8 +450,8 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
       L.cin = cin;
       const bool first = l == 0, last = l + 1 == nl;
       if (pass == 0) {
-        o.sp = a->sv_pre[l] && !last ? reinterpret_cast<bf16*>(a->sv_pre[l]) + b1 * a->sv_s[l][0] + b2 * a->sv_s[l][1]
-                                     : nullptr;
+        o.sp = a->sv_pre[l] && (!last || o.bwd) ? reinterpret_cast<bf16*>(a->sv_pre[l]) + b1 * a->sv_s[l][0] + b2 * a->sv_s[l][1]
+                                                : nullptr;
         o.sa = o.sp ? reinterpret_cast<bf16*>(a->sv_act[l]) + b1 * a->sv_s[l][0] + b2 * a->sv_s[l][1] : nullptr;
         o.st = a->sv_t && last ? a->sv_t + b1 * a->sv_t_s[0] + b2 * a->sv_t_s[1] : nullptr;
       } else {
@@ -491,17 +518,24 @@ extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
   TMAE_REQUIRE(a.G >= 1 && a.G * a.G <= MAXPIX, "tmae_lic_stack: grid %dx%d exceeds %d pixels", a.G, a.G, MAXPIX);
   TMAE_REQUIRE(a.nlayers >= 1 && a.nlayers <= TMAE_LIC_STACK_MAXL, "tmae_lic_stack: %d layers", a.nlayers);
   TMAE_REQUIRE(a.nb1 >= 1 && a.nb2 >= 1 && a.n >= 1, "tmae_lic_stack: batch %d x %d, n %d", a.nb1, a.nb2, a.n);
-  TMAE_REQUIRE(a.x1 != nullptr && a.y != nullptr, "tmae_lic_stack: x1 / y required");
+  const bool bwd = (a.flags & TMAE_LIC_STACK_BWD) != 0;
+  TMAE_REQUIRE(a.x1 != nullptr && (a.y != nullptr || bwd), "tmae_lic_stack: x1 / y required");
+  if (bwd) {
+    TMAE_REQUIRE(!(a.flags & TMAE_LIC_STACK_CHAIN) && !a.addend && !a.lrp_src && !a.x2 && !a.sv_t,
+                 "tmae_lic_stack: the backward chain takes no chain / addend / lrp / second source");
+    for (int l = 0; l < a.nlayers; ++l)
+      TMAE_REQUIRE(a.w[l] && a.sv_pre[l] && a.sv_act[l], "tmae_lic_stack: backward layer %d needs w / sv_pre / sv_act", l);
+  }
   TMAE_REQUIRE(a.c1 >= 0 && a.c2 >= 0 && (a.c2 == 0 || a.x2 != nullptr), "tmae_lic_stack: channels %d + %d", a.c1, a.c2);
   TMAE_REQUIRE(a.c1 % 8 == 0 && a.c2 % 8 == 0 && a.ld1 % 8 == 0 && (a.c2 == 0 || a.ld2 % 8 == 0),
                "tmae_lic_stack: input channels / strides must be multiples of 8");
   TMAE_REQUIRE(pad32(a.c1 + a.c2) <= MAXC, "tmae_lic_stack: %d input channels exceed %d", a.c1 + a.c2, MAXC);
   for (int l = 0; l < a.nlayers; ++l) {
-    TMAE_REQUIRE((a.w[l] != nullptr || (l == 0 && a.c1 + a.c2 == 0)) && a.bias[l] != nullptr,
+    TMAE_REQUIRE((a.w[l] != nullptr || (l == 0 && a.c1 + a.c2 == 0)) && (a.bias[l] != nullptr || bwd),
                  "tmae_lic_stack: layer %d weights", l);
     TMAE_REQUIRE(a.cout[l] >= 4 && a.cout[l] % 8 == 0, "tmae_lic_stack: layer %d cout %d (multiple of 8)", l, a.cout[l]);
-    TMAE_REQUIRE(l + 1 == a.nlayers || pad32(a.cout[l]) <= MAXC, "tmae_lic_stack: layer %d cout %d exceeds %d", l,
-                 a.cout[l], MAXC);
+    TMAE_REQUIRE((l + 1 == a.nlayers && !bwd) || pad32(a.cout[l]) <= MAXC, "tmae_lic_stack: layer %d cout %d exceeds %d",
+                 l, a.cout[l], MAXC);
   }
   TMAE_REQUIRE(!a.lrp_src || !a.y_f32, "tmae_lic_stack: lrp output is bf16");
   if (a.flags & TMAE_LIC_STACK_CHAIN) {

@@ -13,40 +13,7 @@ static int colsum_into(const void* x, int x_dtype, int ld, int rows, int C, int 
 static int tmae_ln_fold(const float* part, int waves, int D, float* dg, float* db, int accumulate, hipStream_t st);
 
 // ================================================================== helpers
-__device__ __forceinline__ float gelu_grad(float x) {
-  // d/dx [0.5 x (1 + erf(x / sqrt2))] = Phi(x) + x phi(x); erf by Abramowitz-Stegun 7.1.26 like gelu_erf
-  const float z = fabsf(x) * 0.70710678118654752440f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  p *= t;
-  const float e = __builtin_amdgcn_exp2f(-z * z * 1.44269504088896341f);  // exp(-x^2 / 2)
-  const float erf_abs = fmaf(-p, e, 1.0f);
-  const float cdf = x >= 0.0f ? 0.5f + 0.5f * erf_abs : 0.5f * p * e;
-  return cdf + x * e * 0.39894228040143267794f;
-}
-
-// gelu_grad on two values with packed f32 math (v_pk_fma / v_pk_mul): the same approximation as the scalar
-// form, ~12 VALU issues per element instead of ~19; the data-gradient epilogues apply it to every fc1 / conv
-// element
-__device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) {
-  const f32x2 z = (f32x2){fabsf(x.x), fabsf(x.y)} * 0.70710678118654752440f;
-  const f32x2 d = __builtin_elementwise_fma((f32x2){0.3275911f, 0.3275911f}, z, (f32x2){1.0f, 1.0f});
-  const f32x2 t = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-  f32x2 p = __builtin_elementwise_fma((f32x2){1.061405429f, 1.061405429f}, t, (f32x2){-1.453152027f, -1.453152027f});
-  p = __builtin_elementwise_fma(p, t, (f32x2){1.421413741f, 1.421413741f});
-  p = __builtin_elementwise_fma(p, t, (f32x2){-0.284496736f, -0.284496736f});
-  p = __builtin_elementwise_fma(p, t, (f32x2){0.254829592f, 0.254829592f});
-  p *= t;
-  const f32x2 a = -z * z * 1.44269504088896341f;
-  const f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
-  const f32x2 erf_abs = __builtin_elementwise_fma(-p, e, (f32x2){1.0f, 1.0f});
-  const f32x2 pos = 0.5f + 0.5f * erf_abs, neg = 0.5f * p * e;
-  const f32x2 cdf = {x.x >= 0.0f ? pos.x : neg.x, x.y >= 0.0f ? pos.y : neg.y};
-  return cdf + x * e * 0.39894228040143267794f;
-}
+// gelu_grad / gelu_grad2: common.h (shared with the fused slice-stack backward, lic_stack.hip)
 
 // ================================================================== weight gradients (split-K TN GEMM)
 template <typename T>
@@ -479,7 +446,9 @@ extern "C" int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0,
 //      the transpose of the weight seen as [Cout][Cin * 9]); 16-B loads and 4-row (8-B bf16) stores when the
 //      source rows are 16-B aligned and R % 4 == 0 (scalar 4-B loads / 2-B stores ran at ~2 TB/s);
 //   2  per-row [A][B] -> [B][A] (conv weight [Cout][Cin][3][3] -> [Cout][3][3][Cin]: A = Cin = d3, B = 9): one row
-//      per chunk through LDS (A * B <= 8192); 16-B loads and 8-B bf16 stores when A % 4 == 0 and aligned.
+//      per chunk through LDS (A * B <= 8192); 16-B loads and 8-B bf16 stores when A % 4 == 0 and aligned;
+//   3  tmae_lic_stack's fragment order of a channel range of a conv weight (below);
+//   4  the same for the transposed, tap-flipped weight (the fused stack backward's).
 template <typename OT>
 __device__ __forceinline__ void relayout_store(void* dst, size_t i, float v) { reinterpret_cast<OT*>(dst)[i] = to_out<OT>(v); }
 
@@ -592,6 +561,26 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
       const unsigned f = r % nfr, tk = r / nfr, kc = tk % nkc, tap = tk / nkc;
       const unsigned co = 16 * f + (lane & 15u), ci = 32 * kc + 8 * (lane >> 4) + e8;
       const float v = (co < cout && ci < cn) ? src[((size_t)co * cin_tot + lo + ci) * 9 + tap] : 0.0f;
+      if (to_bf16) ((bf16*)e[1])[i] = (bf16)v;
+      else ((float*)e[1])[i] = v;
+    }
+    return;
+  }
+  if (mode == 4) {
+    // the transposed, tap-flipped conv weight (the data gradient's: input = the forward's Cout = d1 channels, output
+    // = its Cin = d2) in the same fragment order: element e of lane (fq, fr) in fragment f, k-step kc, tap t =
+    // W[32 kc + 8 fq + e][16 f + fr][8 - t] (ops.pack_lic_stack_weight_t)
+    const unsigned cout = d1, cin = d2;
+    const unsigned nfr = (cin + 15) / 16;
+    const unsigned nkc = (cout + 31) / 32;
+    const unsigned base4 = chunk * 32768u;
+    for (unsigned k = tid; k < 32768u; k += 256u) {
+      const unsigned i = base4 + k;
+      if (i >= total) break;
+      const unsigned e8 = i & 7u, lane = (i >> 3) & 63u, r = i >> 9;
+      const unsigned f = r % nfr, tk = r / nfr, kc = tk % nkc, tap = tk / nkc;
+      const unsigned ci = 16 * f + (lane & 15u), co = 32 * kc + 8 * (lane >> 4) + e8;
+      const float v = (co < cout && ci < cin) ? src[((size_t)co * cin + ci) * 9 + (8 - tap)] : 0.0f;
       if (to_bf16) ((bf16*)e[1])[i] = (bf16)v;
       else ((float*)e[1])[i] = v;
     }

@@ -67,6 +67,8 @@ class _Weights:
             if job[0] == "lic":  # first build of a fragment-order pack (later ones: relayout_multi mode 3)
                 _, co, ci, lo, n = job
                 dst.copy_(ops.pack_lic_stack_weight(w[:, lo:lo + n], self.dtype))
+            elif job[0] == "licT":  # the transposed, tap-flipped pack (relayout mode 4)
+                dst.copy_(ops.pack_lic_stack_weight_t(w, self.dtype))
             else:
                 T.relayout(w, dst, *job)
         self.cache[key] = [sig, dst, p, job]
@@ -94,6 +96,16 @@ class _Weights:
                 buf = torch.empty((len(params), total), dtype=self.dtype, device=p0.device)
                 for j, p in enumerate(params):
                     self.cache[(id(p), kind)] = [None, buf[j], p, ("lic", co, p.shape[1], lo, n)]
+                self.packs[key] = buf
+                for p in params:
+                    self._get(p, kind, None)
+                return buf
+            elif kind == "licT":  # the transposed conv's weight in fragment order (the fused stack backward)
+                co, ci = p0.shape[:2]
+                total = 9 * (-(-co // 32)) * (-(-ci // 16)) * 512
+                buf = torch.empty((len(params), total), dtype=self.dtype, device=p0.device)
+                for j, p in enumerate(params):
+                    self.cache[(id(p), kind)] = [None, buf[j], p, ("licT", co, ci)]
                 self.packs[key] = buf
                 for p in params:
                     self._get(p, kind, None)
@@ -134,6 +146,14 @@ class _Weights:
             sig, dst, p, job = e
             e[0] = (p.data_ptr(), p._version)
             if job is None:
+                continue
+            if job[0] == "licT":  # the transposed fragment order (relayout mode 4)
+                _, co, ci = job
+                total = 9 * (-(-co // 32)) * (-(-ci // 16)) * 512
+                rows.append([p.data_ptr(), dst.data_ptr(), ops.dtype_code(dst.dtype) | (4 << 8), co, ci, 0, 0, 0, 0, 0,
+                             total, chunk])
+                ptrs.append((p.data_ptr(), dst.data_ptr()))
+                chunk += (total + 32767) // 32768
                 continue
             if job[0] == "lic":  # tmae_lic_stack fragment order (relayout mode 3)
                 _, co, ci, lo, n = job
@@ -648,6 +668,8 @@ class TrainExec(_VitTrainBase):
 
     USE_LIC_STACK = True  # test hook: False runs the per-layer conv launches in the bf16 training forward too
     USE_LIC_LATENT = True  # False: the latent partial sums as two implicit-GEMM conv launches
+    USE_LIC_STACK_BWD = True  # False: the slice stacks' data gradients as one conv launch per layer
+    _fused_bwd = False
 
     def _fused_ok(self):
         m = self.m
@@ -774,6 +796,8 @@ class TrainExec(_VitTrainBase):
                           "lrp": [(a[j], p_[j]) for a, p_ in sv_lb] + [tb[j]]}
 
     def _slices_fwd(self):
+        # the fused stack backward reads what the fused forward saved (bf16 pre-activations, [problems][Mp][c])
+        self._fused_bwd = self._fused_ok() and self.USE_LIC_STACK_BWD
         if self._fused_ok():
             return self._slices_fwd_fused()
         m, dt, W, B, g = self.m, self.dtype, self.w, self.batch, self.g
@@ -1225,6 +1249,16 @@ class TrainExec(_VitTrainBase):
             the weight gradients of each of `groups` consecutive problem groups (lrp / mean / scale) as one batched
             launch per layer"""
             P = len(convs)
+            fd = self._fused_dgrads([(convs[p_], saved[p_], dtop[p_]) for p_ in range(P)])
+            if fd is not None:  # the data gradients in one launch, then the weight gradients per layer
+                for l in range(4, 0, -1):
+                    cin, cout = convs[0][l].in_channels, convs[0][l].out_channels
+                    q = P // groups
+                    for g0 in range(0, P, q):
+                        self._wg_many([{"a": fd[l][p_], "b": saved[p_][l - 1][0], "out": G(convs[p_][l].weight),
+                                        "bias": G(convs[p_][l].bias)} for p_ in range(g0, g0 + q)],
+                                      cout, 9 * cin, Mp, dt, conv=dict(c1=cin, H=g, W=g, cin=cin), layout="conv")
+                return fd[0]
             d = dtop
             for l in range(4, 0, -1):
                 cin, cout = convs[0][l].in_channels, convs[0][l].out_channels
@@ -1280,23 +1314,67 @@ class TrainExec(_VitTrainBase):
             self._wg_flush()
             self._ready(cs[j][0].bias)  # every gradient of slices >= i0 + j is final (DP hand-off per slice)
 
+    def _fused_dgrads(self, stacks):
+        """layers 4..1 data gradients of P same-shape stacks (convs, saved, dtop) in ONE tmae_lic_stack backward
+        launch (the chain through LDS, TMAE_LIC_STACK_BWD), or None when the operands do not allow it (the per-layer
+        launches then run).  Returns d[l] for l = 0..4: the gradient w.r.t. layer l's pre-activation, a list over the
+        problems (d[4] = the dtops); d[0..3] are views of one [P][Mp][cout] bf16 buffer per layer."""
+        if not self._fused_bwd:
+            return None
+        P, Mp = len(stacks), self.Mp
+        convs0 = stacks[0][0]
+        couts = [c.out_channels for c in convs0]
+        if len(convs0) != 5 or any(c > ops.LSTK_MAXC for c in couts[:4]):
+            return None
+
+        def delta(ts):
+            d = {t.data_ptr() - ts[0].data_ptr() for t in ts[1:]}
+            return 0 if not d else (next(iter(d)) // ts[0].element_size() if len(d) == 1 else None)
+
+        dts = [s[2] for s in stacks]
+        pres = [[s[1][l][1] for s in stacks] for l in (3, 2, 1, 0)]
+        sx = delta(dts)
+        if sx is None or any(p_[0].dtype != torch.bfloat16 or (P > 1 and delta(p_) != Mp * couts[l])
+                             for p_, l in zip(pres, (3, 2, 1, 0))):
+            return None
+        ws = [self.w.packed([s[0][l].weight for s in stacks], "licT") for l in (4, 3, 2, 1)]
+        outs = [self._e(P, Mp, couts[l]) for l in (3, 2, 1, 0)]
+        st = {"x1": (sx, 0)}
+        for k, l in enumerate((3, 2, 1, 0)):
+            st[f"w{k}"] = (ws[k][0].numel() if P > 1 else 0, 0)
+            st[f"s{k}"] = (Mp * couts[l], 0)
+        ops.lic_stack_bwd(self.batch, self.g, dts[0], couts[4], couts[4], ws, [couts[l] for l in (3, 2, 1, 0)],
+                          [p_[0] for p_ in pres], outs, nb=(P, 1), strides=st)
+        d = [None] * 5
+        for k, l in enumerate((3, 2, 1, 0)):
+            d[l] = [outs[k][p_] for p_ in range(P)]
+        d[4] = dts
+        return d
+
     def _stack_bwd_pair(self, a, b):
         """_stack_bwd of two stacks with the same layer shapes (a slice's mean and scale stacks): the data gradients
-        of layers 4..1 run as one 2-problem launch each (the same per-problem sums as two launches); the weight
-        gradients and the first layers (their own input splits / routes) one by one, a's before b's"""
+        of layers 4..1 as one 2-problem launch (the fused chain, or one 2-problem conv launch per layer); the weight
+        gradients of layers 4..1 as 2-problem launches; the first layers (their own input splits / routes) one by one,
+        a's before b's"""
         dt, W, G, B, g, Mp = self.dtype, self.w, self.grad, self.batch, self.g, self.Mp
         (ca, sa, da, fa, ra), (cb, sb, db, fb, rb) = a, b
+        fd = self._fused_dgrads([(ca, sa, da), (cb, sb, db)])
         for l in range(4, 0, -1):
             cin = ca[l].in_channels
+            dl = (fd[l][0], fd[l][1]) if fd is not None else (da, db)
             self._wg_many([{"a": d, "b": saved[l - 1][0], "out": G(c.weight), "bias": G(c.bias)}
-                           for c, saved, d in ((ca[l], sa, da), (cb[l], sb, db))],
+                           for c, saved, d in ((ca[l], sa, dl[0]), (cb[l], sb, dl[1]))],
                           ca[l].out_channels, 9 * cin, Mp, dt, conv=dict(c1=cin, H=g, W=g, cin=cin), layout="conv")
+            if fd is not None:
+                continue
             cin, cout = ca[l].in_channels, ca[l].out_channels
             assert (cb[l].in_channels, cb[l].out_channels) == (cin, cout)
             dxa, dxb = self._e(Mp, cin), self._e(Mp, cin)
             T.conv_dgrad(da, W.conv_dg(ca[l].weight), B, g, g, 1, cout, cin, dt, out=dxa, pre=sa[l - 1][1],
                          second=(db, W.conv_dg(cb[l].weight), dxb, sb[l - 1][1]))
             da, db = dxa, dxb
+        if fd is not None:
+            da, db = fd[0]
         for c, d, first, routes in ((ca[0], da, fa, ra), (cb[0], db, fb, rb)):
             x1, c1, ld1, x2, c2, ld2 = first
             cin, cout = c1 + c2, c.out_channels
@@ -1309,29 +1387,35 @@ class TrainExec(_VitTrainBase):
         """backward of one 5-layer slice stack; with `defer` (a list) the weight gradients of layers 4..1 are
         appended to it as (_wg_many item, shape args) instead of being queued"""
         dt, W, G, B, g, Mp = self.dtype, self.w, self.grad, self.batch, self.g, self.Mp
+        fd = self._fused_dgrads([(convs, saved, dtop)])
         d = dtop
         for l in range(4, 0, -1):
             c = convs[l]
             cin, cout = c.in_channels, c.out_channels
             act_prev, pre_prev = saved[l - 1]
+            if fd is not None:
+                d = fd[l][0]
             if defer is not None:
                 defer.append(({"a": d, "b": act_prev, "out": G(c.weight), "bias": G(c.bias)},
                               (cout, 9 * cin, Mp, dt, dict(c1=cin, H=g, W=g, cin=cin))))
             else:
                 self._wg(d, act_prev, cout, 9 * cin, Mp, G(c.weight), dt, conv=dict(c1=cin, H=g, W=g, cin=cin),
                          layout="conv", bias=G(c.bias))
+            if fd is not None:
+                continue
             dx = self._e(Mp, cin)
             T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, out=dx, pre=pre_prev)
             d = dx
+        if fd is not None:
+            d = fd[0][0]
         c = convs[0]
         x1, c1, ld1, x2, c2, ld2 = first
         cin, cout = c1 + c2, c.out_channels
         self._wg(d, x1, cout, 9 * cin, Mp, G(c.weight), dt, ldb=ld1,
-                conv=dict(x2=x2, c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
+                 conv=dict(x2=x2, c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
         # zero-width routes (no support slices yet) stay in place: their limits still partition the channels
         T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
         self._wg_flush()
-
 
 def _bias(b):
     return None if b is None else b.detach()

@@ -262,6 +262,35 @@ def pack_lic_stack_weight(w: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor
     return t.view(-1).to(dtype)
 
 
+def pack_lic_stack_weight_t(w: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    """A 3x3 conv weight [Cout][Cin][3][3] as the weight of its transposed conv (the data gradient: input Cout
+    channels, output Cin, taps flipped) in tmae_lic_stack's fragment order (relayout mode 4 builds the same)"""
+    return pack_lic_stack_weight(w.detach().transpose(0, 1).flip(2, 3), dtype)
+
+
+def lic_stack_bwd(n, G, dtop, ldt, c_top, weights, couts, pres, outs, nb=(1, 1), strides=None):
+    """The data-gradient chain of a slice stack's layers L-1..1 in one launch (tmae_lic_stack, TMAE_LIC_STACK_BWD):
+    dtop [rows][c_top] (bf16, rows ldt apart) is the gradient of the stack's output; layer l (the transposed conv
+    of forward layer L-1-l, weights[l] from pack_lic_stack_weight_t) writes outs[l] = (its conv) * GELU'(pres[l]),
+    bf16 [rows][couts[l]].  `strides` maps x1, w<l>, s<l> (pres[l] / outs[l]) -> per-problem (s1, s2)."""
+    a = LicStackArgs()
+    a.n, a.G, a.nlayers = n, G, len(couts)
+    a.nb1, a.nb2 = nb
+    a.x1, a.c1, a.ld1 = _p(dtop), c_top, ldt
+    a.flags = 2
+    for l, (w, c, pre, out) in enumerate(zip(weights, couts, pres, outs)):
+        a.w[l], a.cout[l] = _p(w), c
+        a.sv_pre[l], a.sv_act[l] = _p(pre), _p(out)
+    for name, (s1, s2) in (strides or {}).items():
+        if name[0] == "w":
+            a.w_s[int(name[1:])][:] = (s1, s2)
+        elif name[0] == "s":
+            a.sv_s[int(name[1:])][:] = (s1, s2)
+        else:
+            getattr(a, f"{name}_s")[:] = (s1, s2)
+    _lib.call("tmae_lic_stack", ctypes.byref(a), _stream())
+
+
 def lic_latent_fits(G, cin):
     """True when tmae_lic_latent takes the latent partial sums of this shape (bf16, cin a multiple of 32)"""
     return G * G <= LSTK_MAXPIX and cin % 32 == 0 and 32 <= cin <= 384
