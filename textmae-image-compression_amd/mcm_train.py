@@ -244,6 +244,7 @@ class _VitTrainBase:
     # split-K of the ViT blocks' weight gradients sized for 1 / VIT_WG_SLOT_DIV of the CU slots (test / A-B hook;
     # the side stream shares the chip with the data-gradient chain)
     VIT_WG_SLOT_DIV = _SIDE_SLOT_DIV
+    SIDE_SLOT_DIV = _SIDE_SLOT_DIV  # the other side-stream weight gradients' (LIC convs) split-K slot divisor
     _side_used = False
     _pending = ()
     _queued = ()
@@ -316,13 +317,17 @@ class _VitTrainBase:
         self._side_calls = 0  # weight gradients the side stream ran in this backward (tests)
         self._pending, self._keep, self._queued, self._groups = [], [], [], []
 
+    TIMING_SKIP_WG = False  # diagnostics: drop every queued weight gradient (wrong gradients; timing A/B only)
+
     def _wg(self, a, *args, **kw):
         """T.wgrad for the side stream: a weight gradient has no consumer inside the backward, so it runs under
         the serial data-gradient chain.  Queued here and enqueued by _wg_flush behind ONE fork per group (a stack,
         a block): a captured graph pays a cross-queue dependency per fork.  `a` (this layer's output gradient, a
         fresh tensor of the chain) is kept alive until the join; every other operand is a saved activation."""
+        if self.TIMING_SKIP_WG:  # timing diagnostics only (tools/train_ab.py): the step without weight gradients
+            return
         if self._side is None:  # same split plan as the side stream's, so both modes sum in the same order
-            kw.setdefault("slot_div", _SIDE_SLOT_DIV)
+            kw.setdefault("slot_div", self.SIDE_SLOT_DIV)
             return T.wgrad(a, *args, **kw)
         self._queued.append((a, args, kw))
 
@@ -377,7 +382,7 @@ class _VitTrainBase:
             self._side.wait_event(ev)
             with torch.cuda.stream(self._side):
                 for a, args, kw in group:
-                    kw.setdefault("slot_div", _SIDE_SLOT_DIV)
+                    kw.setdefault("slot_div", self.SIDE_SLOT_DIV)
                     T.wgrad(a, *args, ws_slot=4, **kw)
                     self._keep.append(a)
                     self._side_calls += 1

@@ -18,6 +18,8 @@ from textmae_amd.rd_loss import RateDistortionLoss  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 B = int(sys.argv[2]) if len(sys.argv) > 2 else 64
 settings = sys.argv[3:] or ["base"]
+EAGER = "eager" in settings  # eager steps (engine.train_step) instead of the captured graph
+settings = [st for st in settings if st != "eager"] or ["base"]
 
 
 def parse(st):
@@ -38,7 +40,11 @@ def run(st):
         opt, aux = configure_optimizers(m, lr=1e-4, aux_lr=1e-4, fused=True)
         crit = RateDistortionLoss(lmbda=1e-2)
         imgs, scores = bench.synthetic_inputs(B, 256, 256, 2000, "cuda")
-        g = engine.GraphedTrainStep(m, crit, opt, aux, imgs, scores, clip_max_norm=1.0, warmup=1)
+        if EAGER:
+            def g(i, s_):
+                return engine.train_step(m, crit, i, s_, opt, aux, clip_max_norm=1.0)
+        else:
+            g = engine.GraphedTrainStep(m, crit, opt, aux, imgs, scores, clip_max_norm=1.0, warmup=1)
         for _ in range(3):
             g(imgs, scores)
         torch.cuda.synchronize()
@@ -60,4 +66,4 @@ for rep in range(2):
     for st in (settings if rep == 0 else list(reversed(settings))):
         res[st].append(round(run(st), 3))
         print(st, res[st][-1], flush=True)
-print(json.dumps({"batch": B, "steps": n, "ms_per_step": res}))
+print(json.dumps({"batch": B, "steps": n, "eager": EAGER, "ms_per_step": res}))
