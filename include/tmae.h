@@ -200,16 +200,18 @@ typedef struct tmae_lic_stack_args {
 #define TMAE_LIC_STACK_BWD 2
 int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream);
 
-/* Latent-channel partial sums of the slice stacks' first convs (mcm.py _Executor._slices / mcm_train
- * _slices_fwd_fused; the convs of MCM.py:761-781 restricted to their first `cin` input channels = the
- * latent_means / latent_scales part of the torch.cat): for problem j < nb (<= 4),
- *   y[row][16 f + c] = sum_{tap, ci < cin} W_f[c][ci][tap] x_j[row shifted by tap][ci]   (f32, no bias)
- * over the G x G grid (G*G <= 144, zero padding) of n images, for the weight fragments
- * f = f_off[j] + f_lo .. f_off[j] + f_hi - 1 of w: blocks of nfr fragments, block b = f / nfr at element
- * b * blk, each packed in tmae_lic_stack's order [tap 9][k-step cin/32][fragment nfr][lane 64][8] (one block
- * per stack's latent part, [mean | lrp | scale] x slices, so column 16 f of y is that stack's block of the
- * partial-sum buffer).  x_j: bf16 NHWC rows ldx apart, cin a multiple of 32 and <= 384; nfr, f_lo, f_hi
- * and every f_off[j] even.  One workgroup = one image x 16 fragments. */
+/* A stride-1 3x3 conv over G x G grids (G*G <= 144, zero padding) with each image's input resident in LDS and
+ * the weights streamed from L2 into registers (lic_stack.hip): the latent-channel partial sums of the slice
+ * stacks' first convs (mcm.py _Executor._slices / mcm_train _slices_fwd_fused; MCM.py:761-781 restricted to
+ * the first `cin` = latent_means / latent_scales channels of the torch.cat), and the 12x12 convs of h_a
+ * (layers 0-1, MCM.py:115-134) and h_s (last layer, MCM.py:136-162).  For problem j < nb (<= 4), relative
+ * fragment r in [f_lo, f_hi) (global fragment f = f_off[j] + r):
+ *   y_j[row][16 r + c] = act(bias_j[16 r + c] + sum_{tap, ci < cin} W_f[c][ci][tap] x_j[row shifted][ci])
+ * with y_j = y + y_s[j] elements (f32, or bf16 when y_bf16; rows ldy apart), bias_j optional (f32), act
+ * TMAE_ACT_NONE / _GELU.  w: blocks of nfr fragments, block b = f / nfr at element b * blk, each packed in
+ * tmae_lic_stack's order [tap 9][k-step cin/32][fragment nfr][lane 64][8] (ops.pack_lic_stack_weight).
+ * x_j: bf16 NHWC rows ldx apart, cin a multiple of 32 and <= 384; f_lo even.  One workgroup = one image x 16
+ * fragments. */
 #define TMAE_LIC_LATENT_MAXP 4
 typedef struct tmae_lic_latent_args {
   int n, G, cin, nb;
@@ -217,6 +219,9 @@ typedef struct tmae_lic_latent_args {
   const void* w; int nfr; long long blk;
   int f_off[TMAE_LIC_LATENT_MAXP]; int f_lo, f_hi;
   float* y; int ldy;
+  long long y_s[TMAE_LIC_LATENT_MAXP];
+  const float* bias[TMAE_LIC_LATENT_MAXP];
+  int act, y_bf16;
 } tmae_lic_latent_args;
 int tmae_lic_latent(const tmae_lic_latent_args* args, void* stream);
 

@@ -154,6 +154,36 @@ def test_lic_latent_vs_torch(tmae, G, cin, nfr, nblk, nb, f_lo, f_hi):
     assert torch.isnan(y[:, mask]).all()
 
 
+@pytest.mark.parametrize("G,cin,cout,nb,act", [(12, 384, 336, 1, True), (12, 384, 384, 2, False), (8, 96, 48, 2, True)])
+def test_lic_latent_bias_act_bf16(tmae, G, cin, cout, nb, act):
+    """the resident-input conv as h_a's first layers / h_s's last (mcm.py): bias, GELU, bf16 output at per-problem
+    offsets, an odd fragment count (336 = 21 fragments: the last wave's lone fragment) -- against torch's fp32 conv2d
+    + bias (+ GELU) of the same bf16 operands"""
+    from textmae_amd import ops
+
+    torch.manual_seed(cin + cout + nb)
+    n = 4
+    rows = n * G * G
+    xs = [_bf(torch.randn(rows, cin, device=DEV)) for _ in range(nb)]
+    ws = [_bf(torch.randn(cout, cin, 3, 3, device=DEV) / (9 * cin) ** 0.5) for _ in range(nb)]
+    bs = [torch.randn(cout, device=DEV) for _ in range(nb)]
+    nfr = -(-cout // 16)
+    wpk = torch.stack([ops.pack_lic_stack_weight(w) for w in ws]).contiguous()
+    y = torch.full((nb, rows, cout), float("nan"), device=DEV).to(torch.bfloat16)
+    ops.lic_latent(n, G, [x.to(torch.bfloat16) for x in xs], cin, cin, wpk, nfr, wpk[0].numel(),
+                   [j * nfr for j in range(nb)], 0, nfr, y, cout, y_s=[j * rows * cout for j in range(nb)], biases=bs,
+                   act=ops.ACT_GELU if act else ops.ACT_NONE, y_bf16=True)
+    torch.cuda.synchronize()
+    err = 0.0
+    for j in range(nb):
+        h = xs[j].view(n, G, G, cin).permute(0, 3, 1, 2)
+        ref = F.conv2d(h, ws[j], bs[j], padding=1).permute(0, 2, 3, 1).reshape(rows, cout)
+        if act:
+            ref = F.gelu(ref)
+        err = max(err, _maxrel(y[j].float(), ref))
+    check("lds_conv_maxrel", err, STACK_MAXREL)
+
+
 def _gelu_grad(x):
     return 0.5 * (1.0 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
 

@@ -107,6 +107,7 @@ class LicLatentArgs(ctypes.Structure):
         ("w", P), ("nfr", I), ("blk", LL),
         ("f_off", I * 4), ("f_lo", I), ("f_hi", I),
         ("y", P), ("ldy", I),
+        ("y_s", LL * 4), ("bias", P * 4), ("act", I), ("y_bf16", I),
     ]
 
 

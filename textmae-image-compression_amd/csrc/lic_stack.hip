@@ -582,9 +582,18 @@ __device__ __forceinline__ constexpr unsigned llat_tmask() { return llat::TMASK;
 // one wave: output fragments f0, f0 + 1 x all 9 pixel fragments over the 9 x NKC K-steps.  The tap loop is rolled
 // (108 unrolled steps at cin 384 left the ring arrays in scratch); inside a tap the NKC steps are unrolled, and
 // with D | NKC the A ring's slots stay static registers across taps (step s in slot (s mod NKC) mod D).
+// epilogue operands of one problem: output (f32 or bf16, rows ldy apart) starting at the problem's first fragment's
+// column, optional bias over those columns, optional GELU
+struct LlatOut {
+  void* y;
+  int ldy, bf, act;
+  const float* bias;
+};
+
 template <int NKC>
-__device__ __forceinline__ void llat_item(const bf16* w, int nfr, long long blk, int f0, const unsigned char* lb,
-                                          unsigned pin, int G, int npix, int img, float* y, int ldy, int lane) {
+__device__ __forceinline__ void llat_item(const bf16* w, int nfr, long long blk, int f0, int fcol, bool two,
+                                          const unsigned char* lb, unsigned pin, int G, int npix, int img,
+                                          const LlatOut& o, int lane) {
   constexpr int MF = 9, NS = 9 * NKC;
   constexpr int D = NKC % 4 == 0 ? 4 : NKC % 3 == 0 ? 3 : NKC % 2 == 0 ? 2 : (NKC <= 7 ? NKC : 1);
   asm volatile("" : "+v"(lane));
@@ -599,7 +608,8 @@ __device__ __forceinline__ void llat_item(const bf16* w, int nfr, long long blk,
   bf16x8 ar[D][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int b = f0 / nfr, fi = f0 - b * nfr + i;  // f0 even, nfr even: the pair shares a block
+    const int f = two || i == 0 ? f0 + i : f0;  // a lone last fragment: the pair's second half re-reads the first
+    const int b = f / nfr, fi = f - b * nfr;
     wl[i] = w + b * blk + ((size_t)fi * 64 + lane) * 8;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -659,14 +669,26 @@ __device__ __forceinline__ void llat_item(const bf16* w, int nfr, long long blk,
 #pragma unroll
     for (int j = 0; j < MF; ++j) rb[j] = rn[j];
   }
-  // lane: channels 16 (f0 + i) + 4 fq .. + 3 of pixel 16 j + fr
+  // lane: columns fcol + 16 i + 4 fq .. + 3 (fragment f0 + i) of pixel 16 j + fr
+  f32x4 bias[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    bias[i] = o.bias ? load4f(o.bias + fcol + 16 * (two ? i : 0) + 4 * fq) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < MF; ++j) {
     const int p = 16 * j + fr;
-    if (p < npix) {
-      float* yr = y + ((size_t)img * npix + p) * ldy + 16 * f0 + 4 * fq;
+    if (p >= npix) continue;
+    const size_t at = ((size_t)img * npix + p) * o.ldy + fcol + 4 * fq;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) store4(yr + 16 * i, acc[i][j]);
+    for (int i = 0; i < 2; ++i) {
+      if (i == 1 && !two) break;
+      f32x4 v = acc[i][j] + bias[i];
+      if (o.act == TMAE_ACT_GELU) {
+        const f32x2 lo = gelu2_bf16out(v.xy), hi = gelu2_bf16out(v.zw);
+        v = f32x4{lo.x, lo.y, hi.x, hi.y};
+      }
+      if (o.bf) store4(reinterpret_cast<bf16*>(o.y) + at + 16 * i, v);
+      else store4(reinterpret_cast<float*>(o.y) + at + 16 * i, v);
     }
   }
 }
@@ -704,9 +726,16 @@ __global__ void __launch_bounds__(llat::NW * 64) lic_latent_kernel(tmae_lic_late
     }
   }
   __syncthreads();
-  const int fb = a.f_off[prob] + a.f_lo, f0 = fb + tile * FPW + 2 * wave;
-  if (f0 >= a.f_off[prob] + a.f_hi) return;  // past this launch's fragments (no barrier follows)
-  llat_item<NKC>(reinterpret_cast<const bf16*>(a.w), a.nfr, a.blk, f0, lb, pin, G, npix, img, a.y, a.ldy, lane);
+  const int fr0 = a.f_lo + tile * FPW + 2 * wave;  // this wave's first fragment, relative to the problem's
+  if (fr0 >= a.f_hi) return;  // past this launch's fragments (no barrier follows)
+  LlatOut o;
+  o.ldy = a.ldy;
+  o.bf = a.y_bf16;
+  o.act = a.act;
+  o.bias = a.bias[prob];
+  o.y = a.y_bf16 ? (void*)(reinterpret_cast<bf16*>(a.y) + a.y_s[prob]) : (void*)(a.y + a.y_s[prob]);
+  llat_item<NKC>(reinterpret_cast<const bf16*>(a.w), a.nfr, a.blk, a.f_off[prob] + fr0, 16 * fr0, fr0 + 1 < a.f_hi, lb,
+                 pin, G, npix, img, o, lane);
 }
 
 extern "C" int tmae_lic_latent(const tmae_lic_latent_args* args, void* stream) {
@@ -717,12 +746,14 @@ extern "C" int tmae_lic_latent(const tmae_lic_latent_args* args, void* stream) {
                a.cin, llat::MAXCIN);
   TMAE_REQUIRE(a.nb >= 1 && a.nb <= TMAE_LIC_LATENT_MAXP && a.n >= 1, "tmae_lic_latent: %d problems, %d images", a.nb,
                a.n);
-  TMAE_REQUIRE(a.w && a.y && a.ldx % 8 == 0 && a.ldx >= a.cin && a.ldy % 4 == 0, "tmae_lic_latent: operands / strides");
-  TMAE_REQUIRE(a.nfr >= 2 && a.nfr % 2 == 0 && a.f_lo >= 0 && a.f_hi > a.f_lo && a.f_lo % 2 == 0 && a.f_hi % 2 == 0,
-               "tmae_lic_latent: fragments [%d, %d) of blocks of %d (even)", a.f_lo, a.f_hi, a.nfr);
+  TMAE_REQUIRE(a.w && a.y && a.ldx % 8 == 0 && a.ldx >= a.cin, "tmae_lic_latent: operands / strides");
+  TMAE_REQUIRE(a.nfr >= 1 && a.f_lo >= 0 && a.f_hi > a.f_lo && a.f_lo % 2 == 0, "tmae_lic_latent: fragments [%d, %d) "
+               "of blocks of %d (f_lo even)", a.f_lo, a.f_hi, a.nfr);
   TMAE_REQUIRE(a.blk >= 9LL * (a.cin / 32) * a.nfr * 512 || a.f_off[0] + a.f_hi <= a.nfr, "tmae_lic_latent: block stride");
+  TMAE_REQUIRE(a.act == TMAE_ACT_NONE || a.act == TMAE_ACT_GELU, "tmae_lic_latent: act %d", a.act);
+  TMAE_REQUIRE(a.ldy % 4 == 0 && (a.ldy >= 16 * a.f_hi), "tmae_lic_latent: ldy %d", a.ldy);
   for (int j = 0; j < a.nb; ++j)
-    TMAE_REQUIRE(a.x[j] && a.f_off[j] >= 0 && a.f_off[j] % 2 == 0, "tmae_lic_latent: problem %d", j);
+    TMAE_REQUIRE(a.x[j] && a.f_off[j] >= 0 && a.y_s[j] % 4 == 0, "tmae_lic_latent: problem %d", j);
   const int ntile = (a.f_hi - a.f_lo + llat::FPW - 1) / llat::FPW;
   const dim3 grid(a.n * ntile, a.nb);
   hipStream_t st = (hipStream_t)stream;

@@ -296,19 +296,24 @@ def lic_latent_fits(G, cin):
     return G * G <= LSTK_MAXPIX and cin % 32 == 0 and 32 <= cin <= 384
 
 
-def lic_latent(n, G, xs, ldx, cin, w, nfr, blk, f_off, f_lo, f_hi, y, ldy):
-    """Latent-channel partial sums (tmae_lic_latent): for problem j, y[:, 16 f ..] (f32) = the 3x3 conv of xs[j]'s
-    channels [0, cin) with the packed weight fragments f_off[j] + [f_lo, f_hi) of w: blocks of nfr fragments blk
-    elements apart (pack_lic_stack_weight of each stack's latent part, stacked).  Pointers: tensors or raw
+def lic_latent(n, G, xs, ldx, cin, w, nfr, blk, f_off, f_lo, f_hi, y, ldy, y_s=None, biases=None, act=ACT_NONE,
+               y_bf16=False):
+    """Stride-1 3x3 conv with the input resident in LDS (tmae_lic_latent): for problem j, relative fragment r in
+    [f_lo, f_hi): y + y_s[j] (elements), columns 16 r .. = act(bias_j + the conv of xs[j]'s channels [0, cin) with
+    the packed weight fragments f_off[j] + r of w: blocks of nfr fragments blk elements apart (pack_lic_stack_weight,
+    stacked)).  y_s defaults to 16 f_off[j] (the latent partial sums' column blocks).  Pointers: tensors or raw
     addresses."""
     a = _lib.LicLatentArgs()
     a.n, a.G, a.cin, a.nb = n, G, cin, len(xs)
     for j, (x, fo) in enumerate(zip(xs, f_off)):
         a.x[j] = _p(x)
         a.f_off[j] = fo
+        a.y_s[j] = (16 * fo) if y_s is None else y_s[j]
+        a.bias[j] = _p(biases[j]) if biases is not None else None
     a.ldx, a.w, a.nfr, a.blk = ldx, _p(w), nfr, blk
     a.f_lo, a.f_hi = f_lo, f_hi
     a.y, a.ldy = _p(y), ldy
+    a.act, a.y_bf16 = act, int(y_bf16)
     _lib.call("tmae_lic_latent", ctypes.byref(a), _stream())
 
 
