@@ -491,6 +491,13 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
     }
   }
   static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= NS * ROWS * 128, "epilogue region exceeds the LDS ring");
+#if defined(TMAE_GEMM_DIAG) && (TMAE_GEMM_DIAG & 1)  // phase isolation builds: no epilogue (accumulators kept live)
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
+  return;
+#endif
   epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
                            tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
 }
