@@ -189,6 +189,11 @@ typedef struct tmae_lic_stack_args {
   float* sv_t; long long sv_t_s[2];
   void* csv_pre[TMAE_LIC_STACK_MAXL]; void* csv_act[TMAE_LIC_STACK_MAXL]; long long cs_sv[TMAE_LIC_STACK_MAXL];
   float* csv_t; long long cs_t;
+  /* TMAE_LIC_STACK_BWD with racc[0] set: the last layer is the stack's first conv's input gradient, routed by
+   * consecutive channel ranges [0, rlim[0]), [rlim[0], rlim[1]), [rlim[1], rlim[2]) into the f32 accumulators
+   * racc[r] (rows rld[r] apart, +=; problem b1 at b1 * rs[r] elements) instead of GELU' and sv_act -- the
+   * problems must not share an accumulator */
+  float* racc[3]; int rld[3]; int rlim[3]; long long rs[3];
 } tmae_lic_stack_args;
 #define TMAE_LIC_STACK_CHAIN 1
 /* TMAE_LIC_STACK_BWD (training backward, mcm_train.py): the stack's data-gradient chain through LDS.  x1 = the

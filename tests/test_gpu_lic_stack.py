@@ -188,8 +188,8 @@ def _gelu_grad(x):
     return 0.5 * (1.0 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
 
 
-@pytest.mark.parametrize("G,P", [(12, 2), (12, 3), (8, 1)])
-def test_lic_stack_bwd_vs_torch(tmae, G, P):
+@pytest.mark.parametrize("G,P,routed", [(12, 2, False), (12, 3, False), (8, 1, False), (12, 2, True), (8, 1, True)])
+def test_lic_stack_bwd_vs_torch(tmae, G, P, routed):
     """TMAE_LIC_STACK_BWD (the fused data-gradient chain of a stack's layers 4..1, mcm_train._fused_dgrads) against
     torch: per layer dx = conv_transpose2d(d, W) (conv2d's input gradient) * GELU'(pre), rounded to bf16 as the
     kernel keeps it in LDS; every layer's output compared (the weight gradients' operands)"""
@@ -209,8 +209,19 @@ def test_lic_stack_bwd_vs_torch(tmae, G, P):
     for k, l in enumerate((3, 2, 1, 0)):
         st[f"w{k}"] = (wpk[k][0].numel(), 0)
         st[f"s{k}"] = (rows * chans[l + 1], 0)
-    ops.lic_stack_bwd(n, G, dtop.to(torch.bfloat16), chans[5], chans[5], wpk, [chans[l + 1] for l in (3, 2, 1, 0)],
-                      [pres[l].to(torch.bfloat16) for l in (3, 2, 1, 0)], outs, nb=(P, 1), strides=st)
+    couts = [chans[l + 1] for l in (3, 2, 1, 0)]
+    routes = None
+    cin0, split = 96 + 384, (384, 64, 32)  # the first conv's input: latent | support | own slot, as three ranges
+    if routed:  # + the first conv's input gradient, added into per-problem f32 accumulators (prior contents kept)
+        w0 = [_bf(torch.randn(chans[1], cin0, 3, 3, device=DEV) / (9 * cin0) ** 0.5) for _ in range(P)]
+        wpk.append(torch.stack([ops.pack_lic_stack_weight_t(w) for w in w0]).contiguous())
+        st["w4"] = (wpk[4][0].numel(), 0)
+        couts.append(cin0)
+        accs = [[torch.randn(rows, c + 8, device=DEV) for c in split] for _ in range(P)]
+        acc0 = [[a.clone() for a in ap] for ap in accs]
+        routes = [[(a, c + 8, c) for a, c in zip(ap, split)] for ap in accs]
+    ops.lic_stack_bwd(n, G, dtop.to(torch.bfloat16), chans[5], chans[5], wpk, couts,
+                      [pres[l].to(torch.bfloat16) for l in (3, 2, 1, 0)], outs, nb=(P, 1), strides=st, routes=routes)
     torch.cuda.synchronize()
     err = 0.0
     for p in range(P):
@@ -222,6 +233,14 @@ def test_lic_stack_bwd_vs_torch(tmae, G, P):
             ref = dx * _gelu_grad(pres[l][p])
             err = max(err, _maxrel(outs[k][p].float(), ref))
             d = _bf(ref)
+        if routed:  # d = layer 0's pre-activation gradient (bf16): the first conv's input gradient, routed
+            h = d.view(n, G, G, -1).permute(0, 3, 1, 2)
+            dx = F.conv_transpose2d(h, w0[p], padding=1).permute(0, 2, 3, 1).reshape(rows, -1)
+            c0 = 0
+            for a, a0, c in zip(accs[p], acc0[p], split):
+                err = max(err, _maxrel(a[:, :c] - a0[:, :c], dx[:, c0:c0 + c]))
+                assert torch.equal(a[:, c:], a0[:, c:])  # the row padding untouched
+                c0 += c
     check("lic_stack_bwd_maxrel", err, STACK_MAXREL)
 
 

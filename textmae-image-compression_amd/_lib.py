@@ -96,6 +96,7 @@ class LicStackArgs(ctypes.Structure):
         ("sv_t", P), ("sv_t_s", LL * 2),
         ("csv_pre", P * LSTK_MAXL), ("csv_act", P * LSTK_MAXL), ("cs_sv", LL * LSTK_MAXL),
         ("csv_t", P), ("cs_t", LL),
+        ("racc", P * 3), ("rld", I * 3), ("rlim", I * 3), ("rs", LL * 3),
     ]
 
 

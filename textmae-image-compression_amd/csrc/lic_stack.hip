@@ -62,6 +62,9 @@ struct LstkOut {
   bf16* sa;   // training: its GELU output
   float* st;  // training, lrp last layer: the pre-tanh value, f32 [rows][cout]
   int bwd;    // TMAE_LIC_STACK_BWD: out = acc * GELU'(sp) -> sa (global) and, but for the last layer, LDS
+  int route;  // TMAE_LIC_STACK_BWD, last layer with racc: f32 += into the channel-range accumulators
+  float* racc[3];
+  int rld[3], rlim[3];
 };
 
 #ifndef LSTK_OPT
@@ -199,6 +202,25 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
   }
   auto pix = [&](int j) { return 16 * (j0 + j) + fr; };
   auto grow = [&](int j) { return (size_t)img * npix + (size_t)min(pix(j), npix - 1); };
+  if (o.route) {
+    // the stack's first conv's input gradient, routed by channel range into f32 accumulators (+=); the 4
+    // channels of a lane never straddle a range (limits are multiples of 4)
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      if (!okc[i]) continue;
+      const int c = cc[i];
+      const int r = c < o.rlim[0] ? 0 : (c < o.rlim[1] ? 1 : 2);
+      const int c0 = r == 0 ? 0 : o.rlim[r - 1];
+      float* base = o.racc[r] + (c - c0);
+#pragma unroll
+      for (int j = 0; j < MF; ++j) {
+        if (pix(j) >= npix) continue;
+        float* q = base + grow(j) * o.rld[r];
+        store4(q, load4f(q) + acc[i][j]);
+      }
+    }
+    return;
+  }
   if (o.bwd) {
     // data gradient: the forward's GELU inputs of these channels, loaded for the whole item first
     f32x4 pv[NF][MF];
@@ -378,6 +400,7 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
   for (int pass = 0; pass < (chain ? 2 : 1); ++pass) {
     LstkOut o;
     o.bwd = (a->flags & TMAE_LIC_STACK_BWD) != 0;
+    o.route = 0;
     if (pass == 0) {
       o.add = a->addend ? a->addend + b1 * a->a_s[0] + b2 * a->a_s[1] : nullptr;
       o.ld_add = a->ld_add;
@@ -449,6 +472,15 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
       }
       L.cin = cin;
       const bool first = l == 0, last = l + 1 == nl;
+      o.route = o.bwd && last && a->racc[0] != nullptr;
+      if (o.route) {
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          o.racc[r] = a->racc[r] ? a->racc[r] + b1 * a->rs[r] : nullptr;
+          o.rld[r] = a->rld[r];
+          o.rlim[r] = a->rlim[r];
+        }
+      }
       if (pass == 0) {
         o.sp = a->sv_pre[l] && (!last || o.bwd) ? reinterpret_cast<bf16*>(a->sv_pre[l]) + b1 * a->sv_s[l][0] + b2 * a->sv_s[l][1]
                                                 : nullptr;
@@ -523,8 +555,19 @@ extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
   if (bwd) {
     TMAE_REQUIRE(!(a.flags & TMAE_LIC_STACK_CHAIN) && !a.addend && !a.lrp_src && !a.x2 && !a.sv_t,
                  "tmae_lic_stack: the backward chain takes no chain / addend / lrp / second source");
+    const bool rt = a.racc[0] != nullptr;
     for (int l = 0; l < a.nlayers; ++l)
-      TMAE_REQUIRE(a.w[l] && a.sv_pre[l] && a.sv_act[l], "tmae_lic_stack: backward layer %d needs w / sv_pre / sv_act", l);
+      TMAE_REQUIRE(a.w[l] && ((rt && l + 1 == a.nlayers) || (a.sv_pre[l] && a.sv_act[l])),
+                   "tmae_lic_stack: backward layer %d needs w / sv_pre / sv_act", l);
+    if (rt) {
+      const int cl = a.cout[a.nlayers - 1];
+      TMAE_REQUIRE(a.rlim[0] >= 0 && a.rlim[0] <= a.rlim[1] && a.rlim[1] <= a.rlim[2] && a.rlim[2] == cl &&
+                   a.rlim[0] % 4 == 0 && a.rlim[1] % 4 == 0, "tmae_lic_stack: routes %d / %d / %d of %d channels",
+                   a.rlim[0], a.rlim[1], a.rlim[2], cl);
+      for (int r = 0; r < 3; ++r)
+        TMAE_REQUIRE((r == 0 ? a.rlim[0] : a.rlim[r] - a.rlim[r - 1]) == 0 || (a.racc[r] && a.rld[r] % 4 == 0),
+                     "tmae_lic_stack: route %d accumulator", r);
+    }
   }
   TMAE_REQUIRE(a.c1 >= 0 && a.c2 >= 0 && (a.c2 == 0 || a.x2 != nullptr), "tmae_lic_stack: channels %d + %d", a.c1, a.c2);
   TMAE_REQUIRE(a.c1 % 8 == 0 && a.c2 % 8 == 0 && a.ld1 % 8 == 0 && (a.c2 == 0 || a.ld2 % 8 == 0),
@@ -534,8 +577,8 @@ extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
     TMAE_REQUIRE((a.w[l] != nullptr || (l == 0 && a.c1 + a.c2 == 0)) && (a.bias[l] != nullptr || bwd),
                  "tmae_lic_stack: layer %d weights", l);
     TMAE_REQUIRE(a.cout[l] >= 4 && a.cout[l] % 8 == 0, "tmae_lic_stack: layer %d cout %d (multiple of 8)", l, a.cout[l]);
-    TMAE_REQUIRE((l + 1 == a.nlayers && !bwd) || pad32(a.cout[l]) <= MAXC, "tmae_lic_stack: layer %d cout %d exceeds %d",
-                 l, a.cout[l], MAXC);
+    TMAE_REQUIRE((l + 1 == a.nlayers && (!bwd || a.racc[0])) || pad32(a.cout[l]) <= MAXC,
+                 "tmae_lic_stack: layer %d cout %d exceeds %d", l, a.cout[l], MAXC);
   }
   TMAE_REQUIRE(!a.lrp_src || !a.y_f32, "tmae_lic_stack: lrp output is bf16");
   if (a.flags & TMAE_LIC_STACK_CHAIN) {

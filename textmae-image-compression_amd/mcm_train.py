@@ -674,6 +674,7 @@ class TrainExec(_VitTrainBase):
     USE_LIC_STACK = True  # test hook: False runs the per-layer conv launches in the bf16 training forward too
     USE_LIC_LATENT = True  # False: the latent partial sums as two implicit-GEMM conv launches
     USE_LIC_STACK_BWD = True  # False: the slice stacks' data gradients as one conv launch per layer
+    FUSE_FIRST_DGRAD = True   # the serial slices' first-layer input gradients inside the fused chain (routed)
     _fused_bwd = False
 
     def _fused_ok(self):
@@ -1319,11 +1320,13 @@ class TrainExec(_VitTrainBase):
             self._wg_flush()
             self._ready(cs[j][0].bias)  # every gradient of slices >= i0 + j is final (DP hand-off per slice)
 
-    def _fused_dgrads(self, stacks):
+    def _fused_dgrads(self, stacks, routes=None):
         """layers 4..1 data gradients of P same-shape stacks (convs, saved, dtop) in ONE tmae_lic_stack backward
         launch (the chain through LDS, TMAE_LIC_STACK_BWD), or None when the operands do not allow it (the per-layer
         launches then run).  Returns d[l] for l = 0..4: the gradient w.r.t. layer l's pre-activation, a list over the
-        problems (d[4] = the dtops); d[0..3] are views of one [P][Mp][cout] bf16 buffer per layer."""
+        problems (d[4] = the dtops); d[0..3] are views of one [P][Mp][cout] bf16 buffer per layer.  routes (one list
+        per problem, the problems' accumulators disjoint): the first layers' input gradients too, routed like
+        T.conv_dgrad's (the caller then skips them)."""
         if not self._fused_bwd:
             return None
         P, Mp = len(stacks), self.Mp
@@ -1348,8 +1351,13 @@ class TrainExec(_VitTrainBase):
         for k, l in enumerate((3, 2, 1, 0)):
             st[f"w{k}"] = (ws[k][0].numel() if P > 1 else 0, 0)
             st[f"s{k}"] = (Mp * couts[l], 0)
-        ops.lic_stack_bwd(self.batch, self.g, dts[0], couts[4], couts[4], ws, [couts[l] for l in (3, 2, 1, 0)],
-                          [p_[0] for p_ in pres], outs, nb=(P, 1), strides=st)
+        lcouts = [couts[l] for l in (3, 2, 1, 0)]
+        if routes is not None:  # + the first layers' input gradients, routed
+            ws.append(self.w.packed([s[0][0].weight for s in stacks], "licT"))
+            st["w4"] = (ws[4][0].numel() if P > 1 else 0, 0)
+            lcouts.append(convs0[0].in_channels)
+        ops.lic_stack_bwd(self.batch, self.g, dts[0], couts[4], couts[4], ws, lcouts, [p_[0] for p_ in pres], outs,
+                          nb=(P, 1), strides=st, routes=routes)
         d = [None] * 5
         for k, l in enumerate((3, 2, 1, 0)):
             d[l] = [outs[k][p_] for p_ in range(P)]
@@ -1363,7 +1371,7 @@ class TrainExec(_VitTrainBase):
         a's before b's"""
         dt, W, G, B, g, Mp = self.dtype, self.w, self.grad, self.batch, self.g, self.Mp
         (ca, sa, da, fa, ra), (cb, sb, db, fb, rb) = a, b
-        fd = self._fused_dgrads([(ca, sa, da), (cb, sb, db)])
+        fd = self._fused_dgrads([(ca, sa, da), (cb, sb, db)], routes=[ra, rb] if self.FUSE_FIRST_DGRAD else None)
         for l in range(4, 0, -1):
             cin = ca[l].in_channels
             dl = (fd[l][0], fd[l][1]) if fd is not None else (da, db)
@@ -1385,14 +1393,15 @@ class TrainExec(_VitTrainBase):
             cin, cout = c1 + c2, c.out_channels
             self._wg(d, x1, cout, 9 * cin, Mp, G(c.weight), dt, ldb=ld1,
                      conv=dict(x2=x2, c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
-            T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
+            if fd is None or not self.FUSE_FIRST_DGRAD:
+                T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
         self._wg_flush()
 
     def _stack_bwd(self, convs, saved, dtop, first, routes, defer=None):
         """backward of one 5-layer slice stack; with `defer` (a list) the weight gradients of layers 4..1 are
         appended to it as (_wg_many item, shape args) instead of being queued"""
         dt, W, G, B, g, Mp = self.dtype, self.w, self.grad, self.batch, self.g, self.Mp
-        fd = self._fused_dgrads([(convs, saved, dtop)])
+        fd = self._fused_dgrads([(convs, saved, dtop)], routes=[routes] if self.FUSE_FIRST_DGRAD else None)
         d = dtop
         for l in range(4, 0, -1):
             c = convs[l]
@@ -1419,7 +1428,8 @@ class TrainExec(_VitTrainBase):
         self._wg(d, x1, cout, 9 * cin, Mp, G(c.weight), dt, ldb=ld1,
                  conv=dict(x2=x2, c1=c1, ld2=ld2, H=g, W=g, cin=cin), layout="conv", bias=G(c.bias))
         # zero-width routes (no support slices yet) stay in place: their limits still partition the channels
-        T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
+        if fd is None or not self.FUSE_FIRST_DGRAD:
+            T.conv_dgrad(d, W.conv_dg(c.weight), B, g, g, 1, cout, cin, dt, routes=routes)
         self._wg_flush()
 
 def _bias(b):

@@ -268,19 +268,37 @@ def pack_lic_stack_weight_t(w: torch.Tensor, dtype=torch.bfloat16) -> torch.Tens
     return pack_lic_stack_weight(w.detach().transpose(0, 1).flip(2, 3), dtype)
 
 
-def lic_stack_bwd(n, G, dtop, ldt, c_top, weights, couts, pres, outs, nb=(1, 1), strides=None):
+def lic_stack_bwd(n, G, dtop, ldt, c_top, weights, couts, pres, outs, nb=(1, 1), strides=None, routes=None):
     """The data-gradient chain of a slice stack's layers L-1..1 in one launch (tmae_lic_stack, TMAE_LIC_STACK_BWD):
     dtop [rows][c_top] (bf16, rows ldt apart) is the gradient of the stack's output; layer l (the transposed conv
     of forward layer L-1-l, weights[l] from pack_lic_stack_weight_t) writes outs[l] = (its conv) * GELU'(pres[l]),
-    bf16 [rows][couts[l]].  `strides` maps x1, w<l>, s<l> (pres[l] / outs[l]) -> per-problem (s1, s2)."""
+    bf16 [rows][couts[l]].  `strides` maps x1, w<l>, s<l> (pres[l] / outs[l]) -> per-problem (s1, s2).
+    routes (optional, one list per problem of (acc_f32, ld, ncols), <= 3 consecutive channel ranges): the last
+    layer is the stack's first conv's input gradient, added into those accumulators (no pres / outs entry)."""
     a = LicStackArgs()
+    if routes is not None:
+        lim = 0
+        for r in range(3):
+            if r < len(routes[0]):
+                acc, ld, nc = routes[0][r]
+                a.racc[r], a.rld[r] = _p(acc), ld
+                if len(routes) > 1:
+                    deltas = {_p(rt[r][0]) - _p(acc) for rt in routes[1:]} if nc else {0}
+                    if len(routes) > 2:
+                        steps = [_p(routes[k + 1][r][0]) - _p(routes[k][r][0]) for k in range(len(routes) - 1)]
+                        if len(set(steps)) != 1:
+                            raise ValueError("lic_stack_bwd routes: accumulators not at a constant stride")
+                    a.rs[r] = (next(iter(deltas)) // 4) if nc else 0
+                lim += nc
+            a.rlim[r] = lim
     a.n, a.G, a.nlayers = n, G, len(couts)
     a.nb1, a.nb2 = nb
     a.x1, a.c1, a.ld1 = _p(dtop), c_top, ldt
     a.flags = 2
-    for l, (w, c, pre, out) in enumerate(zip(weights, couts, pres, outs)):
+    for l, (w, c) in enumerate(zip(weights, couts)):
         a.w[l], a.cout[l] = _p(w), c
-        a.sv_pre[l], a.sv_act[l] = _p(pre), _p(out)
+        if l < len(pres):
+            a.sv_pre[l], a.sv_act[l] = _p(pres[l]), _p(outs[l])
     for name, (s1, s2) in (strides or {}).items():
         if name[0] == "w":
             a.w_s[int(name[1:])][:] = (s1, s2)
