@@ -48,6 +48,10 @@ struct LstkLayer {
   int cin, cout;
 };
 
+// the argument block is read in place from the kernarg segment (scalar loads, layer fields indexed at
+// run time): a by-value copy indexed by the layer number would live in scratch
+typedef const __attribute__((address_space(4))) tmae_lic_stack_args LstkArgs;
+
 // per-workgroup outputs of the last layer / the layer-0 addend, problem offsets applied
 struct LstkOut {
   const float* add;
@@ -62,9 +66,9 @@ struct LstkOut {
   bf16* sa;   // training: its GELU output
   float* st;  // training, lrp last layer: the pre-tanh value, f32 [rows][cout]
   int bwd;    // TMAE_LIC_STACK_BWD: out = acc * GELU'(sp) -> sa (global) and, but for the last layer, LDS
-  int route;  // TMAE_LIC_STACK_BWD, last layer with racc: f32 += into the channel-range accumulators
-  float* racc[3];
-  int rld[3], rlim[3];
+  int route;  // TMAE_LIC_STACK_BWD, last layer with racc: f32 += into the channel-range accumulators,
+  LstkArgs* ra;  // read from the kernarg block at the epilogue (copies held per layer spilled SGPRs to scratch)
+  int rb1;       // the problem index the route strides apply to
 };
 
 #ifndef LSTK_OPT
@@ -90,7 +94,7 @@ __device__ __forceinline__ bf16x8 lstk_lds8(const unsigned char* lb, unsigned of
 // MFMAs (at NF = 1 one 1-KiB read per 16-cycle MFMA on each SIMD is exactly the LDS array's 256 B/clk).
 // All 9 x NKC K-steps are unrolled: A fragments stream through a static register ring D steps ahead,
 // B fragments are read one step ahead.
-template <int NF, int MF, int NKC>
+template <int NF, int MF, int NKC, bool BWD>
 __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool last, const LstkOut& o, int img,
                                           int f0, int j0, unsigned char* lb, unsigned in_off, unsigned out_off,
                                           int npix, int G, int lane) {
@@ -198,10 +202,11 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
   for (int i = 0; i < NF; ++i) {
     cc[i] = 16 * (f0 + i) + 4 * fq;
     okc[i] = cc[i] < L.cout;
-    bias[i] = o.bwd ? f32x4{0.f, 0.f, 0.f, 0.f} : load4f(L.b + (okc[i] ? cc[i] : 0));
+    bias[i] = BWD ? f32x4{0.f, 0.f, 0.f, 0.f} : load4f(L.b + (okc[i] ? cc[i] : 0));
   }
   auto pix = [&](int j) { return 16 * (j0 + j) + fr; };
   auto grow = [&](int j) { return (size_t)img * npix + (size_t)min(pix(j), npix - 1); };
+  if constexpr (BWD) {
   if (o.route) {
     // the stack's first conv's input gradient, routed by channel range into f32 accumulators (+=); the 4
     // channels of a lane never straddle a range (limits are multiples of 4)
@@ -209,19 +214,21 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
     for (int i = 0; i < NF; ++i) {
       if (!okc[i]) continue;
       const int c = cc[i];
-      const int r = c < o.rlim[0] ? 0 : (c < o.rlim[1] ? 1 : 2);
-      const int c0 = r == 0 ? 0 : o.rlim[r - 1];
-      float* base = o.racc[r] + (c - c0);
+      const int l0 = o.ra->rlim[0], l1 = o.ra->rlim[1];
+      const int r = c < l0 ? 0 : (c < l1 ? 1 : 2);
+      const int c0 = r == 0 ? 0 : (r == 1 ? l0 : l1);
+      const int ld = o.ra->rld[r];
+      float* base = o.ra->racc[r] + o.rb1 * o.ra->rs[r] + (c - c0);
 #pragma unroll
       for (int j = 0; j < MF; ++j) {
         if (pix(j) >= npix) continue;
-        float* q = base + grow(j) * o.rld[r];
+        float* q = base + grow(j) * ld;
         store4(q, load4f(q) + acc[i][j]);
       }
     }
     return;
   }
-  if (o.bwd) {
+  {
     // data gradient: the forward's GELU inputs of these channels, loaded for the whole item first
     f32x4 pv[NF][MF];
 #pragma unroll
@@ -245,6 +252,7 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
       }
     return;
   }
+  } else {  // forward
   if (!last) {
     if (first && o.add && !(LSTK_DIAG & 64)) {
       f32x4 ad[NF][MF];
@@ -328,14 +336,15 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
         }
       }
   }
+  }  // forward
 }
 
-template <int NF, int MF>
+template <int NF, int MF, bool BWD>
 __device__ __forceinline__ void lstk_dispatch(int nkc, const LstkLayer& L, bool first, bool last, const LstkOut& o,
                                               int img, int f0, int j0, unsigned char* lb, unsigned in_off,
                                               unsigned out_off, int npix, int G, int lane) {
 #define LSTK_CASE(K) \
-  case K: lstk_item<NF, MF, K>(L, first, last, o, img, f0, j0, lb, in_off, out_off, npix, G, lane); break;
+  case K: lstk_item<NF, MF, K, BWD>(L, first, last, o, img, f0, j0, lb, in_off, out_off, npix, G, lane); break;
   switch (nkc) {
     LSTK_CASE(0) LSTK_CASE(1) LSTK_CASE(2) LSTK_CASE(3) LSTK_CASE(4) LSTK_CASE(5) LSTK_CASE(6) LSTK_CASE(7)
     default: break;
@@ -343,10 +352,9 @@ __device__ __forceinline__ void lstk_dispatch(int nkc, const LstkLayer& L, bool 
 #undef LSTK_CASE
 }
 
-// the argument block is read in place from the kernarg segment (scalar loads, layer fields indexed at
-// run time): a by-value copy indexed by the layer number would live in scratch
-typedef const __attribute__((address_space(4))) tmae_lic_stack_args LstkArgs;
 
+// BWD (TMAE_LIC_STACK_BWD) is its own instantiation: the backward epilogue's registers stay out of the forward's
+template <bool BWD>
 __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack_args) {
   using namespace lstk;
   LstkArgs* a = (LstkArgs*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -399,7 +407,7 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
   int cin = cin0;
   for (int pass = 0; pass < (chain ? 2 : 1); ++pass) {
     LstkOut o;
-    o.bwd = (a->flags & TMAE_LIC_STACK_BWD) != 0;
+    o.bwd = BWD;
     o.route = 0;
     if (pass == 0) {
       o.add = a->addend ? a->addend + b1 * a->a_s[0] + b2 * a->a_s[1] : nullptr;
@@ -473,14 +481,8 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
       L.cin = cin;
       const bool first = l == 0, last = l + 1 == nl;
       o.route = o.bwd && last && a->racc[0] != nullptr;
-      if (o.route) {
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-          o.racc[r] = a->racc[r] ? a->racc[r] + b1 * a->rs[r] : nullptr;
-          o.rld[r] = a->rld[r];
-          o.rlim[r] = a->rlim[r];
-        }
-      }
+      o.ra = a;
+      o.rb1 = (int)b1;
       if (pass == 0) {
         o.sp = a->sv_pre[l] && (!last || o.bwd) ? reinterpret_cast<bf16*>(a->sv_pre[l]) + b1 * a->sv_s[l][0] + b2 * a->sv_s[l][1]
                                                 : nullptr;
@@ -509,22 +511,22 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
         const int ng = (nfr + 1) >> 1;
         if (nfr >= 14 || !halves) {
           for (int it = wave; it < ng; it += NW)
-            lstk_dispatch<2, 9>(nkc, L, first, last, o, img, 2 * it, 0, lb, in_off, out_off, npix, G, lane);
+            lstk_dispatch<2, 9, BWD>(nkc, L, first, last, o, img, 2 * it, 0, lb, in_off, out_off, npix, G, lane);
         } else {
           for (int it = wave; it < 2 * ng; it += NW) {
             const int g = it < ng ? it : it - ng;
-            if (it < ng) lstk_dispatch<2, 5>(nkc, L, first, last, o, img, 2 * g, 0, lb, in_off, out_off, npix, G, lane);
-            else lstk_dispatch<2, 4>(nkc, L, first, last, o, img, 2 * g, 5, lb, in_off, out_off, npix, G, lane);
+            if (it < ng) lstk_dispatch<2, 5, BWD>(nkc, L, first, last, o, img, 2 * g, 0, lb, in_off, out_off, npix, G, lane);
+            else lstk_dispatch<2, 4, BWD>(nkc, L, first, last, o, img, 2 * g, 5, lb, in_off, out_off, npix, G, lane);
           }
         }
       } else if (!halves) {
         for (int it = wave; it < nfr; it += NW)
-          lstk_dispatch<1, 5>(nkc, L, first, last, o, img, it, 0, lb, in_off, out_off, npix, G, lane);
+          lstk_dispatch<1, 5, BWD>(nkc, L, first, last, o, img, it, 0, lb, in_off, out_off, npix, G, lane);
       } else {
         for (int it = wave; it < 2 * nfr; it += NW) {
           const int f = it < nfr ? it : it - nfr;
-          if (it < nfr) lstk_dispatch<1, 5>(nkc, L, first, last, o, img, f, 0, lb, in_off, out_off, npix, G, lane);
-          else lstk_dispatch<1, 4>(nkc, L, first, last, o, img, f, 5, lb, in_off, out_off, npix, G, lane);
+          if (it < nfr) lstk_dispatch<1, 5, BWD>(nkc, L, first, last, o, img, f, 0, lb, in_off, out_off, npix, G, lane);
+          else lstk_dispatch<1, 4, BWD>(nkc, L, first, last, o, img, f, 5, lb, in_off, out_off, npix, G, lane);
         }
       }
       if (!last) {
@@ -600,7 +602,8 @@ extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
     TMAE_REQUIRE(!a.csv_pre[l] == !a.csv_act[l], "tmae_lic_stack: chain layer %d keeps pre and output together", l);
   TMAE_REQUIRE(!a.sv_t || a.lrp_src, "tmae_lic_stack: sv_t is the lrp stack's pre-tanh value");
   const int nwg = a.n * a.nb1 * a.nb2;
-  hipLaunchKernelGGL(lic_stack_kernel, dim3(nwg), dim3(NW * 64), 0, (hipStream_t)stream, a);
+  if (bwd) hipLaunchKernelGGL(lic_stack_kernel<true>, dim3(nwg), dim3(NW * 64), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(lic_stack_kernel<false>, dim3(nwg), dim3(NW * 64), 0, (hipStream_t)stream, a);
   TMAE_LAUNCH_CHECK("tmae_lic_stack");
 }
 
