@@ -515,8 +515,11 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
 // fixed order (bitwise reproducible), and nothing is recomputed: the two-phase form above computed S and dP twice
 // (the exp and dS VALU of phase 2) and restaged K / V.  LDS: Q, dO, K [Tpad][LDR] bf16, dS 32 x 32 bf16 per wave,
 // dQ [DH][Tpad + 4] f32 (row stride 4 mod 32 dwords: the 16-B read-modify-writes of a half-wave hit 64 banks).
-template <int DH>
-__global__ void __launch_bounds__(DH == 32 ? 1024 : 512)  // dh 64: <= 256 keys, up to 256 VGPRs
+// MAXT: the launch bound.  dh 32 up to 512 threads (<= 256 keys: two workgroups per CU at 128 VGPRs) and from 11
+// waves on takes 1024; 9-10 waves (the MCM decoder's 257 tokens) run one workgroup per CU (> 80 KB of LDS), so that
+// instance is bounded at 640 threads -> 3 waves per SIMD, 168 VGPRs (at 128 it spilled 10 VGPRs to scratch)
+template <int DH, int MAXT = (DH == 32 ? 1024 : 512)>
+__global__ void __launch_bounds__(MAXT)  // dh 64: <= 256 keys, up to 256 VGPRs
 mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, const bf16* __restrict__ dout,
                      const float* __restrict__ lse, bf16* __restrict__ dqkv, int Tn, int H, int Tpad, float scale) {
   constexpr int LDR = AttnBwd<DH>::LDR;
@@ -852,8 +855,14 @@ static int mha_bwd_launch(const void* qkv, const void* o, const void* dout, cons
     const size_t lds1 = (size_t)(DH == 32 ? 2 : 3) * Tpad * LDR * 2 + (size_t)(Tpad / 32) * 2048 +
                         (size_t)DH * (Tpad + 4) * 4 + (size_t)2 * Tpad * 4;
     if (AttnBwdOnePass<DH>::value && lds1 <= 160 * 1024) {
-      hipLaunchKernelGGL((mha_bwd1_bf16_kernel<AttnBwdOnePass<DH>::value ? DH : 32>), dim3(B * H), dim3(nthr), lds1,
-                         st, (const bf16*)qkv, (const bf16*)o, (const bf16*)dout, lse, (bf16*)dqkv, Tn, H, Tpad, scale);
+      constexpr int D1 = AttnBwdOnePass<DH>::value ? DH : 32;
+      constexpr int M9 = D1 == 32 ? 640 : 512;  // the 9-10-wave instance (dh 32 only)
+      if (D1 == 32 && nthr > 512 && nthr <= 640)
+        hipLaunchKernelGGL((mha_bwd1_bf16_kernel<D1, M9>), dim3(B * H), dim3(nthr), lds1, st, (const bf16*)qkv,
+                           (const bf16*)o, (const bf16*)dout, lse, (bf16*)dqkv, Tn, H, Tpad, scale);
+      else
+        hipLaunchKernelGGL((mha_bwd1_bf16_kernel<D1>), dim3(B * H), dim3(nthr), lds1, st, (const bf16*)qkv,
+                           (const bf16*)o, (const bf16*)dout, lse, (bf16*)dqkv, Tn, H, Tpad, scale);
       TMAE_LAUNCH_CHECK("tmae_mha_bwd");
     }
     const size_t lds = (size_t)2 * Tpad * LDR * 2 + (size_t)2 * Tpad * 4;

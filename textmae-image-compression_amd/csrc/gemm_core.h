@@ -323,6 +323,10 @@ __device__ __forceinline__ void epi_emit8_pre(const EPI& e, int m, int n, f32x4 
   }
 }
 
+#ifndef TMAE_EPI_DEEP_ALWAYS
+#define TMAE_EPI_DEEP_ALWAYS 0  // A/B builds: 1 = the one-block-ahead fetch for every instantiation
+#endif
+
 template <int WN> struct EpiRegion {
   static constexpr int ST = WN + 4;          // row stride (floats)
   static constexpr int FLOATS = 16 * ST;     // one wave's region
@@ -342,16 +346,21 @@ __device__ __forceinline__ void epilogue_lds(const EPI& epi, const f32x4 (&acc)[
   const int ncol = n0 + 8 * cc;
   const EPI e = epi_for_lane(epi, ncol, N);
   using Pre = typename PreOf<EPI>::type;
-  Pre pf[2][QR];
+  // Fetch depth: one block ahead (two operand sets live) unless those sets and the accumulators exceed the
+  // register file -- the 8-wave 256 x 256 tile with the dgrad epilogue's 16-float sets (128 + 128 VGPRs)
+  // spilled 60 VGPRs to scratch; there the next block's operands are fetched after this block's emits.
+  constexpr int kAccRegs = TN * TM * 4, kPreRegs = 2 * QR * (int)(sizeof(Pre) / 4);
+  constexpr int PD = (HasFetch<EPI>::value && kAccRegs + kPreRegs > 224 && !TMAE_EPI_DEEP_ALWAYS) ? 1 : 2;
+  Pre pf[PD][QR];
 #pragma unroll
   for (int q = 0; q < QR; ++q) epi_fetch(e, m0 + q * RPI + rr, ncol, M, N, pf[0][q]);
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
 #pragma unroll
     for (int i = 0; i < TN; ++i) *reinterpret_cast<f32x4*>(region + fr * ST + 16 * i + 4 * fq) = acc[i][j];
-    if (j + 1 < TM) {
+    if (PD == 2 && j + 1 < TM) {
 #pragma unroll
-      for (int q = 0; q < QR; ++q) epi_fetch(e, m0 + 16 * (j + 1) + q * RPI + rr, ncol, M, N, pf[(j + 1) & 1][q]);
+      for (int q = 0; q < QR; ++q) epi_fetch(e, m0 + 16 * (j + 1) + q * RPI + rr, ncol, M, N, pf[(j + 1) % PD][q]);
     }
 #pragma unroll
     for (int q = 0; q < QR; ++q) {
@@ -360,7 +369,11 @@ __device__ __forceinline__ void epilogue_lds(const EPI& epi, const f32x4 (&acc)[
       const f32x4 lo = *reinterpret_cast<const f32x4*>(src);
       const f32x4 hi = *reinterpret_cast<const f32x4*>(src + 4);
       const int m = m0 + 16 * j + row;
-      if (m < M) epi_emit8_pre(e, m, ncol, lo, hi, N, pf[j & 1][q]);
+      if (m < M) epi_emit8_pre(e, m, ncol, lo, hi, N, pf[j % PD][q]);
+    }
+    if (PD == 1 && j + 1 < TM) {
+#pragma unroll
+      for (int q = 0; q < QR; ++q) epi_fetch(e, m0 + 16 * (j + 1) + q * RPI + rr, ncol, M, N, pf[0][q]);
     }
   }
 }

@@ -1119,31 +1119,43 @@ __device__ __forceinline__ float eb_softplus_grad(float x) { return x > 20.0f ? 
 __device__ __forceinline__ float eb_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 __device__ __forceinline__ void eb_load(const tmae_eb_params& p, int c, EbCh& w) {
+#pragma unroll
   for (int j = 0; j < 3; ++j) {
     w.sp0[j] = eb_softplus(p.matrix[0][c * 3 + j]);
     w.b0[j] = p.bias[0][c * 3 + j];
     w.tf0[j] = tanhf(p.factor[0][c * 3 + j]);
   }
+#pragma unroll
   for (int l = 0; l < 3; ++l) {
+#pragma unroll
     for (int e = 0; e < 9; ++e) w.sp[l][e] = eb_softplus(p.matrix[l + 1][c * 9 + e]);
+#pragma unroll
     for (int j = 0; j < 3; ++j) {
       w.bl[l][j] = p.bias[l + 1][c * 3 + j];
       w.tf[l][j] = tanhf(p.factor[l + 1][c * 3 + j]);
     }
   }
+#pragma unroll
   for (int k = 0; k < 3; ++k) w.sp4[k] = eb_softplus(p.matrix[4][c * 3 + k]);
   w.b4 = p.bias[4][c];
 }
 
-// f(v); for upstream gradient go also accumulates the packed-parameter gradients (gr != null) and df/dv
-__device__ float eb_fwd_bwd(const EbCh& w, float v, float go, EbGrad* gr, float* dv) {
+// f(v); for upstream gradient go also accumulates the packed-parameter gradients (GR) and df/dv (dv != null).
+// gr: the packed gradient sums, EbCh field order (sp0 0, b0 3, tf0 6, sp 9, bl 36, tf 45, sp4 54, b4 57), in a
+// plain float array, loops unrolled, GR a template flag rather than a null test: comparing the private array's
+// address with null kept the 58 sums in scratch (236 B per lane, every accumulation a scratch read-modify-write)
+template <bool GR>
+__device__ __forceinline__ float eb_fwd_bwd(const EbCh& w, float v, float go, float* gr, float* dv) {
   float u[4][3], th[4][3], h[4][3];
+#pragma unroll
   for (int j = 0; j < 3; ++j) {
     u[0][j] = w.sp0[j] * v + w.b0[j];
     th[0][j] = tanhf(u[0][j]);
     h[0][j] = u[0][j] + w.tf0[j] * th[0][j];
   }
+#pragma unroll
   for (int l = 0; l < 3; ++l) {
+#pragma unroll
     for (int i = 0; i < 3; ++i) {
       u[l + 1][i] = (w.sp[l][3 * i] * h[l][0] + w.sp[l][3 * i + 1] * h[l][1] + w.sp[l][3 * i + 2] * h[l][2]) + w.bl[l][i];
       th[l + 1][i] = tanhf(u[l + 1][i]);
@@ -1151,35 +1163,41 @@ __device__ float eb_fwd_bwd(const EbCh& w, float v, float go, EbGrad* gr, float*
     }
   }
   const float f = (w.sp4[0] * h[3][0] + w.sp4[1] * h[3][1] + w.sp4[2] * h[3][2]) + w.b4;
-  if (!gr && !dv) return f;
+  if (!GR && !dv) return f;
   float dh[3];
+#pragma unroll
   for (int k = 0; k < 3; ++k) {
     dh[k] = go * w.sp4[k];
-    if (gr) gr->sp4[k] += go * h[3][k];
+    if constexpr (GR) gr[54 + k] += go * h[3][k];
   }
-  if (gr) gr->b4 += go;
+  if constexpr (GR) gr[57] += go;
+#pragma unroll
   for (int l = 2; l >= 0; --l) {
     float du[3], dprev[3] = {0.f, 0.f, 0.f};
+#pragma unroll
     for (int i = 0; i < 3; ++i) {
       du[i] = dh[i] * (1.0f + w.tf[l][i] * (1.0f - th[l + 1][i] * th[l + 1][i]));
-      if (gr) {
-        gr->tf[l][i] += dh[i] * th[l + 1][i];
-        gr->bl[l][i] += du[i];
+      if constexpr (GR) {
+        gr[45 + 3 * l + i] += dh[i] * th[l + 1][i];
+        gr[36 + 3 * l + i] += du[i];
       }
+#pragma unroll
       for (int j = 0; j < 3; ++j) {
-        if (gr) gr->sp[l][3 * i + j] += du[i] * h[l][j];
+        if constexpr (GR) gr[9 + 9 * l + 3 * i + j] += du[i] * h[l][j];
         dprev[j] += w.sp[l][3 * i + j] * du[i];
       }
     }
+#pragma unroll
     for (int j = 0; j < 3; ++j) dh[j] = dprev[j];
   }
   float d = 0.0f;
+#pragma unroll
   for (int j = 0; j < 3; ++j) {
     const float du = dh[j] * (1.0f + w.tf0[j] * (1.0f - th[0][j] * th[0][j]));
-    if (gr) {
-      gr->tf0[j] += dh[j] * th[0][j];
-      gr->b0[j] += du;
-      gr->sp0[j] += du * v;
+    if constexpr (GR) {
+      gr[6 + j] += dh[j] * th[0][j];
+      gr[3 + j] += du;
+      gr[j] += du * v;
     }
     d += w.sp0[j] * du;
   }
@@ -1197,8 +1215,8 @@ eb_bwd_kernel(tmae_eb_params p, const float* __restrict__ z, const float* __rest
   EbCh w;
   eb_load(p, c, w);
   const float med = p.quantiles[c * 3 + 1];
-  EbGrad gr;
-  float* gf = reinterpret_cast<float*>(&gr);
+  float gf[EB_NG];
+#pragma unroll
   for (int k = 0; k < EB_NG; ++k) gf[k] = 0.0f;
   const int total = n * HW;
   for (int e = threadIdx.x; e < total; e += 256) {
@@ -1207,8 +1225,8 @@ eb_bwd_kernel(tmae_eb_params p, const float* __restrict__ z, const float* __rest
     const size_t nchw = ((size_t)b * C + c) * HW + pix;
     const float zv = z[nhwc];
     const float x = noise ? zv + noise[nchw] : rintf(zv - med) + med;
-    const float lower = eb_fwd_bwd(w, x - 0.5f, 0.0f, nullptr, nullptr);
-    const float upper = eb_fwd_bwd(w, x + 0.5f, 0.0f, nullptr, nullptr);
+    const float lower = eb_fwd_bwd<false>(w, x - 0.5f, 0.0f, nullptr, nullptr);
+    const float upper = eb_fwd_bwd<false>(w, x + 0.5f, 0.0f, nullptr, nullptr);
     const float sum = lower + upper;
     const float s = sum > 0.0f ? -1.0f : (sum < 0.0f ? 1.0f : 0.0f);
     const float su = eb_sigmoid(s * upper), sl = eb_sigmoid(s * lower);
@@ -1219,8 +1237,8 @@ eb_bwd_kernel(tmae_eb_params p, const float* __restrict__ z, const float* __rest
     const float gu = gl * sg * s * su * (1.0f - su);
     const float glo = -gl * sg * s * sl * (1.0f - sl);
     float dvu = 0.0f, dvl = 0.0f;
-    if (gu != 0.0f) eb_fwd_bwd(w, x + 0.5f, gu, &gr, &dvu);
-    if (glo != 0.0f) eb_fwd_bwd(w, x - 0.5f, glo, &gr, &dvl);
+    if (gu != 0.0f) eb_fwd_bwd<true>(w, x + 0.5f, gu, gf, &dvu);
+    if (glo != 0.0f) eb_fwd_bwd<true>(w, x - 0.5f, glo, gf, &dvl);
     float d = gzhat ? gzhat[nhwc] : 0.0f;  // quantize_ste pass-through (MCM.py:742-744)
     if (noise) d += dvu + dvl;             // eval: x = round(z - med) + med, no gradient to z
     dz[nhwc] = d;
@@ -1228,6 +1246,7 @@ eb_bwd_kernel(tmae_eb_params p, const float* __restrict__ z, const float* __rest
   // workgroup reduction of the 58 parameter gradients
   __shared__ float red[EB_NG][4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
   for (int k = 0; k < EB_NG; ++k) {
     const float v = wave_allsum(gf[k]);
     if (lane == 0) red[k][wv] = v;
@@ -1295,7 +1314,7 @@ eb_aux_bwd_kernel(tmae_eb_params p, const float* __restrict__ target, const floa
   EbCh w;
   eb_load(p, c, w);
   float d = 0.0f;
-  const float f = eb_fwd_bwd(w, p.quantiles[i], 1.0f, nullptr, &d);
+  const float f = eb_fwd_bwd<false>(w, p.quantiles[i], 1.0f, nullptr, &d);
   const float r = f - target[j];
   const float sg = r > 0.0f ? 1.0f : (r < 0.0f ? -1.0f : 0.0f);
   const float v = (gout ? gout[0] : 1.0f) * sg * d;
