@@ -668,10 +668,15 @@ def test_weight_cache_refresh_modes(dt):
         dg = W.packed([conv, convb], "conv_dg")
         for j, c in enumerate((conv, convb)):
             assert torch.equal(dg[j], c.detach().permute(1, 2, 3, 0).reshape(40, 9 * 72).to(dt))
-        for lo, n in ((8, 24), (0, 40), (16, 0)):
+        # (2, 16): source rows not 16-B aligned (the scalar path of mode 3)
+        for lo, n in ((8, 24), (0, 40), (16, 0), (2, 16)):
             pk = W.packed([conv, convb], ("lic", lo, n))
             for j, c in enumerate((conv, convb)):
                 assert torch.equal(pk[j], ops.pack_lic_stack_weight(c.detach()[:, lo:lo + n], dt)), (lo, n)
+        # the transposed, tap-flipped pack (mode 4): 72 -> 3 ragged k-steps, 40 -> 3 ragged fragments
+        pt = W.packed([conv, convb], "licT")
+        for j, c in enumerate((conv, convb)):
+            assert torch.equal(pt[j], ops.pack_lic_stack_weight_t(c.detach(), dt))
         lat = W.packed([conv, convb], ("conv_lat", 24))
         for j, c in enumerate((conv, convb)):
             assert torch.equal(lat[j], c.detach()[:, :24].permute(0, 2, 3, 1).reshape(72, 9 * 24).to(dt))

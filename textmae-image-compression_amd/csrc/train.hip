@@ -447,7 +447,8 @@ extern "C" int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0,
 //      source rows are 16-B aligned and R % 4 == 0 (scalar 4-B loads / 2-B stores ran at ~2 TB/s);
 //   2  per-row [A][B] -> [B][A] (conv weight [Cout][Cin][3][3] -> [Cout][3][3][Cin]: A = Cin = d3, B = 9): one row
 //      per chunk through LDS (A * B <= 8192); 16-B loads and 8-B bf16 stores when A % 4 == 0 and aligned;
-//   3  tmae_lic_stack's fragment order of a channel range of a conv weight (below);
+//   3  tmae_lic_stack's fragment order of a channel range of a conv weight (below; 256 units of 9 x 8 elements per
+//      chunk);
 //   4  the same for the transposed, tap-flipped weight (the fused stack backward's).
 template <typename OT>
 __device__ __forceinline__ void relayout_store(void* dst, size_t i, float v) { reinterpret_cast<OT*>(dst)[i] = to_out<OT>(v); }
@@ -545,44 +546,58 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
       }
     return;
   }
-  if (mode == 3) {
-    // a 3x3 conv weight [Cout = d1][Cin_tot = d2][3][3] (f32), input channels [d3, d3 + s0), into tmae_lic_stack's
-    // MFMA fragment order [tap][k-step][cout fragment][lane = 16 fq + fr][8]: element e of lane (fq, fr) in
-    // fragment f, k-step kc = W[16 f + fr][d3 + 32 kc + 8 fq + e][tap], zero past Cout / the channel range
-    // (ops.pack_lic_stack_weight's layout, built on the device so a training step re-packs without host work)
-    const unsigned cout = d1, cin_tot = d2, lo = d3, cn = (unsigned)s0;
-    const unsigned nfr = (cout + 15) / 16;
-    const unsigned nkc = (cn + 31) / 32;
-    const unsigned base3 = chunk * 32768u;
-    for (unsigned k = tid; k < 32768u; k += 256u) {
-      const unsigned i = base3 + k;
-      if (i >= total) break;
-      const unsigned e8 = i & 7u, lane = (i >> 3) & 63u, r = i >> 9;  // r = (tap * nkc + kc) * nfr + f
-      const unsigned f = r % nfr, tk = r / nfr, kc = tk % nkc, tap = tk / nkc;
-      const unsigned co = 16 * f + (lane & 15u), ci = 32 * kc + 8 * (lane >> 4) + e8;
-      const float v = (co < cout && ci < cn) ? src[((size_t)co * cin_tot + lo + ci) * 9 + tap] : 0.0f;
-      if (to_bf16) ((bf16*)e[1])[i] = (bf16)v;
-      else ((float*)e[1])[i] = v;
+  if (mode == 3 || mode == 4) {
+    // tmae_lic_stack's MFMA fragment order [tap][k-step][fragment][lane = 16 fq + fr][8] of a 3x3 conv weight.
+    //   3: weight [Cout = d1][Cin_tot = d2][3][3] (f32), input channels [d3, d3 + s0): element e of lane (fq, fr),
+    //      fragment f, k-step kc, tap t = W[16 f + fr][d3 + 32 kc + 8 fq + e][t] (ops.pack_lic_stack_weight);
+    //   4: the transposed, tap-flipped weight (the data gradient's: input = the forward's Cout = d1 channels, output =
+    //      its Cin = d2): W[32 kc + 8 fq + e][16 f + fr][8 - t] (ops.pack_lic_stack_weight_t).
+    // Zero past the channel ranges.  One thread = one (k-step, fragment, lane) unit, all 9 taps: its source values
+    // are 9 consecutive floats per element (the taps), read once; it writes one 16-B run per tap, a wave 1 KiB per
+    // tap.  (An element per thread read each source line once per tap through 4-B gathers: 1.1 TB/s.)
+    const unsigned nfr = mode == 3 ? (d1 + 15) / 16 : (d2 + 15) / 16;
+    const unsigned nkc = mode == 3 ? ((unsigned)s0 + 31) / 32 : (d1 + 31) / 32;
+    const unsigned units = nkc * nfr * 64u;
+    const unsigned u = chunk * 256u + (unsigned)tid;
+    if (u >= units) return;
+    const unsigned lane = u & 63u, fk = u >> 6, f = fk % nfr, kc = fk / nfr;
+    const unsigned fr = lane & 15u, fq = lane >> 4;
+    float v[9][8];
+    if (mode == 3) {
+      const unsigned cout = d1, cin_tot = d2, c_lo = d3, cn = (unsigned)s0;
+      const unsigned co = 16 * f + fr, ci0 = 32 * kc + 8 * fq;
+      const float* rowp = src + ((size_t)co * cin_tot + c_lo + ci0) * 9;
+      if (co < cout && ci0 + 8 <= cn && ((((unsigned long long)rowp) & 15) == 0)) {
+        f32x4 q[18];
+#pragma unroll
+        for (int k = 0; k < 18; ++k) q[k] = load4f(rowp + 4 * k);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int t = 0; t < 9; ++t) v[t][j] = q[(9 * j + t) >> 2][(9 * j + t) & 3];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int t = 0; t < 9; ++t) v[t][j] = (co < cout && ci0 + j < cn) ? rowp[9 * j + t] : 0.0f;
+      }
+    } else {
+      const unsigned cout = d1, cin = d2;
+      const unsigned ci = 16 * f + fr, co0 = 32 * kc + 8 * fq;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool ok = ci < cin && co0 + j < cout;
+        const float* tp = src + ((size_t)(co0 + j) * cin + ci) * 9;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) v[t][j] = ok ? tp[8 - t] : 0.0f;
+      }
     }
-    return;
-  }
-  if (mode == 4) {
-    // the transposed, tap-flipped conv weight (the data gradient's: input = the forward's Cout = d1 channels, output
-    // = its Cin = d2) in the same fragment order: element e of lane (fq, fr) in fragment f, k-step kc, tap t =
-    // W[32 kc + 8 fq + e][16 f + fr][8 - t] (ops.pack_lic_stack_weight_t)
-    const unsigned cout = d1, cin = d2;
-    const unsigned nfr = (cin + 15) / 16;
-    const unsigned nkc = (cout + 31) / 32;
-    const unsigned base4 = chunk * 32768u;
-    for (unsigned k = tid; k < 32768u; k += 256u) {
-      const unsigned i = base4 + k;
-      if (i >= total) break;
-      const unsigned e8 = i & 7u, lane = (i >> 3) & 63u, r = i >> 9;
-      const unsigned f = r % nfr, tk = r / nfr, kc = tk % nkc, tap = tk / nkc;
-      const unsigned ci = 16 * f + (lane & 15u), co = 32 * kc + 8 * (lane >> 4) + e8;
-      const float v = (co < cout && ci < cin) ? src[((size_t)co * cin + ci) * 9 + (8 - tap)] : 0.0f;
-      if (to_bf16) ((bf16*)e[1])[i] = (bf16)v;
-      else ((float*)e[1])[i] = v;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const size_t o = ((size_t)(t * nkc + kc) * nfr + f) * 512 + (size_t)lane * 8;
+      const f32x4 lo4 = f32x4{v[t][0], v[t][1], v[t][2], v[t][3]}, hi4 = f32x4{v[t][4], v[t][5], v[t][6], v[t][7]};
+      if (to_bf16) store8((bf16*)e[1] + o, lo4, hi4);
+      else store8((float*)e[1] + o, lo4, hi4);
     }
     return;
   }

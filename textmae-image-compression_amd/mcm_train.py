@@ -153,7 +153,7 @@ class _Weights:
                 rows.append([p.data_ptr(), dst.data_ptr(), ops.dtype_code(dst.dtype) | (4 << 8), co, ci, 0, 0, 0, 0, 0,
                              total, chunk])
                 ptrs.append((p.data_ptr(), dst.data_ptr()))
-                chunk += (total + 32767) // 32768
+                chunk += -(-(total // 72) // 256)  # 256 units of 9 taps x 8 elements per chunk
                 continue
             if job[0] == "lic":  # tmae_lic_stack fragment order (relayout mode 3)
                 _, co, ci, lo, n = job
@@ -161,7 +161,7 @@ class _Weights:
                 rows.append([p.data_ptr(), dst.data_ptr(), ops.dtype_code(dst.dtype) | (3 << 8), co, ci, lo, n, 0, 0, 0,
                              total, chunk])
                 ptrs.append((p.data_ptr(), dst.data_ptr()))
-                chunk += (total + 32767) // 32768
+                chunk += -(-(total // 72) // 256)
                 continue
             dims, strides = job
             d = list(dims) + [1] * (4 - len(dims))

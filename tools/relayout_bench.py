@@ -1,40 +1,83 @@
-"""Time the multi-tensor weight relayout (tmae_relayout_multi) per layout kind on synthetic ViT-B /
-LIC-shaped parameters: plain casts (nt), transposes (t, conv_dg) and conv rows (conv)."""
-import sys, os, json
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-import torch
-import textmae_amd  # noqa: F401
-from textmae_amd.mcm_train import _Weights
+"""Per-mode timing of the training step's weight re-layout (mcm_train._Weights.refresh -> tmae_relayout_multi) at
+the bench config (ViT-B MCM, batch 64, bf16): one eager step fills the cache, then each group of entries (all, and
+each relayout mode alone) is marked stale and re-laid out; GPU time from events around the launch (a sleep kernel
+ahead of it hides the host's table work), bytes = f32 source read + destination written.
+    python tools/relayout_bench.py"""
+import json
+import sys
 
-dev = "cuda"
-shapes_lin = [(2304, 768), (768, 768), (3072, 768), (768, 3072)] * 12 + [(1536, 512), (512, 512), (2048, 512), (512, 2048)] * 8
-shapes_conv = [(320, 320, 3, 3)] * 16 + [(224, 416, 3, 3)] * 12 + [(128, 224, 3, 3)] * 24 + [(32, 128, 3, 3)] * 24
-res = {}
-kinds = (("nt", shapes_lin), ("t", shapes_lin), ("conv", shapes_conv), ("conv_dg", shapes_conv))
-only = sys.argv[1:]  # e.g. "t": one kind per process, for a per-kind rocprofv3 kernel time
-for kind, shapes in kinds:
-    if only and kind not in only:
-        continue
-    W = _Weights(torch.bfloat16)
-    ps = [torch.nn.Parameter(torch.randn(s, device=dev)) for s in shapes]
-    for p in ps:
-        getattr(W, kind)(p)
-    n = sum(p.numel() for p in ps)
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ts = []
-    for it in range(12):
-        with torch.no_grad():
-            for p in ps:
-                p.add_(0.0)  # new version: every copy is stale
-        torch.cuda.synchronize()
-        ev[0].record()
-        W.refresh()
-        ev[1].record()
-        torch.cuda.synchronize()
-        if it >= 2:
-            ts.append(ev[0].elapsed_time(ev[1]) * 1e3)
-    ts.sort()
-    us = ts[len(ts) // 2]
-    res[kind] = {"params": n, "us": round(us, 1), "GB/s": round(n * 6 / us / 1e3, 1)}
-    print(kind, res[kind], flush=True)
-print(json.dumps(res))
+import torch
+
+sys.path.insert(0, ".")
+import bench  # noqa: E402
+import textmae_amd  # noqa: E402
+from textmae_amd import engine  # noqa: E402
+from textmae_amd.mcm_train import _Weights  # noqa: E402
+from textmae_amd.optim import configure_optimizers  # noqa: E402
+from textmae_amd.rd_loss import RateDistortionLoss  # noqa: E402
+
+
+def mode_of(job):
+    if job[0] == "licT":
+        return "m4_licT"
+    if job[0] == "lic":
+        return "m3_lic"
+    dims, strides = job
+    d = list(dims) + [1] * (4 - len(dims))
+    st = list(strides) + [0] * (4 - len(strides))
+    if _Weights._is_transpose(dims, strides):
+        return "m1_transpose"
+    if d[1] * d[2] * d[3] <= 8192 and st[2] == 1 and st[1] == d[2] and st[3] == d[1] * d[2] and st[0] == d[1] * d[2] * d[3]:
+        return "m2_rows"
+    return "m0_cast"
+
+
+def main():
+    torch.manual_seed(0)
+    m = textmae_amd.MCM(img_size=256, num_keep_patches=144).cuda().train()
+    m.compute_dtype = torch.bfloat16
+    m.distortion = "ssim+l1"
+    opt, aux = configure_optimizers(m, lr=1e-4, aux_lr=1e-4, fused=True)
+    crit = RateDistortionLoss(lmbda=1e-2)
+    imgs, scores = bench.synthetic_inputs(64, 256, 256, 2000, "cuda")
+    engine.train_step(m, crit, imgs, scores, opt, aux, clip_max_norm=1.0)
+    engine.train_step(m, crit, imgs, scores, opt, aux, clip_max_norm=1.0)
+    torch.cuda.synchronize()
+    W = m._train_exec.w
+    entries = [e for e in W.cache.values() if e[3] is not None]
+    groups = {"all": entries}
+    for e in entries:
+        groups.setdefault(mode_of(e[3]), []).append(e)
+    res = {}
+    for name, ents in groups.items():
+        nbytes = sum(e[1].numel() * e[1].element_size() for e in ents)
+        src = 0
+        for e in ents:  # f32 bytes the entry reads
+            job = e[3]
+            if job[0] == "lic":
+                src += 4 * 9 * job[1] * job[4]
+            elif job[0] == "licT":
+                src += 4 * 9 * job[1] * job[2]
+            else:
+                src += 4 * e[1].numel()
+        best = 1e9
+        for rep in range(6):
+            for e in ents:
+                e[0] = (0, 0)
+            torch.cuda.synchronize()
+            torch.cuda._sleep(50_000_000)
+            s, t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            W.refresh()
+            t.record()
+            t.synchronize()
+            if rep:
+                best = min(best, s.elapsed_time(t) * 1e3)
+        res[name] = {"entries": len(ents), "us": round(best, 1), "dst_MB": round(nbytes / 1e6, 1),
+                     "src_MB": round(src / 1e6, 1), "GB_s": round((nbytes + src) / best / 1e3, 1)}
+        print(name, res[name], flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
