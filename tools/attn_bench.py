@@ -1,5 +1,5 @@
 """Attention-core micro-benchmark at the bench shapes (batch 64): encoder T=145, 12 heads x 64;
-decoder T=257, 16 heads x 32.  Forward and backward;
+decoder T=257, 16 heads x 32 (or the shapes given as name=B,T,H,dh arguments).  Forward and backward;
 MFMA utilisation = algorithmic flops (4 B H T^2 dh fwd, 2.5x that bwd incl. recompute) / time / 2.5 PF."""
 import json
 import os
@@ -31,7 +31,10 @@ def ev(fn, reps=20):
 def main():
     out = {}
     dt = torch.bfloat16
-    for name, (B, T, H, dh) in {"enc": (64, 145, 12, 64), "dec": (64, 257, 16, 32)}.items():
+    shapes = {"enc": (64, 145, 12, 64), "dec": (64, 257, 16, 32)}
+    if len(sys.argv) > 1:  # name=B,T,H,dh ...
+        shapes = {a.split("=")[0]: tuple(int(v) for v in a.split("=")[1].split(",")) for a in sys.argv[1:]}
+    for name, (B, T, H, dh) in shapes.items():
         D = H * dh
         qkv = torch.randn(B * T, 3 * D, device="cuda").to(dt)
         o = torch.empty(B * T, D, device="cuda", dtype=dt)
