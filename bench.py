@@ -345,7 +345,7 @@ class LaunchTimer:
         return out
 
 
-def roofline_report(m, imgs, scores, batch, dump=None):
+def roofline_report(m, imgs, scores, batch, dump=None, profiled=True):
     lt = LaunchTimer(m, batch)
     with torch.no_grad():
         fam = lt.run(lambda: m(imgs, scores))
@@ -408,8 +408,12 @@ def roofline_report(m, imgs, scores, batch, dump=None):
                                                    / max(d["launches"], 1))
     # HBM counters (two rocprofv3 PMC passes, tools/pmc_family.py) and the graph-replayed forward's kernel trace
     # (tools/family_summary.py --forward), both committed under profiles/ from a run of this code
-    pmc, pmc_src = _committed("pmc_families.json")
-    trace, trace_src = _committed("trace_families.json")
+    # (committed for the default workload only: another model / batch gets no counter or trace figures)
+    pmc, pmc_src = _committed("pmc_families.json") if profiled else (None, None)
+    trace, trace_src = _committed("trace_families.json") if profiled else (None, None)
+    if not profiled:
+        roof["sources"] = None
+        roof["sources_note"] = "profiles/ hold PMC / trace families of the default workload only (config 2, batch 64)"
     fam_pmc = (pmc or {}).get("per_family", {})
     if dom in fam_pmc:
         roof["traffic"] = fam_pmc[dom]["hbm_bytes_per_launch"]
@@ -1014,7 +1018,8 @@ def main():
     roof = None
     if rank == 0 and not args.no_roofline:
         progress("roofline: per-family replays")
-        roof = roofline_report(model, imgs, scores, args.batch, dump=args.dump_launches)
+        roof = roofline_report(model, imgs, scores, args.batch, dump=args.dump_launches,
+                               profiled=vitb_default(args) and args.batch == 64 and args.img == 256)
 
     k64 = None
     if args.k64_line and vitb_default(args):
