@@ -108,8 +108,10 @@ def test_vitl_vs_oracle_and_split_api(tmae):
         pred2 = m.forward_decoder(lat, rest)
         check("maxrel:pred2", maxrel(pred2, pred), 1e-5)
         np.testing.assert_allclose(float(m.forward_loss(imgs.to(DEV), pred2, mask2)), float(loss), rtol=1e-5)
-    with pytest.raises(NotImplementedError, match="autograd"):
-        m.forward_encoder(imgs.to(DEV), 0.75)  # autograd trains through forward() only (test_gpu_mae_train.py)
+    # under autograd the parts run the training executor (test_gpu_mae_train.py checks their gradients)
+    lat3, mask3, _ = m.forward_encoder(imgs.to(DEV), 0.75, noise=noise.to(DEV))
+    assert lat3.requires_grad and torch.equal(mask3, mask)
+    check("maxrel:lat_autograd", maxrel(lat3.detach(), lat), 1e-5)
 
 
 def test_vitl_literal_config4_batch128_bf16_graph(tmae):

@@ -11,7 +11,7 @@ import pytest
 import torch
 from parity_log import check  # noqa: E402
 
-from oracle.mae_oracle import mae_forward
+from oracle.mae_oracle import mae_decoder, mae_encoder, mae_forward
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -106,6 +106,84 @@ def test_vitb_grads_f32_vs_oracle(tmae):
         if r > worst:
             worst, name_w = r, name
     check("maxrel:mae_train_vitb_grads", worst, 1e-3, note=name_w)
+
+
+@pytest.mark.parametrize("norm_pix", [False, True])
+def test_split_encoder_decoder_grads_f32_vs_oracle(tmae, norm_pix):
+    """forward_encoder -> forward_decoder -> forward_loss as separate module calls under autograd (models_mae.py
+    150-214, the reference's nn.Module behaviour): one autograd node per part, the HIP backward of each; every
+    gradient against autograd through the oracle's whole forward"""
+    m = tiny(tmae, norm_pix)
+    imgs = torch.randn(3, 3, 64, 64, generator=torch.Generator().manual_seed(40))
+    noise = torch.rand(3, 16, generator=torch.Generator().manual_seed(41))
+    rl, rp, rm, rg = oracle_grads(m, imgs, noise, 0.75, 16, 2, 1, 2, 2, norm_pix)
+    m.zero_grad(set_to_none=True)
+    lat, mask, rest = m.forward_encoder(imgs.to(DEV), 0.75, noise=noise.to(DEV))
+    pred = m.forward_decoder(lat, rest)
+    loss = m.forward_loss(imgs.to(DEV), pred, mask)
+    loss.backward()
+    assert torch.equal(mask.cpu(), rm)
+    check(f"maxrel:mae_split_pred_np{int(norm_pix)}", maxrel(pred.detach(), rp), 1e-3)
+    assert abs(float(loss.detach()) - float(rl)) <= 1e-3 * abs(float(rl))
+    worst = 0.0
+    for n, p_ in m.named_parameters():
+        if not p_.requires_grad:
+            assert p_.grad is None, n
+            continue
+        worst = max(worst, maxrel(p_.grad, rg[n]))
+    check(f"maxrel:mae_split_grads_np{int(norm_pix)}", worst, 1e-3)
+
+
+def test_encoder_alone_and_decoder_alone_vs_oracle(tmae):
+    """each part alone: forward_encoder under a random projection of the latent (only encoder parameters get
+    gradients), forward_decoder of a leaf latent (gradients to the latent and the decoder's parameters only), against
+    the oracle's encoder / decoder; a second forward of a part before its backward is refused"""
+    m = tiny(tmae, False)
+    imgs = torch.randn(2, 3, 64, 64, generator=torch.Generator().manual_seed(42))
+    noise = torch.rand(2, 16, generator=torch.Generator().manual_seed(43))
+    sd = {k: v.detach().cpu().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    enc_names = {n for n, _ in m.named_parameters() if n.startswith(("blocks.", "norm.", "patch_embed.", "cls_token"))}
+    # encoder alone
+    lat_o, mask_o, rest_o = mae_encoder(sd, imgs, noise, 0.75, 16, 2, 2)
+    R = torch.randn(lat_o.shape, generator=torch.Generator().manual_seed(44))
+    (lat_o * R).sum().backward()
+    m.zero_grad(set_to_none=True)
+    lat, mask, rest = m.forward_encoder(imgs.to(DEV), 0.75, noise=noise.to(DEV))
+    check("maxrel:mae_enc_alone_latent", maxrel(lat.detach(), lat_o.detach()), 1e-3)
+    assert torch.equal(rest.cpu(), rest_o)
+    (lat * R.to(DEV)).sum().backward()
+    worst = 0.0
+    for n, p_ in m.named_parameters():
+        if n in enc_names:
+            worst = max(worst, maxrel(p_.grad, sd[n].grad))
+        else:
+            assert p_.grad is None, n
+    check("maxrel:mae_enc_alone_grads", worst, 1e-3)
+    # decoder alone, on a leaf latent
+    for v in sd.values():
+        v.grad = None
+    x_o = torch.randn(lat_o.shape, generator=torch.Generator().manual_seed(45)).requires_grad_(True)
+    pred_o = mae_decoder(sd, x_o, rest_o, 1, 2)
+    R2 = torch.randn(pred_o.shape, generator=torch.Generator().manual_seed(46))
+    (pred_o * R2).sum().backward()
+    m.zero_grad(set_to_none=True)
+    x = x_o.detach().to(DEV).requires_grad_(True)
+    pred = m.forward_decoder(x, rest_o.to(DEV))
+    check("maxrel:mae_dec_alone_pred", maxrel(pred.detach(), pred_o.detach()), 1e-3)
+    (pred * R2.to(DEV)).sum().backward()
+    check("maxrel:mae_dec_alone_dx", maxrel(x.grad, x_o.grad), 1e-3)
+    worst = 0.0
+    for n, p_ in m.named_parameters():
+        if n in enc_names or not p_.requires_grad:
+            assert p_.grad is None, n
+        else:
+            worst = max(worst, maxrel(p_.grad, sd[n].grad))
+    check("maxrel:mae_dec_alone_grads", worst, 1e-3)
+    # stale activations
+    lat1, _, _ = m.forward_encoder(imgs.to(DEV), 0.75, noise=noise.to(DEV))
+    m.forward_encoder(imgs.to(DEV), 0.75, noise=noise.to(DEV))
+    with pytest.raises(RuntimeError, match="forward_encoder ran again"):
+        lat1.sum().backward()
 
 
 def test_bf16_bounded_and_adam_steps(tmae):

@@ -102,12 +102,9 @@ class MaskedAutoencoderViT(nn.Module):
         return x.reshape(x.shape[0], 3, h * p, h * p)
 
     # ---------------------------------------------------------------------------------- execution
-    def _check(self, imgs, whole=False):
+    def _check(self, imgs):
         if not imgs.is_cuda:
             raise ValueError("MaskedAutoencoderViT runs on the MI355X kernels: move the model and inputs to the GPU")
-        if not whole and self._training_call():
-            raise NotImplementedError("autograd through forward_encoder / forward_decoder alone is not available in "
-                                      "this build: train through forward() (mae_train.py), or run under torch.no_grad()")
 
     def _training_call(self):
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
@@ -145,8 +142,14 @@ class MaskedAutoencoderViT(nn.Module):
         return x_masked, mask, rest
 
     def forward_encoder(self, x, mask_ratio, noise=None):
-        """models_mae.py:150-170 -> (latent f32 [N, 1 + len_keep, E], mask, ids_restore)"""
+        """models_mae.py:150-170 -> (latent f32 [N, 1 + len_keep, E], mask, ids_restore); under autograd the
+        training executor's encoder part (mae_train.py, HIP backward of the encoder)"""
         self._check(x)
+        if self._training_call():
+            self._check_supported()
+            from .mae_train import train_forward_encoder
+
+            return train_forward_encoder(self, x, mask_ratio, noise)
         with torch.no_grad():
             keep = self._len_keep(mask_ratio)
             ex = self._executor(x.shape[0], keep, x.device)
@@ -154,8 +157,14 @@ class MaskedAutoencoderViT(nn.Module):
             return ex.latent_f32().view(x.shape[0], keep + 1, -1), mask, rest
 
     def forward_decoder(self, x, ids_restore):
-        """models_mae.py:172-196 -> pred f32 [N, L, p*p*C]"""
+        """models_mae.py:172-196 -> pred f32 [N, L, p*p*C]; under autograd (decoder parameters or x requiring
+        gradients) the training executor's decoder part"""
         self._check(x)
+        if self._training_call() or (torch.is_grad_enabled() and x.requires_grad):
+            self._check_supported()
+            from .mae_train import train_forward_decoder
+
+            return train_forward_decoder(self, x, ids_restore)
         with torch.no_grad():
             n, t, _ = x.shape
             ex = self._executor(n, t - 1, x.device)
@@ -175,7 +184,7 @@ class MaskedAutoencoderViT(nn.Module):
     def forward(self, imgs, mask_ratio=0.75, noise=None):
         """models_mae.py:216-220 -> (loss, pred [N, L, p*p*3], mask [N, L]); under autograd the training path
         (mae_train.py: HIP backward of the whole model)"""
-        self._check(imgs, whole=True)
+        self._check(imgs)
         if self._training_call():
             self._check_supported()
             from .mae_train import train_forward

@@ -43,6 +43,7 @@ class MAETrainExec(_VitTrainBase):
             # the bf16 GEMMs take in 16-B rows only; the f32 path (4-value rows) trains patch 14
             raise ValueError(f"MAE training with {self.KP}-value patch rows runs in compute_dtype=torch.float32 only")
         self._wpe_pad = self._gpe_pad = None
+        self.enc_gen = self.dec_gen = 0  # forward counters: a split backward refuses activations a later forward replaced
         self._layout()
 
     def _grad_order(self):
@@ -63,9 +64,18 @@ class MAETrainExec(_VitTrainBase):
     # ------------------------------------------------------------------ forward
     def forward(self, imgs, noise):
         """-> (loss 0-d f32, pred f32 [B*L, p*p*c], mask [B, L])"""
+        lat, mask = self.forward_enc(imgs, noise)
+        pred = self.forward_dec(lat)
+        loss = ops.mae_loss(pred, self.imgs, self.rest, self.keep, self.P, self.m.norm_pix_loss)
+        return loss, pred, mask
+
+    def forward_enc(self, imgs, noise):
+        """forward_encoder (models_mae.py:150-170): -> (latent [B*Te, E] in the compute dtype, mask [B, L]); keeps
+        the encoder's activations and the shuffle for the backward"""
         m, dt, B, keep, W = self.m, self.dtype, self.batch, self.keep, self.w
-        E, Dd = m.pos_embed.shape[-1], m.decoder_pos_embed.shape[-1]
-        L, P, Te = self.L, self.P, keep + 1
+        E = m.pos_embed.shape[-1]
+        P, Te = self.P, keep + 1
+        self.enc_gen += 1
         imgs = imgs.float().contiguous()
         if imgs.shape[2:] != tuple(m.patch_embed.img_size):
             raise ValueError(f"Input image size {tuple(imgs.shape[2:])} doesn't match model {m.patch_embed.img_size}")
@@ -91,8 +101,18 @@ class MAETrainExec(_VitTrainBase):
         for blk in m.blocks:
             tok = self._block_fwd(blk, tok, B, Te)
         self.tok_last = tok
-        self.lat = ops.layernorm(tok, m.norm.weight, m.norm.bias, m.norm.eps, dt)
-        # decoder (172-196): embed every latent row, mask tokens, unshuffle, pos; blocks; norm; pred
+        return ops.layernorm(tok, m.norm.weight, m.norm.bias, m.norm.eps, dt), mask
+
+    def forward_dec(self, lat):
+        """forward_decoder (models_mae.py:172-196) of lat [B*Te, E] (compute dtype) under self.shuf: embed every
+        latent row, mask tokens, unshuffle, pos; blocks; norm; pred -> pred f32 [B*L, p*p*c]"""
+        m, dt, B, keep, W = self.m, self.dtype, self.batch, self.keep, self.w
+        Dd = m.decoder_pos_embed.shape[-1]
+        L, Te = self.L, keep + 1
+        self.dec_gen += 1
+        self.w.refresh()  # (a no-op after forward_enc's)
+        self.lat = lat
+        shuf = self.shuf
         dpos = m.decoder_pos_embed.detach()
         dec = torch.empty((B * (L + 1), Dd), dtype=torch.float32, device=self.device)
         ops.decoder_embed(self.lat, W.nt(m.decoder_embed.weight), m.decoder_embed.bias.detach(), dpos, shuf, dec, B,
@@ -106,25 +126,35 @@ class MAETrainExec(_VitTrainBase):
                                 row_group=L, group_stride=L + 1, row_offset=1)
         self.pred = ops.linear(self.dn, W.nt(m.decoder_pred.weight), m.decoder_pred.bias.detach(), dt,
                                out_dtype=torch.float32)
-        loss = ops.mae_loss(self.pred, imgs, rest, keep, P, m.norm_pix_loss)
-        return loss, self.pred, mask
+        return self.pred
 
     # ------------------------------------------------------------------ backward
     def backward(self, dloss, dpred, gflat, sync=None):
-        m, dt, W, B, keep = self.m, self.dtype, self.w, self.batch, self.keep
-        E, Dd = m.pos_embed.shape[-1], m.decoder_pos_embed.shape[-1]
-        L, P, Te = self.L, self.P, keep + 1
+        self.bwd_begin(gflat, sync)
+        m, B, L = self.m, self.batch, self.L
+        # ---- forward_loss (models_mae.py:198-214)
+        dl = dloss.float().contiguous().reshape(1) if dloss is not None else None
+        dp_in = dpred.float().contiguous() if dpred is not None else None
+        dP = T.mae_loss_bwd(self.pred, self.imgs, self.rest, self.keep, self.P, m.norm_pix_loss, dl, dp_in,
+                            self._e(B * L, self.pred.shape[1]), self.dtype)
+        self.enc_bwd(self.dec_bwd(dP))
+        self._side_join()
+
+    def bwd_begin(self, gflat, sync=None):
         self.gflat, self.sync = gflat, sync
         if sync is not None:
             sync.attach(gflat)
         self._side_begin()
+
+    def dec_bwd(self, dP):
+        """decoder backward from dP [B*L, p*p*c] (compute dtype): every decoder parameter's gradient; -> the
+        gradient of the decoder's input latent, f32 [B*Te, E]"""
+        m, dt, W, B, keep = self.m, self.dtype, self.w, self.batch, self.keep
+        E, Dd = m.pos_embed.shape[-1], m.decoder_pos_embed.shape[-1]
+        L, Te = self.L, keep + 1
         G = self.grad
         npred = self.pred.shape[1]
-        # ---- forward_loss + decoder_pred (models_mae.py:193, 198-214)
-        dl = dloss.float().contiguous().reshape(1) if dloss is not None else None
-        dp_in = dpred.float().contiguous() if dpred is not None else None
-        dP = T.mae_loss_bwd(self.pred, self.imgs, self.rest, keep, P, m.norm_pix_loss, dl, dp_in,
-                            self._e(B * L, npred), dt)
+        # ---- decoder_pred (models_mae.py:193)
         self._wg(dP, self.dn, npred, Dd, B * L, G(m.decoder_pred.weight), dt, bias=G(m.decoder_pred.bias))
         ddn = torch.empty((B * L, Dd), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dP, W.t(m.decoder_pred.weight), B * L, npred, Dd, dt, out=ddn)
@@ -145,6 +175,13 @@ class MAETrainExec(_VitTrainBase):
         dlat = torch.empty((B * Te, E), dtype=torch.float32, device=self.device)
         T.dgrad_linear(dtok, W.t(m.decoder_embed.weight), B * Te, Dd, E, dt, out=dlat)
         self._ready(m.mask_token)
+        return dlat
+
+    def enc_bwd(self, dlat):
+        """encoder backward from the latent's gradient dlat f32 [B*Te, E]: every encoder parameter's gradient"""
+        m, dt, B, keep = self.m, self.dtype, self.batch, self.keep
+        E, Te = m.pos_embed.shape[-1], keep + 1
+        G = self.grad
         # ---- encoder norm (every row, cls included) + blocks
         dt_tok = self._z(B * Te, E)
         dt_op = dt_tok if dt == torch.float32 else self._z(B * Te, E, dtype=dt)
@@ -167,7 +204,6 @@ class MAETrainExec(_VitTrainBase):
         T.colsum(dt_tok, B * keep, E, G(m.patch_embed.proj.bias), row_group=keep, group_stride=Te, row_offset=1)
         T.colsum(dt_tok, B, E, G(m.cls_token).view(-1), row_group=1, group_stride=Te, row_offset=0)
         self._ready(m.cls_token)
-        self._side_join()
 
 
 class _MAETrainFn(torch.autograd.Function):
@@ -212,3 +248,101 @@ def train_forward(m, imgs, mask_ratio, noise):
     params = [p for p in m.parameters()]
     loss, pred, mask = _MAETrainFn.apply(ex, noise.to(imgs.device).float().contiguous(), imgs, *params)
     return loss, pred.view(B, ex.L, -1), mask
+
+
+# ---------------------------------------------------------------------- forward_encoder / forward_decoder alone
+# (models_mae.py:150-196 as separate nn.Module calls under autograd: each is its own node over its own parameters;
+# the executor keeps one set of activations per part, so a part's backward must come before that part's next
+# forward -- checked by the executor's forward counters)
+def _enc_params(m):
+    out = [m.norm.weight, m.norm.bias]
+    for blk in m.blocks:
+        out += _block_params(blk)
+    return out + [m.patch_embed.proj.weight, m.patch_embed.proj.bias, m.cls_token]
+
+
+def _dec_params(m):
+    out = [m.decoder_pred.weight, m.decoder_pred.bias, m.decoder_norm.weight, m.decoder_norm.bias,
+           m.decoder_embed.weight, m.decoder_embed.bias, m.mask_token]
+    for blk in m.decoder_blocks:
+        out += _block_params(blk)
+    return out
+
+
+def _param_grads(ex, params, gflat):
+    return [gflat[ex.offsets[id(p)]:ex.offsets[id(p)] + p.numel()].view(p.shape) if p.requires_grad else None
+            for p in params]
+
+
+class _MAEEncFn(torch.autograd.Function):
+    """forward_encoder: (imgs, *encoder params) -> (latent f32 [B, Te, E], mask, ids_restore)"""
+
+    @staticmethod
+    def forward(ctx, ex, noise, imgs, *params):
+        lat, mask = ex.forward_enc(imgs, noise)
+        ctx.ex, ctx.params, ctx.gen = ex, params, ex.enc_gen
+        ctx.mark_non_differentiable(mask, ex.rest)
+        return lat.float().view(ex.batch, ex.keep + 1, -1), mask, ex.rest
+
+    @staticmethod
+    def backward(ctx, dlat, dmask, drest):
+        ex, params = ctx.ex, ctx.params
+        if ex.enc_gen != ctx.gen:
+            raise RuntimeError("forward_encoder ran again on this model before this backward: its saved activations "
+                               "are gone (backward each forward_encoder before the next)")
+        gflat = ex.grads_buffer(any(p.grad is not None for p in params if p.requires_grad))
+        ex.bwd_begin(gflat)
+        ex.enc_bwd(dlat.float().contiguous().view(ex.batch * (ex.keep + 1), -1))
+        ex._side_join()
+        return (None, None, None, *_param_grads(ex, params, gflat))
+
+
+class _MAEDecFn(torch.autograd.Function):
+    """forward_decoder: (latent [B, Te, E], *decoder params) -> pred f32 [B, L, p*p*c] (ids_restore fixed)"""
+
+    @staticmethod
+    def forward(ctx, ex, ids_restore, x, *params):
+        ex.rest = ids_restore
+        ex.shuf = ops.invert_permutation(ids_restore)
+        lat = x.reshape(ex.batch * (ex.keep + 1), -1).to(ex.dtype).contiguous()
+        pred = ex.forward_dec(lat)
+        ctx.ex, ctx.params, ctx.gen, ctx.xshape = ex, params, ex.dec_gen, x.shape
+        return pred.view(ex.batch, ex.L, -1)
+
+    @staticmethod
+    def backward(ctx, dpred):
+        ex, params = ctx.ex, ctx.params
+        if ex.dec_gen != ctx.gen:
+            raise RuntimeError("forward_decoder ran again on this model before this backward: its saved activations "
+                               "are gone (backward each forward_decoder before the next)")
+        gflat = ex.grads_buffer(any(p.grad is not None for p in params if p.requires_grad))
+        ex.bwd_begin(gflat)
+        dP = ex._e(ex.batch * ex.L, ex.pred.shape[1])
+        dP.copy_(dpred.reshape(dP.shape))
+        dlat = ex.dec_bwd(dP)
+        ex._side_join()
+        return (None, None, dlat.view(ctx.xshape), *_param_grads(ex, params, gflat))
+
+
+def _exec_for(m, B, keep, device):
+    ex = getattr(m, "_train_exec", None)
+    if ex is None or (ex.batch, ex.keep, ex.dtype, ex.device) != (B, keep, m.compute_dtype, device):
+        ex = m._train_exec = MAETrainExec(m, B, keep, m.compute_dtype, device)
+    return ex
+
+
+def train_forward_encoder(m, imgs, mask_ratio, noise):
+    """MaskedAutoencoderViT.forward_encoder with autograd: (latent f32 [N, 1 + len_keep, E], mask, ids_restore)"""
+    imgs = imgs.float().contiguous()
+    ex = _exec_for(m, imgs.shape[0], m._len_keep(mask_ratio), imgs.device)
+    if noise is None:
+        noise = torch.rand(imgs.shape[0], ex.L, device=imgs.device)
+    return _MAEEncFn.apply(ex, noise.to(imgs.device).float().contiguous(), imgs, *_enc_params(m))
+
+
+def train_forward_decoder(m, x, ids_restore):
+    """MaskedAutoencoderViT.forward_decoder with autograd: pred f32 [N, L, p*p*c] (gradients to x and the
+    decoder's parameters)"""
+    n, t, _ = x.shape
+    ex = _exec_for(m, n, t - 1, x.device)
+    return _MAEDecFn.apply(ex, ids_restore.to(x.device).to(torch.int64).contiguous(), x, *_dec_params(m))
