@@ -186,22 +186,24 @@ def test_encoder_alone_and_decoder_alone_vs_oracle(tmae):
         lat1.sum().backward()
 
 
-def test_bf16_bounded_and_adam_steps(tmae):
+@pytest.mark.parametrize("patch", [16, 14])
+def test_bf16_bounded_and_adam_steps(tmae, patch):
     """bf16 operands: gradients within a relative L2 bound of the f32 oracle; then FusedAdam steps on one batch
-    drive the loss down (the training loop a user of the reference runs)"""
+    drive the loss down (the training loop a user of the reference runs).  Patch 14: decoder_pred's 588 outputs
+    run its weight / data gradients on zero-tailed 592-column copies"""
     from textmae_amd.optim import FusedAdam
 
-    m = tiny(tmae, True, dec_dim=64)
+    m = tiny(tmae, True, dec_dim=64, patch=patch)
     m.compute_dtype = torch.bfloat16
-    imgs = torch.randn(8, 3, 64, 64, generator=torch.Generator().manual_seed(27))
+    imgs = torch.randn(8, 3, 4 * patch, 4 * patch, generator=torch.Generator().manual_seed(27))
     noise = torch.rand(8, 16, generator=torch.Generator().manual_seed(28))
-    rl, rp, rm, rg = oracle_grads(m, imgs, noise, 0.75, 16, 2, 1, 2, 2, True)
+    rl, rp, rm, rg = oracle_grads(m, imgs, noise, 0.75, patch, 2, 1, 2, 2, True)
     loss, pred, mask, grads = run_train(m, imgs, noise, 0.75)
     worst = 0.0
     for name, g in grads.items():
         ref = rg[name].double()
         worst = max(worst, float((g.double().cpu() - ref).norm() / ref.norm().clamp_min(1e-30)))
-    check("relL2:mae_train_bf16_grads", worst, 2e-2)  # measured 9.2e-3
+    check("relL2:mae_train_bf16_grads" + ("" if patch == 16 else f"_p{patch}"), worst, 2e-2)  # measured 9.2e-3
     opt = FusedAdam([p for p in m.parameters() if p.requires_grad], lr=1e-3)
     first = None
     for _ in range(8):

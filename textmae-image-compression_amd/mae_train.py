@@ -38,11 +38,10 @@ class MAETrainExec(_VitTrainBase):
         # gradient of which the first KP columns are the parameter's
         self.KP = C * self.P * self.P
         self.Kw = -(-self.KP // 8) * 8
-        if self.KP != self.Kw and dtype != torch.float32:
-            # decoder_pred's 588 outputs are the K of its data gradient and the rows of its weight gradient, which
-            # the bf16 GEMMs take in 16-B rows only; the f32 path (4-value rows) trains patch 14
-            raise ValueError(f"MAE training with {self.KP}-value patch rows runs in compute_dtype=torch.float32 only")
+        # decoder_pred's KP outputs are the K of its data gradient and the rows of its weight gradient: in bf16
+        # (16-B GEMM rows) a KP that is not a multiple of 8 runs on zero-tailed Kw-wide copies (dec_bwd)
         self._wpe_pad = self._gpe_pad = None
+        self._dp_pad = None
         self.enc_gen = self.dec_gen = 0  # forward counters: a split backward refuses activations a later forward replaced
         self._layout()
 
@@ -155,9 +154,26 @@ class MAETrainExec(_VitTrainBase):
         G = self.grad
         npred = self.pred.shape[1]
         # ---- decoder_pred (models_mae.py:193)
-        self._wg(dP, self.dn, npred, Dd, B * L, G(m.decoder_pred.weight), dt, bias=G(m.decoder_pred.bias))
         ddn = torch.empty((B * L, Dd), dtype=torch.float32, device=self.device)
-        T.dgrad_linear(dP, W.t(m.decoder_pred.weight), B * L, npred, Dd, dt, out=ddn)
+        if npred % 8 and dt != torch.float32:
+            # bf16, patch 14 (588 outputs): the gradient and W^T zero-tailed to 592 columns (the tails stay zero), the
+            # weight gradient [592][Dd] into a scratch whose first 588 rows are the parameter's
+            npad = -(-npred // 8) * 8
+            if self._dp_pad is None:
+                self._dp_pad = self._z(B * L, npad, dtype=dt)
+                self._wt_pad = self._z(Dd, npad, dtype=dt)
+                self._gdp_pad = torch.empty((npad, Dd), dtype=torch.float32, device=self.device)
+                self._gdb_pad = torch.empty(npad, dtype=torch.float32, device=self.device)
+            self._dp_pad[:, :npred].copy_(dP)
+            self._wt_pad[:, :npred].copy_(W.t(m.decoder_pred.weight))
+            T.wgrad(self._dp_pad, self.dn, npad, Dd, B * L, self._gdp_pad, dt, bias=self._gdb_pad,
+                    slot_div=_SIDE_SLOT_DIV)
+            G(m.decoder_pred.weight).copy_(self._gdp_pad[:npred])
+            G(m.decoder_pred.bias).copy_(self._gdb_pad[:npred])
+            T.dgrad_linear(self._dp_pad, self._wt_pad, B * L, npad, Dd, dt, out=ddn)
+        else:
+            self._wg(dP, self.dn, npred, Dd, B * L, G(m.decoder_pred.weight), dt, bias=G(m.decoder_pred.bias))
+            T.dgrad_linear(dP, W.t(m.decoder_pred.weight), B * L, npred, Dd, dt, out=ddn)
         # ---- decoder_norm (the cls row gets no gradient: pred drops it) + blocks
         ddec = self._z(B * (L + 1), Dd)
         ddec_op = ddec if dt == torch.float32 else self._z(B * (L + 1), Dd, dtype=dt)
