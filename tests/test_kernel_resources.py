@@ -11,7 +11,8 @@ import kernel_resources as kr  # noqa: E402
 
 # mangled-name substrings allowed to keep scratch, and why
 ALLOWED = {
-    "mha_fwd_kernelIDF16bLi80E": "head dim 80 (ViT-H) bf16 attention forward, 3 VGPRs at the 1024-thread bound",
+    "mha_fwd_kernelIDF16bLi80ELi1024E": "head dim 80 (ViT-H) bf16 attention forward past 8 waves (T > 256): 3 VGPRs "
+                                        "at the 1024-thread bound; up to 8 waves the 512 instance runs",
     "mha_bwd1_bf16_kernelILi32ELi1024E": "dh 32 backward up to 8 / from 11 waves (MAE decoder: two workgroups per CU "
                                          "at 128 VGPRs); the MCM decoder's 9-wave launch takes the 640 instance",
     "mha_bwd_f32_kernel": "f32 parity path",

@@ -18,8 +18,9 @@ template <typename T> struct AttnCfg;
 template <> struct AttnCfg<bf16> { static constexpr int KPAD = 8, VPAD = 4, EPC = 8; };
 template <> struct AttnCfg<float> { static constexpr int KPAD = 4, VPAD = 1, EPC = 4; };
 
-template <typename T, int DH>
-__global__ void __launch_bounds__(1024)
+// MAXT: the launch bound (the dh-80 / ViT-H case also has a 512-thread instance: at 1024 it spilled 3 VGPRs)
+template <typename T, int DH, int MAXT = 1024>
+__global__ void __launch_bounds__(MAXT)
 mha_fwd_kernel(const T* __restrict__ qkv, T* __restrict__ out, float* __restrict__ lse, int Tn, int H, int Tpad,
                float scale_log2e) {
   constexpr int KPAD = AttnCfg<T>::KPAD, VPAD = AttnCfg<T>::VPAD, EPC = AttnCfg<T>::EPC;
@@ -255,6 +256,11 @@ static int mha_launch(const void* qkv, void* out, int B, int Tn, int H, float sc
       TMAE_LAUNCH_CHECK("tmae_mha_fwd");
     }
   }
+  constexpr int M80 = (DH == 80 && sizeof(T) == 2) ? 512 : 1024;  // the 512-bound instance: bf16 dh 80 only
+  if (M80 == 512 && nthr <= 512)
+    hipLaunchKernelGGL((mha_fwd_kernel<T, DH, M80>), dim3(B * H), dim3(nthr), lds, st, (const T*)qkv, (T*)out, lse, Tn,
+                       H, Tpad, scale * 1.4426950408889634f);
+  else
     hipLaunchKernelGGL((mha_fwd_kernel<T, DH>), dim3(B * H), dim3(nthr), lds, st, (const T*)qkv, (T*)out, lse, Tn, H,
                        Tpad, scale * 1.4426950408889634f);
   TMAE_LAUNCH_CHECK("tmae_mha_fwd");
