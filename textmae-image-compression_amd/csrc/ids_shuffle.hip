@@ -74,25 +74,33 @@ __device__ float torch_cascade_sum(const float* x, int n, int W, float* acc) {
   return fin;
 }
 
-// exclusive scan of `n` ints in LDS (n <= IDS_MAXL), returns total.  All threads call.
-__device__ int block_exclusive_scan(int* a, int n, int* tmp /*IDS_THREADS*/) {
-  const int t = threadIdx.x;
+// exclusive scan of `n` ints in LDS (n <= IDS_MAXL), returns total.  All threads call.  Each thread sums its chunk,
+// the chunk sums are scanned inside each wave by lane shuffles and across the waves through tmp (two barriers;
+// a Hillis-Steele scan over the workgroup took 16).  Integer sums: the same result in any order.
+__device__ int block_exclusive_scan(int* a, int n, int* tmp /*IDS_THREADS / 64*/) {
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  constexpr int NWV = IDS_THREADS / 64;
   const int per = (n + IDS_THREADS - 1) / IDS_THREADS;
   const int beg = min(n, t * per), end = min(n, beg + per);
   int s = 0;
   for (int i = beg; i < end; ++i) s += a[i];
-  tmp[t] = s;
-  __syncthreads();
-  for (int off = 1; off < IDS_THREADS; off <<= 1) {
-    int v = (t >= off) ? tmp[t - off] : 0;
-    __syncthreads();
-    tmp[t] += v;
-    __syncthreads();
+  int x = s;  // inclusive scan of the chunk sums within the wave
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
   }
-  int run = tmp[t] - s;  // exclusive prefix of this thread's chunk
-  const int total = tmp[IDS_THREADS - 1];
+  if (lane == 63) tmp[wave] = x;
+  __syncthreads();
+  int run = x - s, total = 0;
+#pragma unroll
+  for (int w = 0; w < NWV; ++w) {
+    const int tw = tmp[w];
+    run += w < wave ? tw : 0;
+    total += tw;
+  }
   for (int i = beg; i < end; ++i) {
-    int v = a[i];
+    const int v = a[i];
     a[i] = run;
     run += v;
   }
@@ -116,7 +124,9 @@ ids_shuffle_kernel(const float* __restrict__ scores, int64_t* __restrict__ ids_s
   __shared__ float gacc[IDS_GROUPS][4 * 4 * 16];
   __shared__ int scan_tmp[IDS_THREADS];
   __shared__ int gcnt[IDS_GROUPS], goff[IDS_GROUPS], gbeg[IDS_GROUPS];
+  __shared__ int wcnt[IDS_THREADS / 64][IDS_GROUPS];  // per wave: indices of each group (the compaction's ranks)
   __shared__ float gmean[IDS_GROUPS];
+  __shared__ float e9[9];
   __shared__ float thr[9];
   __shared__ int keep[9];
   __shared__ int nuniq, cnt9, nsel_other;
@@ -139,7 +149,8 @@ ids_shuffle_kernel(const float* __restrict__ scores, int64_t* __restrict__ ids_s
   __syncthreads();
 
   // 2. bitonic sort ascending by (value, index)
-  lds_bitonic_sort<IDS_THREADS>(key, P);
+  if (P <= IDS_THREADS) reg_bitonic_sort<IDS_THREADS>(key, P);
+  else lds_bitonic_sort<IDS_THREADS>(key, P);
 
   // 3. runs of equal values (float equality)
   for (int p = t; p < L; p += IDS_THREADS) {
@@ -188,10 +199,29 @@ ids_shuffle_kernel(const float* __restrict__ scores, int64_t* __restrict__ ids_s
   }
   __syncthreads();
   // compact scores by (group, index): rank within group = #earlier indices of the same group
-  for (int i = t; i < L; i += IDS_THREADS) {
-    int c = cat_idx[i], r = 0;
-    for (int j = 0; j < i; ++j) r += (cat_idx[j] == c);
-    glist[goff[c] + r] = sv[i];
+  if (L <= IDS_THREADS) {
+    // one index per thread: per-group ballots give the rank inside the wave, per-wave counts the waves before
+    const int lane = t & 63, wave = t >> 6;
+    const int c = t < L ? cat_idx[t] : -1;
+    unsigned long long mine = 0;
+#pragma unroll
+    for (int g = 0; g < IDS_GROUPS; ++g) {
+      const unsigned long long bm = __ballot(c == g);
+      if (lane == 0) wcnt[wave][g] = __popcll(bm);
+      if (c == g) mine = bm;
+    }
+    __syncthreads();
+    if (c >= 0) {
+      int r = __popcll(mine & ((1ull << lane) - 1ull));
+      for (int w = 0; w < wave; ++w) r += wcnt[w][c];
+      glist[goff[c] + r] = sv[t];
+    }
+  } else {
+    for (int i = t; i < L; i += IDS_THREADS) {
+      int c = cat_idx[i], r = 0;
+      for (int j = 0; j < i; ++j) r += (cat_idx[j] == c);
+      glist[goff[c] + r] = sv[i];
+    }
   }
   __syncthreads();
 
@@ -202,17 +232,23 @@ ids_shuffle_kernel(const float* __restrict__ scores, int64_t* __restrict__ ids_s
   }
   __syncthreads();
 
-  // 7. softmax over groups 0..8, scaled targets (MCM.py:399-402), slice lengths (MCM.py:405-408)
+  // 7. softmax over groups 0..8, scaled targets (MCM.py:399-402), slice lengths (MCM.py:405-408); the nine
+  //    exponentials (rounded from double) in parallel, everything order-dependent on one thread
+  if (t < 9) {
+    float m = gmean[0];
+    for (int g = 0; g < 9; ++g) m = fmaxf(m, gmean[g]);
+    e9[t] = (float)exp((double)(gmean[t] - m));
+  }
+  __syncthreads();
   if (t == 0) {
     int c9 = gcnt[9];
     cnt9 = c9;
     int new_target = K - c9;
-    float m = gmean[0];
     bool has_nan = false;
-    for (int g = 0; g < 9; ++g) { has_nan |= isnan(gmean[g]); m = fmaxf(m, gmean[g]); }
+    for (int g = 0; g < 9; ++g) has_nan |= isnan(gmean[g]);
     float e[9];
     float sum = 0.0f;
-    for (int g = 0; g < 9; ++g) { e[g] = (float)exp((double)(gmean[g] - m)); sum = sum + e[g]; }
+    for (int g = 0; g < 9; ++g) { e[g] = e9[g]; sum = sum + e[g]; }
     float rs = 1.0f / sum;
     int beg = 0;
     for (int g = 0; g < 9; ++g) {
