@@ -481,8 +481,10 @@ int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0, int d1, in
  * total, first_chunk} (int64, device memory), first_chunk = the chunks of the tensors before t (mode 0, a plain
  * or strided copy: ceil(total / 32768); mode 1, a 2-D transpose: 64 x 64 tiles; mode 2, a per-row transpose:
  * rows; mode 3, a 3x3 conv weight [d1 = Cout][d2 = Cin][3][3] restricted to input channels [d3, d3 + s0) into
- * tmae_lic_stack's fragment order, total = 9 * ceil(s0 / 32) * ceil(Cout / 16) * 512: ceil(total / 32768)),
- * then nchunks more int64: the row t of every chunk (ntensors * 12 + nchunks values in all) */
+ * tmae_lic_stack's fragment order, total = 9 * ceil(s0 / 32) * ceil(Cout / 16) * 512; mode 4, the transposed,
+ * tap-flipped weight of [d1 = Cout][d2 = Cin][3][3] (input Cout, output Cin) in the same order, total = 9 *
+ * ceil(Cout / 32) * ceil(Cin / 16) * 512; modes 3 and 4: ceil(total / 72 / 256) chunks, 256 units of 9 taps x 8
+ * elements each), then nchunks more int64: the row t of every chunk (ntensors * 12 + nchunks values in all) */
 int tmae_relayout_multi(const long long* table, int ntensors, long long nchunks, void* stream);
 
 /* bias gradient: out[c] (=/+=) sum over rows r of x[(r/G)*Gs + off + r%G][c]; work >= 256*C floats */
