@@ -537,10 +537,11 @@ int tmae_add(const float* a, const float* b, float* out, long long n, void* stre
  * when clip != NULL */
 int tmae_adam(float* p, const float* g, float* m, float* v, long long n, float lr, float beta1, float beta2, float eps,
               float weight_decay, int step, const float* clip, void* stream);
-/* the same over many tensors: table (device int64) = ntensors x {p, g, m, v, n, first_chunk, step}, chunks of
- * 1024 elements, nchunks in total; step = device address of the tensor's int32 step count (torch.optim.Adam's
- * per-parameter state["step"]), advanced by one before the update on the stream, so a captured graph replays
- * correct bias corrections */
+/* the same over many tensors: table (device int64) = ntensors x {p, g, m, v, n, first_chunk, step, bc}, then
+ * nchunks more int64 (the row of every chunk); chunks of 1024 elements, nchunks in total; step = device address of
+ * the tensor's int32 step count (torch.optim.Adam's per-parameter state["step"]), advanced by one before the
+ * update on the stream, so a captured graph replays correct bias corrections; bc = device address of 2 f32 the
+ * launch writes the tensor's bias corrections to (1 - b1^step, sqrt(1 - b2^step)) */
 int tmae_adam_multi(const long long* table, int ntensors, long long nchunks, float lr, float beta1, float beta2,
                     float eps, float weight_decay, const float* clip, void* stream);
 /* clip_grad_norm_: out[0] = ||g||_2, out[1] = min(1, max_norm / (norm + 1e-6)); work >= 2048 doubles */

@@ -1581,44 +1581,50 @@ extern "C" int tmae_adam(float* p, const float* g, float* m, float* v, long long
 // tensor by binary search over first_chunk.  One launch updates every parameter of a group.  The step counts
 // live on the device (advanced by adam_step_kernel right before), so the bias corrections need no host value
 // and a captured HIP graph replays a correct optimizer step every time.
-__global__ void adam_step_kernel(const long long* __restrict__ tab, int nt) {
+// table rows: {p, g, m, v, n, first_chunk, step, bc}; then one int64 per chunk: its row.  The step kernel advances
+// each tensor's device step count and writes its bias corrections (f64 pow rounded to f32, as tmae_adam does on
+// the host) to bc[0..1] once, instead of every thread of every chunk recomputing two f64 pows.
+__global__ void adam_step_kernel(const long long* __restrict__ tab, int nt, float b1, float b2) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < nt) ++*reinterpret_cast<int*>(tab[7 * t + 6]);
+  if (t >= nt) return;
+  const int step = ++*reinterpret_cast<int*>(tab[8 * t + 6]);
+  float* bc = reinterpret_cast<float*>(tab[8 * t + 7]);
+  bc[0] = (float)(1.0 - pow((double)b1, (double)step));
+  bc[1] = (float)sqrt(1.0 - pow((double)b2, (double)step));
 }
 
 __global__ void __launch_bounds__(256)
 adam_multi_kernel(const long long* __restrict__ tab, int nt, float lr, float b1, float b2, float eps, float wd,
                   const float* __restrict__ clip) {
   const long long b = blockIdx.x;
-  int lo = 0, hi = nt - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (tab[7 * mid + 5] <= b) lo = mid;
-    else hi = mid - 1;
-  }
-  const long long* e = tab + 7 * lo;
-  float* p = (float*)e[0];
-  const float* g = (const float*)e[1];
-  float* m = (float*)e[2];
-  float* v = (float*)e[3];
+  const long long* e = tab + 8 * tab[8 * (long long)nt + b];  // this chunk's row: one load (no search)
+  float* __restrict__ p = (float*)e[0];
+  const float* __restrict__ g = (const float*)e[1];
+  float* __restrict__ m = (float*)e[2];
+  float* __restrict__ v = (float*)e[3];
   const long long n = e[4];
-  const long long base = (b - e[5]) * 1024;
-  // bias corrections in f64 from the device step, rounded to f32 as tmae_adam does on the host
-  const int step = *reinterpret_cast<const int*>(e[6]);
-  const float bc1 = (float)(1.0 - pow((double)b1, (double)step));
-  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, (double)step));
+  const long long base = (b - e[5]) * 1024 + threadIdx.x;
+  const float* bcp = (const float*)e[7];
+  const float bc1 = bcp[0], bc2_sqrt = bcp[1];
   const float cs = clip ? clip[0] : 1.0f;
-  for (int k = threadIdx.x; k < 1024; k += 256) {
-    const long long i = base + k;
+  // a thread's 4 elements 256 apart (each wave access contiguous), every load issued before the math and stores
+  float gg[4], pv[4], mv[4], vv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const long long i = base + 256 * u;
+    if (i < n) { gg[u] = g[i]; pv[u] = p[i]; mv[u] = m[i]; vv[u] = v[i]; }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const long long i = base + 256 * u;
     if (i >= n) break;
-    float gg = g[i] * cs;
-    const float pv = p[i];
-    if (wd != 0.0f) gg += wd * pv;
-    const float mm = b1 * m[i] + (1.0f - b1) * gg;
-    const float vv = b2 * v[i] + (1.0f - b2) * gg * gg;
+    float gr = gg[u] * cs;
+    if (wd != 0.0f) gr += wd * pv[u];
+    const float mm = b1 * mv[u] + (1.0f - b1) * gr;
+    const float vq = b2 * vv[u] + (1.0f - b2) * gr * gr;
     m[i] = mm;
-    v[i] = vv;
-    p[i] = pv - (lr / bc1) * mm / (sqrtf(vv) / bc2_sqrt + eps);
+    v[i] = vq;
+    p[i] = pv[u] - (lr / bc1) * mm / (sqrtf(vq) / bc2_sqrt + eps);
   }
 }
 
@@ -1626,7 +1632,7 @@ extern "C" int tmae_adam_multi(const long long* table, int ntensors, long long n
                                float beta2, float eps, float weight_decay, const float* clip, void* stream) {
   TMAE_REQUIRE(table && ntensors > 0 && nchunks >= 0, "tmae_adam_multi: bad arguments");
   hipLaunchKernelGGL(adam_step_kernel, dim3((unsigned)((ntensors + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
-                     table, ntensors);
+                     table, ntensors, beta1, beta2);
   TMAE_LAUNCH_CHECK_NORET("tmae_adam_multi (steps)");
   if (nchunks == 0) return TMAE_OK;
   hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)nchunks), dim3(256), 0, (hipStream_t)stream, table, ntensors,

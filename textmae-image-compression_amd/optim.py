@@ -109,7 +109,13 @@ class FusedAdam(torch.optim.Optimizer):
                 if p.dtype != torch.float32 or not p.is_cuda or not p.is_contiguous():
                     raise ValueError("FusedAdam needs contiguous f32 device parameters")
         self._flat = [self._new_flat(g) for g in self.param_groups]  # per group: [m, v, steps, offsets]
+        self._bc = [self._new_bc(g) for g in self.param_groups]  # per group: 2 f32 bias corrections per parameter
         self._tabs = [None] * len(self.param_groups)
+
+    @staticmethod
+    def _new_bc(group):
+        dev = group["params"][0].device if group["params"] else None
+        return torch.zeros(2 * max(len(group["params"]), 1), dtype=torch.float32, device=dev)
 
     @staticmethod
     def _new_flat(group):
@@ -126,6 +132,7 @@ class FusedAdam(torch.optim.Optimizer):
         super().add_param_group(param_group)
         if hasattr(self, "_flat"):
             self._flat.append(self._new_flat(self.param_groups[-1]))
+            self._bc.append(self._new_bc(self.param_groups[-1]))
             self._tabs.append(None)
 
     def _table(self, gi, live):
@@ -134,14 +141,17 @@ class FusedAdam(torch.optim.Optimizer):
         if hit is not None and hit[0] == key and table_usable(hit[3]):
             return hit[1], hit[2]
         mb, vb, steps, off = self._flat[gi]
-        rows, chunk = [], 0
-        for p in live:
+        bc = self._bc[gi]
+        rows, owner, chunk = [], [], 0
+        for t, p in enumerate(live):
             n = p.numel()
             o, i = off[id(p)]
-            rows.append([p.data_ptr(), p.grad.data_ptr(), mb[o:].data_ptr(), vb[o:].data_ptr(), n, chunk,
-                         steps[i:].data_ptr()])
-            chunk += (n + CHUNK - 1) // CHUNK
-        tab, epoch = device_table(rows, mb.device)
+            rows += [p.data_ptr(), p.grad.data_ptr(), mb[o:].data_ptr(), vb[o:].data_ptr(), n, chunk,
+                     steps[i:].data_ptr(), bc[2 * i:].data_ptr()]
+            nch = (n + CHUNK - 1) // CHUNK
+            owner += [t] * nch
+            chunk += nch
+        tab, epoch = device_table(rows + owner, mb.device)  # the rows, then each chunk's row (tmae.h)
         self._tabs[gi] = (key, tab, chunk, epoch)
         return tab, chunk
 
@@ -190,6 +200,7 @@ class FusedAdam(torch.optim.Optimizer):
         # map_location="cpu", model_utils.py:14-17); the flat moments are rebuilt from it
         super().load_state_dict(state_dict)
         self._flat = [self._new_flat(g) for g in self.param_groups]
+        self._bc = [self._new_bc(g) for g in self.param_groups]
         self._tabs = [None] * len(self.param_groups)
         for gi, group in enumerate(self.param_groups):
             mb, vb, steps, off = self._flat[gi]
