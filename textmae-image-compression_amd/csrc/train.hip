@@ -441,7 +441,8 @@ extern "C" int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0,
 // and layout.  Modes (host-chosen):
 //   0  32768-element chunks: plain casts as 16-B vectors (4 rounds of 4 x 8 elements per thread), anything else
 //      as a strided gather;
-//   1  2-D transpose dst[c][r] = src[r * s3 + c] (R = d3 source rows, C = total / R): 64 x 64 LDS tiles, coalesced
+//   1  2-D transpose dst[c][r] = src[r * s3 + c] (R = d3 source rows, C = total / R; s1 != 0: also the plain cast
+//      into s1 = a second destination [R][C], one read for both layouts): 64 x 64 LDS tiles, coalesced
 //      both ways (nn.Linear data-gradient operands W^T; the conv data-gradient layout [Cin][3][3][Cout], which is
 //      the transpose of the weight seen as [Cout][Cin * 9]); 16-B loads and 4-row (8-B bf16) stores when the
 //      source rows are 16-B aligned and R % 4 == 0 (scalar 4-B loads / 2-B stores ran at ~2 TB/s);
@@ -474,8 +475,10 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
     const unsigned ntc = (C + 63) / 64;
     const unsigned r0 = (chunk / ntc) * 64, c0 = (chunk % ntc) * 64;
     const int tx = tid & 63, ty = tid >> 6;
+    // s1 != 0: also the plain cast of the same source into dst2 [R][C] (a weight needed both ways reads once)
+    void* dst2 = (void*)s1;
     const bool vec = to_bf16 && (R & 3u) == 0 && (C & 3u) == 0 && (s3 & 3) == 0 && (((unsigned long long)src) & 15) == 0 &&
-                     (((unsigned long long)dstp) & 7) == 0;
+                     (((unsigned long long)dstp) & 7) == 0 && (((unsigned long long)dst2) & 7) == 0;
     if (vec) {
       // loads: a thread reads 4 consecutive columns of rows ty4, ty4 + 16, .. (16 rows of 16 float4 per pass)
       const int c4 = 4 * (tid & 15), ty4 = tid >> 4;
@@ -483,7 +486,15 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
       for (int k = ty4; k < 64; k += 16) {
         const unsigned r = r0 + k, c = c0 + c4;
         f32x4 v = f32x4{0.f, 0.f, 0.f, 0.f};
-        if (r < R && c < C) v = load4f(src + (size_t)r * s3 + c);  // C % 4 == 0: all 4 columns valid
+        if (r < R && c < C) {
+          v = load4f(src + (size_t)r * s3 + c);  // C % 4 == 0: all 4 columns valid
+          if (dst2) {
+            bf16x4 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = (bf16)v[j];
+            *reinterpret_cast<bf16x4*>((bf16*)dst2 + (size_t)r * C + c) = o;
+          }
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) sm[k * 65 + c4 + j] = v[j];
       }
@@ -505,7 +516,12 @@ relayout_multi_kernel(const long long* __restrict__ tab, int nt) {
 #pragma unroll 4
     for (int k = ty; k < 64; k += 4) {
       const unsigned r = r0 + k, c = c0 + tx;
-      sm[k * 65 + tx] = (r < R && c < C) ? src[(size_t)r * s3 + c] : 0.0f;
+      const float v = (r < R && c < C) ? src[(size_t)r * s3 + c] : 0.0f;
+      sm[k * 65 + tx] = v;
+      if (dst2 && r < R && c < C) {
+        if (to_bf16) relayout_store<bf16>(dst2, (size_t)r * C + c, v);
+        else relayout_store<float>(dst2, (size_t)r * C + c, v);
+      }
     }
     __syncthreads();
 #pragma unroll 4

@@ -142,10 +142,25 @@ class _Weights:
         if not stale:
             return
         rows, chunk, ptrs = [], 0, []
+        # a parameter whose plain cast and transpose are both stale: the transpose row writes the cast too (mode 1
+        # with a second destination), so the f32 weight is read once
+        casts = {id(e[2]): e for e in stale if e[3] is not None and e[3][0] != "lic" and e[3][0] != "licT"
+                 and tuple(e[3][0]) == (e[2].numel(),) and tuple(e[3][1]) == (1,)}
+        fused = {}
+        for e in stale:
+            job = e[3]
+            if job is None or job[0] in ("lic", "licT") or id(e[2]) not in casts:
+                continue
+            d = list(job[0]) + [1] * (4 - len(job[0]))
+            st = list(job[1]) + [0] * (4 - len(job[1]))
+            # the transpose of the parameter's own contiguous [R][C] storage
+            if self._is_transpose(job[0], job[1]) and st[3] * d[3] == e[2].numel() and st[3] == d[0]:
+                fused[id(e[2])] = (e, casts[id(e[2])])
+        skip = {id(c) for _, c in fused.values()}
         for e in stale:
             sig, dst, p, job = e
             e[0] = (p.data_ptr(), p._version)
-            if job is None:
+            if job is None or id(e) in skip:
                 continue
             if job[0] == "licT":  # the transposed fragment order (relayout mode 4)
                 _, co, ci = job
@@ -171,6 +186,10 @@ class _Weights:
                 raise ValueError(f"weight relayout of {total} elements exceeds the 32-bit index range")
             if self._is_transpose(dims, strides):  # dst [C][R] of src [R][C] (C = d0, R = d3, ld = s3)
                 mode, n = 1, -(-d[3] // 64) * -(-d[0] // 64)
+                f = fused.get(id(p))
+                if f is not None and f[0] is e:  # + the plain cast into the "nt" copy (s1 = its address)
+                    st[1] = f[1][1].data_ptr()
+                    ptrs.append((p.data_ptr(), st[1]))
             elif (d[1] * d[2] * d[3] <= 8192 and st[2] == 1 and st[1] == d[2] and st[3] == d[1] * d[2]
                   and st[0] == d[1] * d[2] * d[3]):  # per-row [A][B] -> [B][A]
                 mode, n = 2, d[0]
