@@ -479,7 +479,8 @@ int tmae_relayout(const float* src, void* dst, int dst_dtype, int d0, int d1, in
                   long long s2, long long s3, void* stream);
 /* every relayout of a table in one launch: table[t] = {src, dst, dst_dtype | mode << 8, d1, d2, d3, s0, s1, s2, s3,
  * total, first_chunk} (int64, device memory), first_chunk = the chunks of the tensors before t (mode 0, a plain
- * or strided copy: ceil(total / 32768); mode 1, a 2-D transpose: 64 x 64 tiles; mode 2, a per-row transpose:
+ * or strided copy: ceil(total / 32768); mode 1, a 2-D transpose: 64 x 64 tiles (s1 != 0: also the plain cast of the
+ * same [d3][total / d3] source into the address s1); mode 2, a per-row transpose:
  * rows; mode 3, a 3x3 conv weight [d1 = Cout][d2 = Cin][3][3] restricted to input channels [d3, d3 + s0) into
  * tmae_lic_stack's fragment order, total = 9 * ceil(s0 / 32) * ceil(Cout / 16) * 512; mode 4, the transposed,
  * tap-flipped weight of [d1 = Cout][d2 = Cin][3][3] (input Cout, output Cin) in the same order, total = 9 *
