@@ -437,8 +437,14 @@ def roofline_report(m, imgs, scores, batch, dump=None, profiled=True):
         e = {"launches": n, "time_us": round(t * 1e6, 1), "algorithmic_bytes_per_launch": int(nbytes / max(n, 1)),
              "achieved": round(gbs, 1), "peak": PEAK_HBM / 1e9, "unit": "GB/s", "frac": round(gbs * 1e9 / PEAK_HBM, 4)}
         if f in fam_pmc:
-            e["traffic"] = fam_pmc[f]["hbm_bytes_per_launch"]
-            e["traffic_over_algorithmic"] = round(e["traffic"] / max(e["algorithmic_bytes_per_launch"], 1), 3)
+            # normalised per forward: a PMC family can hold more kernels per ABI call than the launch timer counts
+            # (eb_likelihood = eb_prep_kernel + eb_likelihood_kernel per tmae_eb_likelihood_fwd call)
+            fp = fam_pmc[f]
+            per_fwd = fp.get("hbm_bytes_per_fwd", fp["hbm_bytes_per_launch"] * fp.get("launches_per_fwd", n))
+            e["traffic"] = int(per_fwd / max(n, 1))
+            e["traffic_bytes_per_fwd"] = int(per_fwd)
+            e["kernels_per_fwd_pmc"] = fp.get("launches_per_fwd")
+            e["traffic_over_algorithmic"] = round(per_fwd / max(nbytes, 1), 3)
         if f in fwd:
             e["avg_launch_us_in_forward"] = fwd[f]["avg_launch_us"]
             e["frac_in_forward"] = round(nbytes / max(n, 1) / (fwd[f]["avg_launch_us"] * 1e-6) / PEAK_HBM, 4)

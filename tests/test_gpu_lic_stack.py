@@ -188,7 +188,8 @@ def _gelu_grad(x):
     return 0.5 * (1.0 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
 
 
-@pytest.mark.parametrize("G,P,routed", [(12, 2, False), (12, 3, False), (8, 1, False), (12, 2, True), (8, 1, True)])
+@pytest.mark.parametrize("G,P,routed", [(12, 2, False), (12, 3, False), (8, 1, False), (12, 2, True), (8, 1, True),
+                                        (12, 3, True)])
 def test_lic_stack_bwd_vs_torch(tmae, G, P, routed):
     """TMAE_LIC_STACK_BWD (the fused data-gradient chain of a stack's layers 4..1, mcm_train._fused_dgrads) against
     torch: per layer dx = conv_transpose2d(d, W) (conv2d's input gradient) * GELU'(pre), rounded to bf16 as the
@@ -217,7 +218,10 @@ def test_lic_stack_bwd_vs_torch(tmae, G, P, routed):
         wpk.append(torch.stack([ops.pack_lic_stack_weight_t(w) for w in w0]).contiguous())
         st["w4"] = (wpk[4][0].numel(), 0)
         couts.append(cin0)
-        accs = [[torch.randn(rows, c + 8, device=DEV) for c in split] for _ in range(P)]
+        # each range's accumulators of all problems at one constant stride inside one buffer (the route stride
+        # lic_stack_bwd derives from problems 0 -> 1 must hold for every later problem too: P = 3 checks it)
+        bufs = [torch.randn(P, rows, c + 8, device=DEV) for c in split]
+        accs = [[b[p] for b in bufs] for p in range(P)]
         acc0 = [[a.clone() for a in ap] for ap in accs]
         routes = [[(a, c + 8, c) for a, c in zip(ap, split)] for ap in accs]
     ops.lic_stack_bwd(n, G, dtop.to(torch.bfloat16), chans[5], chans[5], wpk, couts,

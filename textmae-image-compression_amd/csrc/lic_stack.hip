@@ -563,6 +563,8 @@ extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {
                    "tmae_lic_stack: backward layer %d needs w / sv_pre / sv_act", l);
     if (rt) {
       const int cl = a.cout[a.nlayers - 1];
+      // the routed accumulators step by the problem's nb1 index only (racc + b1 * rs)
+      TMAE_REQUIRE(a.nb2 <= 1, "tmae_lic_stack: routed accumulators need nb2 == 1 (got %d)", a.nb2);
       TMAE_REQUIRE(a.rlim[0] >= 0 && a.rlim[0] <= a.rlim[1] && a.rlim[1] <= a.rlim[2] && a.rlim[2] == cl &&
                    a.rlim[0] % 4 == 0 && a.rlim[1] % 4 == 0, "tmae_lic_stack: routes %d / %d / %d of %d channels",
                    a.rlim[0], a.rlim[1], a.rlim[2], cl);

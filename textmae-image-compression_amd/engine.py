@@ -12,8 +12,6 @@ Logging (MetricLogger / TensorBoard) is out of scope.
 """
 from __future__ import annotations
 
-import time
-
 import torch
 
 from . import distributed
@@ -27,6 +25,16 @@ def _clip_buffer(optimizer):
         dev = next(p.device for g in optimizer.param_groups for p in g["params"])
         buf = optimizer._clip_buf = torch.empty(2, dtype=torch.float32, device=dev)
     return buf
+
+def _drain_watchdog(group):
+    """Return once the process group's watchdog holds no pending work: ``_wait_for_pending_works`` blocks until
+    its work list is empty (the GPU must have finished them, so the device is synchronised first)."""
+    import torch.distributed as dist
+
+    torch.cuda.synchronize()
+    pg = group if group is not None else dist.group.WORLD
+    pg._wait_for_pending_works()
+
 
 METRICS = ("loss", "L1_loss", "ssim_loss", "vgg_loss", "bpp_loss", "aux_loss")
 
@@ -128,15 +136,18 @@ class GraphedTrainStep:
         bump_versions(self.params)
         self._staging = reserve_capture_staging()  # the graph's copy nodes read it at every replay
         sync = getattr(self.model, "grad_sync", None)
-        if sync is not None and sync.world() >= 1 and (sync.world() > 1 or sync.always_collective):
+        mode = "global"
+        if sync is not None and (sync.world() > 1 or sync.always_collective):
             # the warm-up step's RCCL works sit in the process group's watchdog until it sees them complete; it
             # queries their end events, recorded on the process group's stream -- which the capture below turns
             # into a capturing stream, where such a query fails (hipErrorCapturedEvent) and takes the watchdog
-            # down.  Let every eager collective finish and the watchdog (100 ms poll) retire it first.
-            torch.cuda.synchronize()
-            time.sleep(0.5)
+            # down.  By construction: block until the watchdog has retired every pending work (collectives issued
+            # during the capture are never handed to it), and capture in thread-local mode so that a query from
+            # the watchdog's thread cannot invalidate the capture either.
+            _drain_watchdog(sync.group)
+            mode = "thread_local"
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode=mode):
             out = self._step()
         self.graph, self.out = g, out
         self._hyper_at_capture = self._hyper()

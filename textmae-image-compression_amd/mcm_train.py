@@ -186,8 +186,11 @@ class _Weights:
                 raise ValueError(f"weight relayout of {total} elements exceeds the 32-bit index range")
             if self._is_transpose(dims, strides):  # dst [C][R] of src [R][C] (C = d0, R = d3, ld = s3)
                 mode, n = 1, -(-d[3] // 64) * -(-d[0] // 64)
+                st[1] = 0  # mode 1 reads s1 as the second destination (none unless fused below)
                 f = fused.get(id(p))
                 if f is not None and f[0] is e:  # + the plain cast into the "nt" copy (s1 = its address)
+                    if f[1][1].dtype != dst.dtype:
+                        raise ValueError("relayout: a fused cast copy must have the transpose's dtype")
                     st[1] = f[1][1].data_ptr()
                     ptrs.append((p.data_ptr(), st[1]))
             elif (d[1] * d[2] * d[3] <= 8192 and st[2] == 1 and st[1] == d[2] and st[3] == d[1] * d[2]

@@ -277,18 +277,21 @@ def lic_stack_bwd(n, G, dtop, ldt, c_top, weights, couts, pres, outs, nb=(1, 1),
     layer is the stack's first conv's input gradient, added into those accumulators (no pres / outs entry)."""
     a = LicStackArgs()
     if routes is not None:
+        if nb[1] != 1:
+            # the kernel steps routed accumulators by problem index along nb1 only
+            raise ValueError("lic_stack_bwd routes: nb2 must be 1")
+        if len(routes) > 1 and len(routes) != nb[0]:
+            raise ValueError("lic_stack_bwd routes: one route list per problem")
         lim = 0
         for r in range(3):
             if r < len(routes[0]):
                 acc, ld, nc = routes[0][r]
                 a.racc[r], a.rld[r] = _p(acc), ld
-                if len(routes) > 1:
-                    deltas = {_p(rt[r][0]) - _p(acc) for rt in routes[1:]} if nc else {0}
-                    if len(routes) > 2:
-                        steps = [_p(routes[k + 1][r][0]) - _p(routes[k][r][0]) for k in range(len(routes) - 1)]
-                        if len(set(steps)) != 1:
-                            raise ValueError("lic_stack_bwd routes: accumulators not at a constant stride")
-                    a.rs[r] = (next(iter(deltas)) // 4) if nc else 0
+                if len(routes) > 1 and nc:
+                    steps = [_p(routes[k + 1][r][0]) - _p(routes[k][r][0]) for k in range(len(routes) - 1)]
+                    if len(set(steps)) != 1 or steps[0] % 4:
+                        raise ValueError("lic_stack_bwd routes: accumulators not at a constant stride")
+                    a.rs[r] = steps[0] // 4  # problem k's accumulator = problem 0's + k * stride (f32 elements)
                 lim += nc
             a.rlim[r] = lim
     a.n, a.G, a.nlayers = n, G, len(couts)
