@@ -230,6 +230,17 @@ static int linear_t(const void* x, int x_f32, int ldx, int G, int Gs, int off, c
   return linear_epi<T, DenseSrc<T>, true>(W, N, K, xs, y, y_f32, ldy, y32, ld32, bias, M, act, st, pre, ldp);
 }
 
+#if TMAE_GEMM_TRACE
+extern "C" int tmae_gemm_trace_read(void* dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_gemm_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+extern "C" int tmae_gemm_trace_reset() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_gemm_trace)) != hipSuccess) return 1;
+  return hipMemset(p, 0, sizeof(g_gemm_trace)) == hipSuccess ? 0 : 1;
+}
+#endif
+
 extern "C" int tmae_linear_fwd_pre(const void* x, int x_f32, int ldx, int row_group, int group_stride, int row_offset,
                                    const void* w, const float* bias, void* y, int y_f32, int ldy, void* pre, int ldp,
                                    int M, int N, int K, int act, int dtype, void* stream) {

@@ -378,6 +378,25 @@ __device__ __forceinline__ void epilogue_lds(const EPI& epi, const f32x4 (&acc)[
   }
 }
 
+// ------------------------------------------------------------------ timeline builds (tools/gemm_trace.py)
+// -DTMAE_GEMM_TRACE=1: wave 0 of every workgroup of gemm_glds_kernel stamps the shader clock (s_memtime) at its
+// start, after the prologue's DMA wait, after the K loop and after the epilogue, with its HW_ID / XCC_ID, into one
+// row per workgroup of g_gemm_trace (read by tmae_gemm_trace_read in gemm.hip).
+#ifndef TMAE_GEMM_TRACE
+#define TMAE_GEMM_TRACE 0
+#endif
+#if TMAE_GEMM_TRACE
+constexpr int GEMM_TR_WG = 8192, GEMM_TR_SLOTS = 8;
+static __device__ unsigned long long g_gemm_trace[GEMM_TR_WG * GEMM_TR_SLOTS];
+__device__ __forceinline__ void gemm_tr(int slot, unsigned long long v) {
+  const int wg = blockIdx.x + gridDim.x * blockIdx.y;
+  if (threadIdx.x == 0 && wg < GEMM_TR_WG) g_gemm_trace[(size_t)wg * GEMM_TR_SLOTS + slot] = v;
+}
+#define GEMM_TR(slot) gemm_tr(slot, __builtin_amdgcn_s_memtime())
+#else
+#define GEMM_TR(slot) ((void)0)
+#endif
+
 // ------------------------------------------------------------------ glds kernel
 // One output tile per workgroup (XCD-aware tile order), 2-stage LDS ring: the next K-step's
 // LDS-DMA is in flight under the current K-step's MFMAs.  After the last K-step the ring is reused
@@ -420,6 +439,11 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
   static_assert(NS >= 2 && NS <= 4, "stages");
   __shared__ __attribute__((aligned(16))) uint4 lds[NS * ROWS * 8];
 
+  GEMM_TR(0);
+#if TMAE_GEMM_TRACE
+  gemm_tr(4, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4));   // HW_ID
+  gemm_tr(5, (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20));  // XCC_ID
+#endif
   const int b1 = blockIdx.y / n2, b2 = blockIdx.y - (blockIdx.y / n2) * n2;
   ws.batch(b1, b2);
   xs.batch(b1, b2);
@@ -480,6 +504,7 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
     issue(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    GEMM_TR(1);
     int stage = 0;
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) issue(stage ^ 1, kt + 1);
@@ -497,12 +522,14 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
     for (int s = 0; s < NS - 1; ++s)
       if (s < nk) issue(s, s);
     gemm_ring_wait<PER, NS>(min(NS - 2, nk - 1));
+    GEMM_TR(1);
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + NS - 1 < nk) issue((kt + NS - 1) % NS, kt + NS - 1);
       mfma_tile<T, BN, WN, WM, TN, TM>(lds + (kt % NS) * ROWS * 8, wn, wm, lane, acc);
       gemm_ring_wait<PER, NS>(min(kt + NS - 1, nk - 1) - (kt + 1));
     }
   }
+  GEMM_TR(2);
   static_assert(NW * EpiRegion<WN>::FLOATS * 4 <= NS * ROWS * 128, "epilogue region exceeds the LDS ring");
 #if defined(TMAE_GEMM_DIAG) && (TMAE_GEMM_DIAG & 1)  // phase isolation builds: no epilogue (accumulators kept live)
 #pragma unroll
@@ -513,6 +540,11 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
 #endif
   epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
                            tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
+  GEMM_TR(3);
+#if TMAE_GEMM_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  GEMM_TR(6);  // wave 0's stores complete
+#endif
 }
 
 // ------------------------------------------------------------------ register-staged kernel

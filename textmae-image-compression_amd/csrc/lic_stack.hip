@@ -69,6 +69,7 @@ struct LstkOut {
   int route;  // TMAE_LIC_STACK_BWD, last layer with racc: f32 += into the channel-range accumulators,
   LstkArgs* ra;  // read from the kernarg block at the epilogue (copies held per layer spilled SGPRs to scratch)
   int rb1;       // the problem index the route strides apply to
+  int trl;       // LSTK_TRACE: the layer's trace slot base
 };
 
 #ifndef LSTK_OPT
@@ -77,6 +78,34 @@ struct LstkOut {
 #ifndef LSTK_DIAG
 #define LSTK_DIAG 0  // phase isolation builds (tools/lstk_diag.sh): 4 = no MFMA, 8 = no B reads, 16 = no A loads,
                      // 32 = no epilogue, 64 = no layer-0 addend loads, 128 = no GELU (bias only)
+#endif
+
+#ifndef LSTK_TRACE
+#define LSTK_TRACE 0  // timeline builds (tools/lstk_trace.py): per wave and layer, K-loop / epilogue cycles, done / exit times
+#endif
+#if LSTK_TRACE
+// [workgroup][wave][48] shader-clock stamps (s_memtime): 0 start, 1 after the prologue barrier, then per layer slot
+// 2 + 4 l: layer start, K-loop cycles, epilogue cycles, items done; 47 end.  One writer per slot (lane 0).
+constexpr int LSTK_TR_WG = 1024, LSTK_TR_SLOTS = 48;
+__device__ unsigned long long g_lstk_trace[LSTK_TR_WG * 8 * LSTK_TR_SLOTS];
+__device__ __forceinline__ unsigned long long* lstk_tr_slot(int s) {
+  const int wg = blockIdx.x < LSTK_TR_WG ? blockIdx.x : LSTK_TR_WG - 1;
+  return g_lstk_trace + ((size_t)wg * 8 + (threadIdx.x >> 6)) * LSTK_TR_SLOTS + s;
+}
+__device__ __forceinline__ void lstk_tr_set(int s, unsigned long long v) {
+  if ((threadIdx.x & 63) == 0) *lstk_tr_slot(s) = v;
+}
+__device__ __forceinline__ void lstk_tr_add(int s, unsigned long long v) {
+  if ((threadIdx.x & 63) == 0) *lstk_tr_slot(s) += v;
+}
+extern "C" int tmae_lstk_trace_read(void* dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_lstk_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+extern "C" int tmae_lstk_trace_reset() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_lstk_trace)) != hipSuccess) return 1;
+  return hipMemset(p, 0, sizeof(g_lstk_trace)) == hipSuccess ? 0 : 1;
+}
 #endif
 
 __device__ __forceinline__ bf16x8 lstk_lds8(const unsigned char* lb, unsigned off) {
@@ -102,6 +131,9 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
   // opaque per item: keeps the per-fragment pixel / address math inside the item (hoisted out of the
   // layer loop it was ~70 VGPRs of 64-bit epilogue addresses, all spilled)
   asm volatile("" : "+v"(lane));
+#if LSTK_TRACE
+  const unsigned long long tr_a = __builtin_amdgcn_s_memtime();
+#endif
   const int fr = lane & 15, fq = lane >> 4;
   const int nfr = (L.cout + 15) >> 4;
   f32x4 acc[NF][MF];
@@ -183,7 +215,21 @@ __device__ __forceinline__ void lstk_item(const LstkLayer& L, bool first, bool l
     }
   }
 
+  // (Round 6 measured the bias loaded before the K loop -- ms_3 65.3-65.9 vs 65.7-66.1 us, profiles/r06/c4_lstk.txt
+  // -- and a deferred epilogue: a wave's two items of a hidden layer, the first item's GELU / LDS stores issued inside
+  // the second item's K loop, bitwise the same outputs, ms_3 65.5 vs 65.3 us and the forward 9806 / 9823 vs
+  // 9862 / 9855 img/s same box, c7_*: the K loops do not leave the MFMA pipe idle enough for the epilogue's VALU to
+  // hide in.  Neither was kept.)
   // epilogue: lane holds channels c..c+3 of pixel 16 (j0 + j) + fr
+#if LSTK_TRACE
+  const unsigned long long tr_b = __builtin_amdgcn_s_memtime();
+  lstk_tr_add(o.trl + 1, tr_b - tr_a);
+  struct TrEnd {
+    unsigned long long b;
+    int slot;
+    __device__ ~TrEnd() { lstk_tr_add(slot, __builtin_amdgcn_s_memtime() - b); }
+  } tr_end{tr_b, o.trl + 2};
+#endif
 #if LSTK_DIAG & 32  // phase isolation: no epilogue (keep the accumulators alive)
 #pragma unroll
   for (int i = 0; i < NF; ++i)
@@ -368,6 +414,9 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
   const bool ilv = a->flags & TMAE_LIC_STACK_CHAIN;
   const long long b1 = ilv ? prob % a->nb1 : prob / nb2, b2 = ilv ? prob / a->nb1 : prob - (prob / nb2) * nb2;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if LSTK_TRACE
+  lstk_tr_set(0, __builtin_amdgcn_s_memtime());
+#endif
 
   // zero row + layer-0 input -> buffer 0 (channels [0, c1) from x1, [c1, cin0) from x2, pad zeros)
   for (int i = tid; i < 16 * MAXPITCH / 16; i += NW * 64) reinterpret_cast<uint4*>(lds)[ZOFF / 16 + i] = uint4{0, 0, 0, 0};
@@ -400,6 +449,10 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
     }
   }
   __syncthreads();
+#if LSTK_TRACE
+  lstk_tr_set(1, __builtin_amdgcn_s_memtime());
+  int tr_layer = 0;
+#endif
 
   // pass 0: the stack of this problem; pass 1 (TMAE_LIC_STACK_CHAIN, problem (0, 0) = a slice's mean stack):
   // that slice's lrp stack, same workgroup, its input built from the mean stack's output
@@ -493,6 +546,10 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
         o.sa = o.sp ? reinterpret_cast<bf16*>(a->csv_act[l]) + b2 * a->cs_sv[l] : nullptr;
         o.st = a->csv_t && last ? a->csv_t + b2 * a->cs_t : nullptr;
       }
+#if LSTK_TRACE
+      o.trl = 2 + 4 * min(tr_layer, 10);
+      lstk_tr_set(o.trl, __builtin_amdgcn_s_memtime());
+#endif
       const unsigned in_off = (l & 1) ? (unsigned)BUF : 0u, out_off = (l & 1) ? 0u : (unsigned)BUF;
       const int nfr = (L.cout + 15) >> 4;
       const int nkc = pad32(L.cin) >> 5;
@@ -540,9 +597,16 @@ __global__ void __launch_bounds__(lstk::NW * 64) lic_stack_kernel(tmae_lic_stack
           }
       }
       cin = L.cout;
+#if LSTK_TRACE
+      lstk_tr_set(o.trl + 3, __builtin_amdgcn_s_memtime());
+      ++tr_layer;
+#endif
       __syncthreads();
     }
   }
+#if LSTK_TRACE
+  lstk_tr_set(47, __builtin_amdgcn_s_memtime());
+#endif
 }
 
 extern "C" int tmae_lic_stack(const tmae_lic_stack_args* args, void* stream) {

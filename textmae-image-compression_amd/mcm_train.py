@@ -311,7 +311,15 @@ class _VitTrainBase:
     def _ready(self, p):
         """every gradient up to and including p's is final (DP bucket hand-off).  With weight gradients on the
         side stream the hand-off lags one call: the compute stream waits for the side stream's work up to the
-        PREVIOUS hand-off point (long done by then), so the collective never stalls the data-gradient chain."""
+        PREVIOUS hand-off point and issues that bucket's collective.
+        Round 6 (profiles/r06/c2_*, c5-c7): in a captured one-rank DP step these waits are what costs the +4 ms
+        over the plain graphed step (31.8-32.9 vs 27.8-28.6 ms): the side stream runs far behind the data-gradient
+        chain, so the chain stalls at some hand-offs (a kernel trace: 24 HIP-queue hops of the compute chain, 3.75 ms
+        of gaps at them, the largest 1.76 ms), and RCCL's one-rank reduce kernels (32 workgroups, ~110 us per 64 MB
+        bucket) share the chip with the backward.  Issuing each collective from the side stream instead (it then
+        waits for the compute stream's hand-off point, the compute stream never waits inside the backward), or from a
+        third stream joined to both, measured 36.7-37.6 ms; a lag of 2 / 4 hand-offs 31.8 / 33.2 ms; HIP graph
+        queue counts (DEBUG_HIP_FORCE_GRAPH_QUEUES 2 / 3) changed nothing."""
         if self.sync is None:
             self._wg_flush()
             return
