@@ -323,6 +323,9 @@ __device__ __forceinline__ void epi_emit8_pre(const EPI& e, int m, int n, f32x4 
   }
 }
 
+#ifndef TMAE_EPI_BF16_DIRECT
+#define TMAE_EPI_BF16_DIRECT 1  // A/B builds: 0 = plain bf16 stores through the f32 transpose (epilogue_lds)
+#endif
 #ifndef TMAE_EPI_DEEP_ALWAYS
 #define TMAE_EPI_DEEP_ALWAYS 0  // A/B builds: 1 = the one-block-ahead fetch for every instantiation
 #endif
@@ -376,6 +379,71 @@ __device__ __forceinline__ void epilogue_lds(const EPI& epi, const f32x4 (&acc)[
       for (int q = 0; q < QR; ++q) epi_fetch(e, m0 + 16 * (j + 1) + q * RPI + rr, ncol, M, N, pf[0][q]);
     }
   }
+}
+
+// Plain bf16 stores (EpiStore<bf16, ACT> with no addend / pre-activation / f32 copy; N, ldo multiples of 8): bias and
+// the activation are applied in the MFMA layout (each lane's 4 consecutive columns), the values rounded to bf16 and
+// only THEN transposed through the wave's LDS region -- 8-B writes and half the read-back bytes of the f32 transpose
+// (ds_write_b64 rows WN + 4 bf16 apart: conflict-free; ds_read_b128 2-way at most).  Same arithmetic per element as
+// epilogue_lds + EpiStore::wide (acc + bias, the packed GELU, round to bf16): bitwise the same output.
+template <class E, class = void> struct HasDirectBf16 : std::false_type {};
+template <class E>
+struct HasDirectBf16<E, std::enable_if_t<E::kDirectBf16>> : std::true_type {};
+
+template <int TN, int TM, int WN, class EPI>
+__device__ __forceinline__ void epilogue_lds_bf16(const EPI& e, const f32x4 (&acc)[TN][TM], bf16* region, int n0,
+                                                  int m0, int lane, int M, int N) {
+  constexpr int ST = WN + 4;     // row stride (bf16)
+  constexpr int LPR = WN / 8;    // lanes per row (8 bf16 = 16 B each)
+  constexpr int RPI = 64 / LPR;  // rows per read round
+  constexpr int QR = 16 / RPI;   // read rounds per 16-row block
+  const int fr = lane & 15, fq = lane >> 4;
+  const int rr = lane / LPR, cc = lane - rr * LPR;
+  f32x4 bv[TN];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int n = n0 + 16 * i + 4 * fq;
+    bv[i] = (e.bias && n < N) ? load4f(e.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const int ncol = n0 + 8 * cc;
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      f32x4 v = acc[i][j] + bv[i];
+      if constexpr (EPI::kAct == TMAE_ACT_GELU) {
+        v.xy = gelu2_bf16out(v.xy);
+        v.zw = gelu2_bf16out(v.zw);
+      }
+      if constexpr (EPI::kAct == TMAE_ACT_RELU) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = fmaxf(v[k], 0.0f);
+      }
+      bf16x4 q;
+      q[0] = (bf16)v[0]; q[1] = (bf16)v[1]; q[2] = (bf16)v[2]; q[3] = (bf16)v[3];
+      *reinterpret_cast<bf16x4*>(region + fr * ST + 16 * i + 4 * fq) = q;
+    }
+#pragma unroll
+    for (int q = 0; q < QR; ++q) {
+      const int row = q * RPI + rr;
+      const uint4 val = *reinterpret_cast<const uint4*>(region + row * ST + 8 * cc);
+      const int m = m0 + 16 * j + row;
+      if (m < M && ncol < N) *reinterpret_cast<uint4*>(e.out + (size_t)m * e.ldo + ncol) = val;
+    }
+  }
+}
+
+// the epilogue of one wave's tile: the bf16-first transpose when the functor allows it, else epilogue_lds
+template <int TN, int TM, int WN, class EPI>
+__device__ __forceinline__ void epilogue_any(const EPI& epi, const f32x4 (&acc)[TN][TM], float* region, int n0, int m0,
+                                             int lane, int M, int N) {
+  if constexpr (HasDirectBf16<EPI>::value && TMAE_EPI_BF16_DIRECT) {
+    if (epi.direct_ok(N)) {  // wave-uniform
+      epilogue_lds_bf16<TN, TM, WN>(epi, acc, reinterpret_cast<bf16*>(region), n0, m0, lane, M, N);
+      return;
+    }
+  }
+  epilogue_lds<TN, TM, WN>(epi, acc, region, n0, m0, lane, M, N);
 }
 
 // ------------------------------------------------------------------ timeline builds (tools/gemm_trace.py)
@@ -538,7 +606,7 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
     for (int j = 0; j < TM; ++j) asm volatile("" ::"v"(acc[i][j]));
   return;
 #endif
-  epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
+  epilogue_any<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS,
                            tn * BN + wn * WN, tm * BM + wm * WM, lane, M, N);
   GEMM_TR(3);
 #if TMAE_GEMM_TRACE
@@ -614,7 +682,7 @@ gemm_reg_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
     __syncthreads();
   }
   static_assert(4 * EpiRegion<WN>::FLOATS * 4 <= 2 * ROWS * 128, "epilogue region exceeds the LDS ring");
-  epilogue_lds<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS, n0 + wn * WN,
+  epilogue_any<TN, TM, WN>(epi, acc, reinterpret_cast<float*>(lds) + wave * EpiRegion<WN>::FLOATS, n0 + wn * WN,
                            m0 + wm * WM, lane, M, N);
 }
 
@@ -726,6 +794,8 @@ static int launch_gemm(const char* name, const T* w, long long ws1, long long ws
 // ------------------------------------------------------------------ shared epilogues
 // out[m][n..n+3] = act(acc + bias (+ addend[m][n])) in OT; optional second f32 copy (out32).
 template <typename OT, int ACT> struct EpiStore {
+  static constexpr bool kDirectBf16 = sizeof(OT) == 2;  // epilogue_lds_bf16 (when direct_ok)
+  static constexpr int kAct = ACT;
   OT* out;
   int ldo;
   const float* bias;
@@ -757,6 +827,9 @@ template <typename OT, int ACT> struct EpiStore {
     }
     store4(out + (size_t)m * ldo + n, v);
     if (out32) store4(out32 + (size_t)m * ld32 + n, v);
+  }
+  __device__ bool direct_ok(int N) const {
+    return !addend && !pre && !out32 && (N & 7) == 0 && (ldo & 7) == 0 && ((uintptr_t)out & 15) == 0;
   }
   // epilogue_lds hooks: this lane's bias columns once, the addend one row block ahead
   f32x4 pb0, pb1;

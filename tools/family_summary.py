@@ -84,6 +84,7 @@ def summarize(rows, mode):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
+    ap.add_argument("--cite", default=None, help="the committed copy of the trace to name in the JSON (profiles/rNN/...)")
     ap.add_argument("--json")
     g = ap.add_mutually_exclusive_group()
     g.add_argument("--replay", action="store_true")
@@ -93,7 +94,8 @@ def main():
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     if a.both:
-        out = {"trace": a.trace, "forward": summarize(rows, "forward"), "replay": summarize(rows, "replay")}
+        out = {"trace": a.cite or a.trace, "trace_raw": a.trace, "forward": summarize(rows, "forward"),
+               "replay": summarize(rows, "replay")}
     else:
         out = summarize(rows, "replay" if a.replay else "forward" if a.forward else "all")
     print(json.dumps(out, indent=1))
