@@ -553,38 +553,37 @@ mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, c
   const bf16* gbase = dout + (size_t)b * Tn * D + h * DH;
   const int tid = threadIdx.x, nthr = blockDim.x;
 
-  attn_stage2<DH, LDR>(Qs, base, ld, Gs, gbase, D, Tn, Tpad, tid, nthr);  // Q, dO
-  if constexpr (!KREG)
-    for (int i = tid; i < Tpad * CPR; i += nthr) {                          // K
-      const int r = i / CPR, c = i - r * CPR;
-      uint4 x = uint4{0, 0, 0, 0};
-      if (r < Tn) x = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + D + c * 8);
-      *reinterpret_cast<uint4*>(Ks + (size_t)r * LDR + c * 8) = x;
-    }
-  for (int i = tid; i < DH * LDQ / 4; i += nthr) reinterpret_cast<f32x4*>(dQs)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int r = tid; r < Tpad; r += nthr) {  // delta = rowsum(dO * O), lse
-    float d = 0.0f, l = 0.0f;
+  // Prologue: EVERY global load of the staging (Q, dO, K), of delta / lse and of this wave's K / V fragments is
+  // issued before the first LDS store.  Written as separate loops (the stores of one chunk before the next chunk's
+  // loads) it was ~10 dependent HBM round trips per workgroup at one workgroup per CU.  nthr == 2 Tpad (one wave
+  // per 32 rows), so each thread stages exactly CPR / 2 chunks of each array and delta for at most one row.
+  static_assert(CPR % 2 == 0, "staging: an even number of 16-B chunks per row");
+  constexpr int IT = CPR / 2;
+  uint4 qv[IT], gv[IT], kv[KREG ? 1 : IT];
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int i = tid + k * nthr, r = i / CPR, c = i - r * CPR;
+    qv[k] = gv[k] = uint4{0, 0, 0, 0};
+    if constexpr (!KREG) kv[k] = uint4{0, 0, 0, 0};
     if (r < Tn) {
-      const bf16* orow = obase + (size_t)r * D;
-      const bf16* grow = gbase + (size_t)r * D;
-#pragma unroll
-      for (int c = 0; c < CPR; ++c) {
-        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(orow + 8 * c);
-        const bf16x8 gv = *reinterpret_cast<const bf16x8*>(grow + 8 * c);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) d += (float)ov[e] * (float)gv[e];
-      }
-      l = lse[(size_t)bh * Tn + r];
+      qv[k] = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + c * 8);
+      gv[k] = *reinterpret_cast<const uint4*>(gbase + (size_t)r * D + c * 8);
+      if constexpr (!KREG) kv[k] = *reinterpret_cast<const uint4*>(base + (size_t)r * ld + D + c * 8);
     }
-    dl_s[r] = d;
-    lse_s[r] = l;
   }
-  __syncthreads();
-
+  bf16x8 orow_v[CPR], grow_v[CPR];
+  float lrow = 0.0f;
+  const bool drow = tid < Tn;  // delta = rowsum(dO * O) and lse of row tid (rows Tn .. Tpad - 1: 0)
+  if (drow) {
+#pragma unroll
+    for (int c = 0; c < CPR; ++c) {
+      orow_v[c] = *reinterpret_cast<const bf16x8*>(obase + (size_t)tid * D + 8 * c);
+      grow_v[c] = *reinterpret_cast<const bf16x8*>(gbase + (size_t)tid * D + 8 * c);
+    }
+    lrow = lse[(size_t)bh * Tn + tid];
+  }
   const int lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, hh = lane >> 5;
-  const float c2 = scale * 1.4426950408889634f;
-  const bool ragged = (Tn & 31) != 0;
   const int kb = 32 * wave;
   const int kr = min(kb + col, Tn - 1);
   bf16x8 kf[DH / 16], vf[DH / 16];
@@ -593,6 +592,29 @@ mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, c
     kf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)kr * ld + D + 16 * s + 8 * hh);
     vf[s] = *reinterpret_cast<const bf16x8*>(base + (size_t)kr * ld + 2 * D + 16 * s + 8 * hh);
   }
+  for (int i = tid; i < DH * LDQ / 4; i += nthr) reinterpret_cast<f32x4*>(dQs)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int i = tid + k * nthr, r = i / CPR, c = i - r * CPR;
+    *reinterpret_cast<uint4*>(Qs + (size_t)r * LDR + c * 8) = qv[k];
+    *reinterpret_cast<uint4*>(Gs + (size_t)r * LDR + c * 8) = gv[k];
+    if constexpr (!KREG) *reinterpret_cast<uint4*>(Ks + (size_t)r * LDR + c * 8) = kv[k];
+  }
+  if (tid < Tpad) {
+    float d = 0.0f;
+    if (drow) {
+#pragma unroll
+      for (int c = 0; c < CPR; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d += (float)orow_v[c][e] * (float)grow_v[c][e];
+    }
+    dl_s[tid] = d;
+    lse_s[tid] = lrow;
+  }
+  __syncthreads();
+
+  const float c2 = scale * 1.4426950408889634f;
+  const bool ragged = (Tn & 31) != 0;
   f32x16 dV[NDT], dK[NDT];
 #pragma unroll
   for (int t = 0; t < NDT; ++t)
