@@ -514,6 +514,24 @@ mha_bwd_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, co
   }
 }
 
+#ifndef TMAE_ATTN_TRACE
+#define TMAE_ATTN_TRACE 0  // timeline builds (tools/attn_trace.py): wave 0's shader clock at the backward's phases
+#endif
+#if TMAE_ATTN_TRACE
+// [workgroup][16]: 0 start, 1 prologue barrier passed, 2 + it: step it's barrier passed (<= 10 steps), 14 dK / dV
+// stored, 15 dQ stored
+static __device__ unsigned long long g_attn_trace[4096 * 16];
+#define ATTN_TR(slot)                                                                                          \
+  do {                                                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_attn_trace[blockIdx.x * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+extern "C" int tmae_attn_trace_read(void* dst, size_t bytes) {
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_attn_trace), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#else
+#define ATTN_TR(slot) ((void)0)
+#endif
+
 // One-pass form: each wave owns 32 keys (dK^T, dV^T in registers) and walks the query tiles in a STAGGERED order --
 // wave w takes tile (w + it) mod nw at step it -- so at every step each query tile belongs to exactly one wave.
 // That wave's dQ contribution dS K (dS through a per-wave LDS scratch, the only operand crossing lanes) is added
@@ -552,6 +570,7 @@ mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, c
   const bf16* obase = o + (size_t)b * Tn * D + h * DH;
   const bf16* gbase = dout + (size_t)b * Tn * D + h * DH;
   const int tid = threadIdx.x, nthr = blockDim.x;
+  ATTN_TR(0);
 
   // Prologue: EVERY global load of the staging (Q, dO, K), of delta / lse and of this wave's K / V fragments is
   // issued before the first LDS store.  Written as separate loops (the stores of one chunk before the next chunk's
@@ -612,6 +631,7 @@ mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, c
     lse_s[tid] = lrow;
   }
   __syncthreads();
+  ATTN_TR(1);
 
   const float c2 = scale * 1.4426950408889634f;
   const bool ragged = (Tn & 31) != 0;
@@ -718,6 +738,7 @@ mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, c
         *pq = v;
       }
     __syncthreads();
+    ATTN_TR(2 + min(it, 11));
   }
 #pragma unroll
   for (int t = 0; t < NDT; ++t)
@@ -730,6 +751,7 @@ mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, c
         row[2 * D] = (bf16)dV[t][r];
       }
     }
+  ATTN_TR(14);
   // dQ rows -> dqkv (8 head-dim values per thread, one 16-B store)
   for (int i = tid; i < Tn * CPR; i += nthr) {
     const int q = i / CPR, c = i - q * CPR;
@@ -738,6 +760,10 @@ mha_bwd1_bf16_kernel(const bf16* __restrict__ qkv, const bf16* __restrict__ o, c
     for (int e = 0; e < 8; ++e) v[e] = (bf16)dQs[(size_t)(8 * c + e) * LDQ + q];
     *reinterpret_cast<bf16x8*>(dqkv + ((size_t)b * Tn + q) * ld + h * DH + 8 * c) = v;
   }
+#if TMAE_ATTN_TRACE
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ATTN_TR(15);
+#endif
 }
 
 // f32 (parity) form: same two phases on v_mfma_f32_32x32x2_f32, operands read straight from global memory
