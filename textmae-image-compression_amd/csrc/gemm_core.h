@@ -131,7 +131,44 @@ template <typename T> struct ConvSrc {
     return (ci < c1) ? (const void*)(x1 + (size_t)pix * ld1 + ci) : (const void*)(x2 + (size_t)pix * ld2 + (ci - c1));
   }
   __device__ uint4 load(const Row& r, int kt, int c) const { return *reinterpret_cast<const uint4*>(addr(r, kt, c)); }
+  // K iterator for the LDS-DMA ring, whose K-steps are issued once each and in order from step 0: a lane's chunk
+  // carries its tap and channel from step to step (one add and a compare; the tap's pixel pointers are rebuilt
+  // only when the chunk crosses into the next tap, every Cin / 64 steps) instead of dividing them out of k per
+  // step (~35 VALU per chunk, which made these GEMMs 30-50 % slower than a dense GEMM of the same shape).  The
+  // addresses are exactly addr_k's.
+  struct It { const T* p1; const T* p2; int ci, tap, pix, iy0, ix0; bool ok, in; };
+  __device__ void it_tap(It& it) const {
+    const int ky = (it.tap * 11) >> 5, kx = it.tap - 3 * ky;  // tap / 3 for tap < 9
+    const int iy = it.iy0 + ky, ix = it.ix0 + kx;
+    it.in = it.ok && it.tap < 9 && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    const int pix = it.in ? it.pix + iy * W + ix : 0;
+    it.p1 = x1 + (size_t)pix * ld1;
+    it.p2 = x2 ? x2 + (size_t)pix * ld2 - c1 : it.p1;
+  }
+  __device__ It iter(const Row& r, int c) const {
+    It it{nullptr, nullptr, c * Elt<T>::EPC, 0, r.pix, r.iy0, r.ix0, r.ok && Cin > 0, false};
+    while (it.ok && it.ci >= Cin) { it.ci -= Cin; ++it.tap; }
+    it_tap(it);
+    return it;
+  }
+  // this step's chunk address, then the iterator moves one K-step on
+  __device__ const void* next(It& it) const {
+    const void* a = !it.in ? (const void*)g_tmae_zero_page
+                           : it.ci < c1 ? (const void*)(it.p1 + it.ci) : (const void*)(it.p2 + it.ci);
+    it.ci += 8 * Elt<T>::EPC;
+    if (it.ci >= Cin && it.ok) {
+      do { it.ci -= Cin; ++it.tap; } while (it.ci >= Cin);
+      it_tap(it);
+    }
+    return a;
+  }
 };
+
+template <class S, class = void> struct HasIter : std::false_type {};
+template <class S>
+struct HasIter<S, std::void_t<typename S::It>> : std::true_type {};
+template <class S, bool B> struct ItOf { using type = int; };
+template <class S> struct ItOf<S, true> { using type = typename S::It; };
 
 // Patch-embed gather over the KEPT patches (timm PatchEmbed conv16/s16 as a GEMM, MCM.py:615):
 // row m = (image b, kept rank k) reads patch ids_shuffle[b][k] of the f32 NCHW image; converts.
@@ -531,16 +568,40 @@ gemm_glds_kernel(WS ws, XS xs, EPI epi, int M, int N, int K, int n2) {
   for (int j = 0; j < XJ; ++j) xc[j] = pch ^ (((PR * j + lr) >> 1) & 7);
   typename WS::Row wrow[WJ];
   typename XS::Row xrow[XJ];
+  // token-side K iterators (sources with one, the implicit conv): issue() below runs once per K-step, in order
+  constexpr bool XIT = HasIter<XS>::value;
+  struct NoIt {};
+  using XIt = typename std::conditional<XIT, typename ItOf<XS, XIT>::type, NoIt>::type;
+  XIt xit[XJ];
   auto set_rows = [&](int tn, int tm) {
 #pragma unroll
     for (int j = 0; j < WJ; ++j) wrow[j] = ws.row(tn * BN + PR * j + lr);
 #pragma unroll
     for (int j = 0; j < XJ; ++j) xrow[j] = xs.row(tm * BM + PR * j + lr);
+    if constexpr (XIT)
+#pragma unroll
+      for (int j = 0; j < XJ; ++j) xit[j] = xs.iter(xrow[j], xc[j]);
   };
   const unsigned wave_u = __builtin_amdgcn_readfirstlane(tid >> 6);
   const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
   auto issue = [&](int stage, int kt) {
     const unsigned sb = lds_base + (unsigned)stage * ROWS * 128u;
+    if constexpr (XIT) {
+      if (kt * BKE + BKE <= K) {
+#pragma unroll
+        for (int j = 0; j < WJ; ++j)
+          glds16(src_addr_full(ws, wrow[j], kt, wc[j]), sb + (unsigned)(PR * j + 8 * wave_u) * 128u);
+      } else {
+#pragma unroll
+        for (int j = 0; j < WJ; ++j) glds16(ws.addr(wrow[j], kt, wc[j]), sb + (unsigned)(PR * j + 8 * wave_u) * 128u);
+      }
+#pragma unroll
+      for (int j = 0; j < XJ; ++j) {
+        const void* a = xs.next(xit[j]);  // every lane advances, including those of a partial round
+        if (!XPART || PR * j + 8 * (int)wave_u < BM) glds16(a, sb + (unsigned)(BN + PR * j + 8 * wave_u) * 128u);
+      }
+      return;
+    }
     if (kt * BKE + BKE <= K) {  // whole K-step: sources with addr_full skip the per-lane bounds select
 #pragma unroll
       for (int j = 0; j < WJ; ++j)
