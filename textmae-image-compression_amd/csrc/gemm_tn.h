@@ -73,7 +73,56 @@ template <typename T> struct KConvSrc {
     const size_t pix = (size_t)b * H * W + iy * W + ix;
     return ci < c1 ? (const void*)(x1 + pix * ld1 + ci) : (const void*)(x2 + pix * ld2 + (ci - c1));
   }
+  // K iterator for the LDS-DMA ring (k = output pixel, issued once per K-step and in order): a lane's column --
+  // its tap, channel and source map -- is fixed for the whole launch, and its pixel (b, oy, ox) moves by the
+  // K-step's pixel count without the two integer divisions addr() pays per piece per step (~60 VALU: the wgrad
+  // K loops were VALU-bound).  Same addresses as addr().
+  struct Step { int db, dy, dx; };
+  __device__ Step step(int dk) const {
+    const int hw = Ho * Wo, r = dk % hw;
+    return Step{dk / hw, r / Wo, r % Wo};
+  }
+  struct It { const T* base; int ldx, k, b, oy, ox, ky, kx; bool col; };
+  __device__ It iter(int k, int c) const {
+    It it;
+    it.col = c < cols;
+    const int cc = it.col ? c : 0;
+    const int tap = cc / Cin, ci = cc - tap * Cin;
+    it.ky = (tap * 11) >> 5;  // tap / 3
+    it.kx = tap - 3 * it.ky;
+    it.base = ci < c1 ? x1 + ci : x2 + (ci - c1);
+    it.ldx = ci < c1 ? ld1 : ld2;
+    it.k = k;
+    const int hw = Ho * Wo;
+    it.b = k / hw;
+    const int rem = k - it.b * hw;
+    it.oy = rem / Wo;
+    it.ox = rem - it.oy * Wo;
+    return it;
+  }
+  // this step's address (the zero page past k1, outside the map or past the columns), then one K-step on
+  __device__ const void* next(It& it, int k1, int dk, const Step& st) const {
+    const int iy = it.oy * stride - 1 + it.ky, ix = it.ox * stride - 1 + it.kx;
+    const bool ok = it.col && it.k < k1 && iy >= 0 && iy < H && ix >= 0 && ix < W;
+    const size_t pix = (size_t)it.b * H * W + iy * W + ix;
+    const void* a = ok ? (const void*)(it.base + pix * it.ldx) : (const void*)g_tmae_zero_page;
+    it.k += dk;
+    it.ox += st.dx;
+    if (it.ox >= Wo) { it.ox -= Wo; ++it.oy; }
+    it.oy += st.dy;
+    if (it.oy >= Ho) { it.oy -= Ho; ++it.b; }
+    it.b += st.db;
+    return a;
+  }
 };
+
+template <class S, class = void> struct HasKIter : std::false_type {};
+template <class S>
+struct HasKIter<S, std::void_t<typename S::It>> : std::true_type {};
+template <class S, bool B> struct KItOf { struct type {}; };
+template <class S> struct KItOf<S, true> { using type = typename S::It; };
+template <class S, bool B> struct KStepOf { struct type {}; };
+template <class S> struct KStepOf<S, true> { using type = typename S::Step; };
 
 // partial tile -> workspace slab of this split; bws (optional): the bias slab [split][M] of column sums
 struct EpiSplitWs {
@@ -176,9 +225,35 @@ gemm_tn_bf16_kernel(AS as, BS bs, EpiSplitWs epi, int M, int N, int K, int kchun
   const unsigned lds_base = (unsigned)(size_t)(lds_void_t*)lds;
   const float inv_ga = tn_inv_g(as), inv_gb = tn_inv_g(bs);
   const bool grp_a = tn_grouped(as, K), grp_b = tn_grouped(bs, K);  // wave-uniform
+  // N-side K iterators (the implicit im2col source): issue() below runs once per K-step, in order from step 0
+  constexpr bool BIT = HasKIter<BS>::value;
+  typename KItOf<BS, BIT>::type bit[WPN];
+  typename KStepOf<BS, BIT>::type bst{};
+  if constexpr (BIT) {
+    bst = bs.step(BK);
+#pragma unroll
+    for (int p = 0; p < WPN; ++p) bit[p] = bs.iter(k0 + nrow[p], ncol[p]);
+  }
   auto issue = [&](int stage, int kt) {
     const unsigned sb = lds_base + (unsigned)stage * STAGE;
     const int kb = k0 + kt * BK;
+    if constexpr (BIT) {
+      const bool full = kb + BK <= k1;
+#pragma unroll
+      for (int p = 0; p < WPN; ++p) glds16(bs.next(bit[p], k1, BK, bst), sb + (wave_u + NW * p) * 1024u);
+      if (full) {
+#pragma unroll
+        for (int p = 0; p < WPM; ++p)
+          glds16(tn_addr_in(as, kb + mrow[p], mcol[p], inv_ga, grp_a), sb + IMG_N + (wave_u + NW * p) * 1024u);
+      } else {
+#pragma unroll
+        for (int p = 0; p < WPM; ++p) {
+          const int k = kb + mrow[p];
+          glds16(k < k1 ? as.addr(k, mcol[p]) : (const void*)g_tmae_zero_page, sb + IMG_N + (wave_u + NW * p) * 1024u);
+        }
+      }
+      return;
+    }
     if (kb + BK <= k1) {  // whole K-step inside this split's range (wave-uniform): no per-row bounds select
 #pragma unroll
       for (int p = 0; p < WPN; ++p) glds16(tn_addr_in(bs, kb + nrow[p], ncol[p], inv_gb, grp_b), sb + (wave_u + NW * p) * 1024u);
