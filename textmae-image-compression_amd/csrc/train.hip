@@ -334,6 +334,38 @@ template <typename T> struct ConvTSrc {
     return addr_k(r, kt * 8 * Elt<T>::EPC + c * Elt<T>::EPC);
   }
   __device__ uint4 load(const Row& r, int kt, int c) const { return *reinterpret_cast<const uint4*>(addr(r, kt, c)); }
+  // K iterator for the LDS-DMA ring (as ConvSrc::It, gemm_core.h): a lane's chunk carries its tap and output
+  // channel from K-step to K-step; the tap's dy pointer is rebuilt only when the chunk crosses into the next tap.
+  // Same addresses as addr_k.
+  struct It { const T* p; int co, tap, b, iy, ix; bool ok, in; };
+  __device__ void it_tap(It& it) const {
+    const int ky = (it.tap * 11) >> 5;  // tap / 3 for tap < 9
+    int ty = it.iy + 1 - ky, tx = it.ix + 1 - (it.tap - 3 * ky);
+    bool in = it.ok && it.tap < 9 && ty >= 0 && tx >= 0;
+    if (stride == 2) {
+      in = in && !((ty | tx) & 1);
+      ty >>= 1;
+      tx >>= 1;
+    }
+    in = in && ty < Ho && tx < Wo;
+    it.in = in;
+    it.p = dy + ((size_t)(it.b * Ho + (in ? ty : 0)) * Wo + (in ? tx : 0)) * ldy;
+  }
+  __device__ It iter(const Row& r, int c) const {
+    It it{nullptr, c * Elt<T>::EPC, 0, r.b, r.iy, r.ix, r.ok && Cout > 0, false};
+    while (it.ok && it.co >= Cout) { it.co -= Cout; ++it.tap; }
+    it_tap(it);
+    return it;
+  }
+  __device__ const void* next(It& it) const {
+    const void* a = it.in ? (const void*)(it.p + it.co) : (const void*)g_tmae_zero_page;
+    it.co += 8 * Elt<T>::EPC;
+    if (it.co >= Cout && it.ok) {
+      do { it.co -= Cout; ++it.tap; } while (it.co >= Cout);
+      it_tap(it);
+    }
+    return a;
+  }
 };
 
 template <typename T>
