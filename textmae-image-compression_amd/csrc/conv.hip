@@ -123,6 +123,13 @@ static int conv_go(const char* nm, const tmae_conv_args& a, const T* W, int N, i
       return launch_conv_halo(nm, W, BStride{a.w_s1, a.w_s2}, hs, epi, N, a.n, a.nb1, a.nb2, st);
     }
   }
+  if constexpr (sizeof(T) == 2 && std::is_same<XS, ConvSrc<T>>::value) {
+    if (xs.Cin >= 128) {  // the K iterator source (gemm_core.h ConvSrcIt): wide inputs only
+      ConvSrcIt<T> xi;
+      static_cast<ConvSrc<T>&>(xi) = xs;
+      return launch_gemm<true, T>(nm, W, a.w_s1, a.w_s2, N, K, xi, epi, M, a.nb1, a.nb2, st);
+    }
+  }
   return launch_gemm<true, T>(nm, W, a.w_s1, a.w_s2, N, K, xs, epi, M, a.nb1, a.nb2, st);
 }
 

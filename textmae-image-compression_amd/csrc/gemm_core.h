@@ -131,6 +131,16 @@ template <typename T> struct ConvSrc {
     return (ci < c1) ? (const void*)(x1 + (size_t)pix * ld1 + ci) : (const void*)(x2 + (size_t)pix * ld2 + (ci - c1));
   }
   __device__ uint4 load(const Row& r, int kt, int c) const { return *reinterpret_cast<const uint4*>(addr(r, kt, c)); }
+};
+
+// ConvSrc with a K iterator for the LDS-DMA ring, whose K-steps are issued once each and in order from step 0.
+// tmae_conv3x3 picks it for bf16 inputs of >= 128 channels.  With 64 channels a chunk changes tap every K-step,
+// and the pointer rebuild costs more than addr_k's division: VGG's 64-channel layers ran 6 % slower with the
+// iterator.  A kernel that has both paths is slower on either, so they are separate instantiations.
+template <typename T> struct ConvSrcIt : ConvSrc<T> {
+  using ConvSrc<T>::x1; using ConvSrc<T>::x2; using ConvSrc<T>::c1; using ConvSrc<T>::ld1; using ConvSrc<T>::ld2;
+  using ConvSrc<T>::Cin; using ConvSrc<T>::H; using ConvSrc<T>::W;
+  using Row = typename ConvSrc<T>::Row;
   // K iterator for the LDS-DMA ring, whose K-steps are issued once each and in order from step 0: a lane's chunk
   // carries its tap and channel from step to step (one add and a compare; the tap's pixel pointers are rebuilt
   // only when the chunk crosses into the next tap, every Cin / 64 steps) instead of dividing them out of k per
