@@ -185,6 +185,31 @@ def test_conv3x3_two_segments(tmae, stride, dtype, H):
     check("rel:y_view_n_Ho_Ho_cout_permute_0_3_1_2", rel(y.view(n, Ho, Ho, cout).permute(0, 3, 1, 2), ref), tol(dtype))
 
 
+@pytest.mark.parametrize("cin,c2,H,stride,cout,ps", [(336, 0, 12, 2, 288, False), (288, 0, 6, 1, 240, False),
+                                                      (240, 0, 3, 1, 1152, True), (160, 32, 7, 2, 96, False),
+                                                      (136, 64, 6, 1, 64, True)])
+def test_conv3x3_wide_k_iterator(tmae, cin, c2, H, stride, cout, ps):
+    """bf16 implicit-GEMM convs of >= 128 input channels, which take the K-iterator source (gemm_core.h ConvSrcIt):
+    the hyperprior's strided / 6x6 / 3x3 shapes, a pixel-shuffle epilogue, and two input segments whose boundary
+    falls inside a 64-channel K-step (a chunk's tap and source change mid-sweep), against the fp32 conv2d"""
+    torch.manual_seed(cin + H + stride)
+    dt, n, c1 = torch.bfloat16, 4, cin - c2
+    xa, xb = torch.randn(n, c1, H, H), torch.randn(n, max(c2, 1), H, H)
+    w, b = torch.randn(cout, cin, 3, 3) / (9 * cin) ** 0.5, torch.randn(cout)
+    x = torch.cat([xa, xb[:, :c2]], 1) if c2 else xa
+    pre = F.conv2d(x.to(dt).float(), w.to(dt).float(), b, stride=stride, padding=1)
+    ref = F.gelu(F.pixel_shuffle(pre, 2) if ps else pre)
+    Ho = ref.shape[2]
+    cy = cout // 4 if ps else cout
+    y = torch.full((n * Ho * Ho, cy), float("nan"), device=DEV, dtype=dt)
+    extra = dict(x2=_nhwc(xb, dt), c2=c2, ld2=c2) if c2 else {}
+    tmae.ops.conv3x3(_nhwc(xa, dt), c1, c1, n, H, H, _wk(w, dt), b.to(DEV), y, cy, cout, dt, stride=stride, act=1,
+                     pixel_shuffle=ps, **extra)
+    torch.cuda.synchronize()
+    assert not torch.isnan(y.float()).any()
+    check(f"rel:wide_{cin}_{H}_{stride}_{ps}", rel(y.float().view(n, Ho, Ho, cy).permute(0, 3, 1, 2), ref), tol(dt))
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 def test_conv3x3_batched_addend(tmae, dtype):
     """nb1 x nb2 problems in one launch, per-problem weights/bias/addend/outputs, shared input"""
